@@ -1,0 +1,186 @@
+/*
+ * mswegnn.h -- C ABI of the MI355X (gfx950) multi-scale SWE-GNN rollout engine.
+ *
+ * Drop-in boundary for the hot path of sdat2/mSWE-GNN.  The reference
+ * has no FFI/plugin layer: its hot path sits behind the Python nn.Module API
+ *   MSGNN.forward(graph)   models/gnn.py:267-350
+ *   GNN.forward(graph)     models/gnn.py:102-152   (type_GNN='SWEGNN')
+ *   rollout_test(model,b)  training/train.py:67-95
+ * and the package's Python host side (mswe-gnn_amd/models/gnn.py, training/train.py)
+ * binds the entry points below through ctypes (mswe-gnn_amd/mswegnn/_lib.py); the binding
+ * a maintainer would add on the reference side is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - plain C types, no torch types; all float data is fp32, row-major.
+ *   - host pointers are read only during msw_plan_create (graph + weights are copied to
+ *     device memory the plan owns); device pointers passed to msw_forward / msw_rollout
+ *     are owned by the caller and must stay valid until the stream has executed the work.
+ *   - every function returns MSW_OK (0) or a negative MSW_ERR_* code and never aborts;
+ *     msw_last_error() returns a thread-local message for the last failure.
+ *   - a plan is bound to one device and is not re-entrant: one stream at a time.
+ *   - msw_forward / msw_rollout enqueue asynchronously on `stream` (a hipStream_t, NULL =
+ *     default stream) and never synchronise the host.
+ */
+#ifndef MSWEGNN_H
+#define MSWEGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSW_ABI_VERSION 1
+
+#define MSW_OK 0
+#define MSW_ERR_INVALID (-1)     /* bad argument / inconsistent graph or model description */
+#define MSW_ERR_HIP (-2)         /* HIP runtime error (allocation, launch, ...)           */
+#define MSW_ERR_UNSUPPORTED (-3) /* configuration outside what the engine implements      */
+
+/* Activation codes: activation_functions(), models/models.py:149-169. */
+enum msw_activation {
+  MSW_ACT_NONE = 0,
+  MSW_ACT_PRELU = 1, /* single learned slope (nn.PReLU() default num_parameters=1) */
+  MSW_ACT_RELU = 2,
+  MSW_ACT_LEAKYRELU = 3, /* slope 0.1 */
+  MSW_ACT_ELU = 4,
+  MSW_ACT_SWISH = 5, /* SiLU */
+  MSW_ACT_SIGMOID = 6,
+  MSW_ACT_TANH = 7
+};
+
+/* One nn.Linear followed by its activation (make_mlp, models/models.py:121-146:
+ * the activation follows EVERY layer, including the last). */
+typedef struct {
+  int32_t in_features;
+  int32_t out_features;
+  const float* weight; /* host [out_features][in_features] */
+  const float* bias;   /* host [out_features] or NULL (bias=False) */
+  int32_t act;         /* enum msw_activation */
+  float act_param;     /* PReLU slope */
+} msw_linear;
+
+#define MSW_MAX_MLP_LAYERS 4
+typedef struct {
+  int32_t n_layers;
+  msw_linear layer[MSW_MAX_MLP_LAYERS];
+} msw_mlp;
+
+/* One SWEGNN layer (models/gnn.py:352-445). */
+typedef struct {
+  int32_t K;                  /* hops */
+  int32_t normalize;          /* s_ij / ||s_ij||, NaN -> 0  (gnn.py:424-426) */
+  int32_t with_filter_matrix; /* filter_matrix[0..K] (gnn.py:381-384) */
+  int32_t with_gradient;      /* (out[col]-out[row]) * s  vs  s * out[row] (gnn.py:429-435) */
+  int32_t upwind_mode;        /* clamp negative gradients (gnn.py:431-432) */
+  int32_t edge_features;      /* width of edge_attr fed to this layer; 0 for intra_scale_gnn */
+  msw_mlp edge_mlp;           /* input 4F + edge_features -> 2F -> ... -> F */
+  const float* const* filter; /* K+1 host pointers to [F][F] (bias-free) or NULL */
+} msw_swegnn;
+
+/* Model description.  model_type 0 = MSGNN (models/gnn.py:154-350),
+ * 1 = GNN with type_GNN='SWEGNN' (models/gnn.py:13-152). */
+typedef struct {
+  int32_t model_type;
+  int32_t hid_features;      /* F: 16, 32 or 64 supported (F=16 runs zero-padded to 32) */
+  int32_t num_scales;        /* S (GNN: 1) */
+  int32_t previous_t;        /* p */
+  int32_t num_node_features; /* static + 2p */
+  int32_t with_WL;           /* append DEM + h_t to the static input (gnn.py:288-291) */
+  int32_t skip_connections;  /* MSGNN x_down skips (gnn.py:330-331) */
+  int32_t learned_pooling;   /* must be 0 (no shipped config uses it) */
+  int32_t gnn_act;           /* MSGNN: on x_up (gnn.py:335-336); GNN: after every layer */
+  float gnn_act_param;
+  /* residual: res_var = sum_tau residual_weights[tau][var] * x[:, dyn + 2 tau + var]
+   * (models/models.py:50-77 folded to a [p][2] matrix by the host; NULL = none) */
+  const float* residual_weights;
+  int32_t edge_mlp;      /* edge encoder present (gnn.py:203-206) */
+  msw_mlp edge_encoder;  /* raw edge features -> F */
+  msw_mlp static_encoder;
+  msw_mlp dynamic_encoder;
+  msw_mlp decoder; /* F -> ... -> 2 */
+  int32_t num_processors;        /* MSGNN: 2S-1 (down 0..S-2, coarsest, up); GNN: n_GNN_layers */
+  const msw_swegnn* processors;
+  int32_t num_unpool;            /* MSGNN: S-1 intra_scale_gnn; GNN: 0 */
+  const msw_swegnn* unpool;
+} msw_model_desc;
+
+/* Graph description in the reference's layout:
+ *   - nodes of graph g, scale s: [node_ptr[g*(S+1)+s], node_ptr[g*(S+1)+s+1])
+ *     (a single Data: num_graphs=1; a Batch after update_batch_multiscale, train.py:31-65)
+ *   - edge_index[0] = row (source j), edge_index[1] = col (target i); scale s edges are
+ *     [edge_ptr[s], edge_ptr[s+1]) (scale-major)
+ *   - intra_edge_index rows (coarse, fine), level l (coarse scale l+1, fine scale l) is
+ *     [intra_edge_ptr[l], intra_edge_ptr[l+1]). */
+typedef struct {
+  int64_t num_nodes;
+  int32_t num_scales;
+  int32_t num_graphs;
+  const int64_t* node_ptr; /* [num_graphs][num_scales+1] */
+  int64_t num_edges;
+  const int64_t* edge_index; /* [2][num_edges] */
+  const float* edge_attr;    /* [num_edges][num_edge_features] */
+  int32_t num_edge_features;
+  const int64_t* edge_ptr; /* [num_scales+1] */
+  int64_t num_intra_edges;
+  const int64_t* intra_edge_index; /* [2][num_intra_edges] */
+  const int64_t* intra_edge_ptr;   /* [num_scales] */
+} msw_graph_desc;
+
+typedef struct msw_plan msw_plan;
+
+/* Statistics for tests / benchmarks. */
+typedef struct {
+  int64_t num_nodes;
+  int64_t num_edges;
+  int32_t num_scales;
+  int32_t hid_features;
+  int32_t padded_features;
+  int32_t kernels_per_step;  /* launches one forward enqueues */
+  int64_t forward_calls;     /* forwards executed through the HIP path so far */
+  int64_t rollout_steps;     /* rollout steps executed through the HIP path so far */
+  int64_t device_bytes;      /* device memory owned by the plan */
+  int32_t graph_captured;    /* a hipGraph of one rollout step is instantiated */
+} msw_plan_stats;
+
+/* Build CSR-by-destination per scale, pooling/unpooling maps, pack the weights for
+ * the gfx950 kernels, allocate workspaces.  Host-synchronous; call once per graph. */
+int msw_plan_create(const msw_graph_desc* graph, const msw_model_desc* model, int device,
+                    msw_plan** out_plan);
+int msw_plan_destroy(msw_plan* plan);
+
+/* One forward (MSGNN.forward / GNN.forward): x [N][num_node_features] -> y [N][2].
+ * Does not modify x.  Equivalent to models/gnn.py:267-350 (MSGNN) or :102-152 (GNN). */
+int msw_forward(msw_plan* plan, const float* x, float* y, void* stream);
+
+/* Autoregressive rollout (rollout_test, training/train.py:67-95 with
+ * apply_boundary_condition / use_prediction, utils/dataset.py:486-529):
+ *   for t in 0..T-1: x[node_bc, dyn + (type_bc-1) + 2 tau] = bc[b][tau][t]
+ *                    pred = forward(x); x = shift(x, pred); out[:, :, t] = pred
+ * x0 [N][nnf] (device, not modified), bc [n_bc][p][T_bc] device with T_bc >= T,
+ * node_bc host int32 [n_bc] (node ids in the graph's numbering), out [N][2][T] device. */
+int msw_rollout(msw_plan* plan, const float* x0, const float* bc, int32_t bc_time_stride,
+                const int32_t* node_bc, int32_t n_bc, int32_t type_bc, int32_t T, float* out,
+                void* stream);
+
+/* Copy an internal per-node buffer ("x_s", "x_d", "x_down", "x_up") of the last forward
+ * into dst (device, [N][F], graph numbering).  Debug / parity localisation only. */
+int msw_debug_buffer(msw_plan* plan, const char* name, float* dst, void* stream);
+
+/* Enable (1) / disable (0) capturing one rollout step into a hipGraph (default 1). */
+int msw_set_graph_capture(msw_plan* plan, int enable);
+
+int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
+
+/* sizeof() of a descriptor struct ("msw_linear", "msw_mlp", "msw_swegnn",
+ * "msw_model_desc", "msw_graph_desc", "msw_plan_stats"); -1 if unknown.  Pure host code:
+ * lets FFI bindings verify their struct layouts without a GPU. */
+int64_t msw_struct_size(const char* name);
+const char* msw_last_error(void);
+int msw_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSWEGNN_H */

@@ -1,0 +1,306 @@
+"""Drop-in for the reference's ``models.gnn`` (sdat2/mSWE-GNN models/gnn.py).
+
+``GNN``, ``MSGNN`` and ``SWEGNN`` keep the reference's constructor signatures, attributes
+(``previous_t``, ``NUM_WATER_VARS``, ``out_dim``, ``type_model``, ``_create_scale_mask``),
+module tree and parameter names, and the seeded construction order, so checkpoints and
+callers (main.py, test_model.py, training/train.py) work unchanged.
+
+Execution paths of ``forward(graph)``:
+
+* **HIP engine** (the product hot path) -- input on a GPU and no autograd needed: the whole
+  forward runs as hand-written gfx950 kernels behind the C ABI (include/mswegnn.h) through
+  :mod:`mswegnn.engine`.  No PyTorch Geometric, no torch ops on the data path.  If the
+  native library is missing this raises; there is no silent fallback.
+* **autograd path** -- CPU tensors or gradients required (training, main.py): the same
+  mathematics as composite torch ops, so the module stays trainable.  It is not the
+  measured hot path.
+
+``engine`` ('auto' | 'hip' | 'torch') on a model instance forces a path.
+
+Reference: GNN models/gnn.py:13-152, MSGNN :154-350, SWEGNN :352-450.
+"""
+from typing import Optional
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from models.models import BaseFloodModel, make_mlp, activation_functions
+from utils.dataset import create_scale_mask
+
+
+def _engine_wanted(model, x: Tensor) -> bool:
+    mode = getattr(model, "engine", "auto")
+    if mode == "torch":
+        return False
+    if mode == "hip":
+        if not x.is_cuda:
+            raise RuntimeError("engine='hip' needs the graph on a GPU")
+        return True
+    needs_grad = torch.is_grad_enabled() and (
+        x.requires_grad or any(p.requires_grad for p in model.parameters()))
+    return x.is_cuda and not needs_grad
+
+
+class SWEGNN(nn.Module):
+    r"""Shallow-water-equation inspired message passing (models/gnn.py:352-450).
+
+    .. math::
+        \mathbf{x}^{\prime}_{di} = \mathbf{x}_{di} + \sum_{j \in \mathcal{N}(i)}
+        \mathbf{s}_{ij} \odot (\mathbf{x}_{di} - \mathbf{x}_{dj}),\quad
+        \mathbf{s}_{ij} = MLP(\mathbf{x}_{si}, \mathbf{x}_{sj}, \mathbf{x}_{di},
+        \mathbf{x}_{dj}, \mathbf{e}_{ij})
+
+    (the code subtracts ``out[row]`` from ``out[col]``, col being the receiving node).
+    """
+
+    def __init__(self, static_node_features: int, dynamic_node_features: int, edge_features: int,
+                 K: int = 2, normalize=True, with_filter_matrix=True, with_gradient=True,
+                 upwind_mode=False, device='cpu', **mlp_kwargs):
+        super().__init__()
+        self.edge_features = edge_features
+        self.edge_input_size = edge_features + 2 * static_node_features + 2 * dynamic_node_features
+        self.edge_output_size = dynamic_node_features
+        self.normalize = normalize
+        self.K = K
+        self.with_filter_matrix = with_filter_matrix
+        self.device = device
+        self.with_gradient = with_gradient
+        self.upwind_mode = upwind_mode
+        self.edge_mlp = make_mlp(self.edge_input_size, self.edge_output_size,
+                                 hidden_size=2 * self.edge_output_size, device=device, **mlp_kwargs)
+        if with_filter_matrix:
+            self.filter_matrix = nn.ModuleList([
+                nn.Linear(dynamic_node_features, dynamic_node_features, bias=False, device=device)
+                for _ in range(K + 1)])
+
+    def edge_weights(self, x_s, x_d, edge_index, edge_attr=None):
+        """s_ij for every edge (gnn.py:414-426).  The inputs do not change across the K
+        hops, so s_ij is computed once; hops mask inactive edges instead."""
+        row, col = edge_index[0], edge_index[1]
+        parts = [x_s[row], x_s[col], x_d[row], x_d[col]]
+        if self.edge_features > 0:
+            parts.append(edge_attr)
+        s = self.edge_mlp(torch.cat(parts, 1))
+        if self.normalize:
+            s = s / torch.linalg.vector_norm(s, dim=1, keepdim=True)
+            s = s.masked_fill(torch.isnan(s), 0)
+        return s
+
+    def forward(self, x_s: Tensor, x_d: Tensor, edge_index: Tensor,
+                edge_attr: Optional[Tensor] = None) -> Tensor:
+        row, col = edge_index[0], edge_index[1]
+        out = self.filter_matrix[0](x_d) if self.with_filter_matrix else x_d.clone()
+        s = self.edge_weights(x_s, x_d, edge_index, edge_attr)
+        for k in range(self.K):
+            nz = out.sum(1) != 0                      # active-edge predicate (gnn.py:408-411)
+            active = (nz[row] | nz[col]).unsqueeze(1)
+            if self.with_gradient:
+                g = out[col] - out[row]
+                if self.upwind_mode:
+                    g = g.clamp(min=0)
+                msg = g * s
+            else:
+                msg = s * out[row]
+            msg = torch.where(active, msg, torch.zeros_like(msg))
+            agg = torch.zeros_like(out).index_add_(0, col, msg)
+            if self.with_filter_matrix:
+                agg = self.filter_matrix[k + 1](agg)
+            out = out + agg
+        return out
+
+    def __repr__(self):
+        return '{}(node_features={}, edge_features={}, K={}, with_filter_matrix={}, with_gradient={})'.format(
+            self.__class__.__name__, self.edge_output_size, self.edge_features, self.K,
+            self.with_filter_matrix, self.with_gradient)
+
+
+class _EngineMixin:
+    """Binds a model to the HIP engine (one cached plan per graph topology + weights)."""
+
+    engine = "auto"
+
+    def _engine_for(self, graph):
+        from mswegnn.engine import plan_for
+        return plan_for(self, graph)
+
+    def rollout(self, graph, steps: Optional[int] = None):
+        """Fused autoregressive rollout on the GPU (rollout_test semantics,
+        training/train.py:67-95) -> [N, 2, T]."""
+        from mswegnn.engine import plan_for
+        T = graph.y.shape[-1] if steps is None else steps
+        return plan_for(self, graph).rollout(graph.x, graph.BC, graph.node_BC, graph.type_BC, T)
+
+
+class GNN(_EngineMixin, BaseFloodModel):
+    """Single-scale encoder-processor-decoder (models/gnn.py:13-152)."""
+
+    def __init__(self, num_node_features, num_edge_features, hid_features=32, K=2, n_GNN_layers=2,
+                 type_GNN="SWEGNN", mlp_layers=1, mlp_activation='prelu', gnn_activation='prelu',
+                 dropout=0, with_WL=True, normalize=True, with_filter_matrix=True, edge_mlp=True,
+                 with_gradient=True, **base_model_kwargs):
+        super().__init__(**base_model_kwargs)
+        if type_GNN != "SWEGNN":
+            raise NotImplementedError(
+                f"type_GNN={type_GNN!r} (PyG ChebConv/TAGConv/GATConv) is outside the MI355X hot "
+                "path; no shipped config or checkpoint uses it")
+        self.type_model = "GNN"
+        self.hid_features = hid_features
+        self.num_node_features = num_node_features
+        self.num_edge_features = num_edge_features
+        self.type_GNN = type_GNN
+        self.edge_mlp = edge_mlp
+        self.with_WL = with_WL
+        self.dropout = dropout
+        self.mlp_layers = mlp_layers
+        self.dynamic_node_features = self.previous_t * self.out_dim
+        self.static_node_features = num_node_features - self.dynamic_node_features + self.with_WL
+        if edge_mlp:
+            self.num_edge_features = hid_features
+            self.edge_encoder = make_mlp(num_edge_features, hid_features, hid_features,
+                                         n_layers=mlp_layers, bias=True,
+                                         activation=mlp_activation, device=self.device)
+        self.dynamic_node_encoder = make_mlp(self.dynamic_node_features, hid_features, hid_features,
+                                             n_layers=mlp_layers, activation=mlp_activation,
+                                             device=self.device)
+        self.static_node_encoder = make_mlp(self.static_node_features, hid_features, hid_features,
+                                            n_layers=2, bias=True, activation=mlp_activation,
+                                            device=self.device)
+        self.gnn_processor = nn.ModuleList([
+            SWEGNN(hid_features, hid_features, self.num_edge_features, K=K, device=self.device,
+                   n_layers=mlp_layers, activation=mlp_activation, bias=True, normalize=normalize,
+                   with_filter_matrix=with_filter_matrix, with_gradient=with_gradient)
+            for _ in range(n_GNN_layers)])
+        self.gnn_activation = activation_functions(gnn_activation, device=self.device)
+        self.node_decoder = make_mlp(hid_features, self.out_dim, hid_features, n_layers=mlp_layers,
+                                     dropout=dropout, activation=mlp_activation, device=self.device)
+
+    def _split_inputs(self, x):
+        nst = self.static_node_features - self.with_WL
+        x_s, x_d = x[:, :nst], x[:, nst:]
+        if self.with_WL:
+            x_s = torch.cat((x_s, (x_s[:, -1] + x_d[:, -self.out_dim]).unsqueeze(-1)), 1)
+        return x_s, x_d
+
+    def forward(self, graph):
+        if _engine_wanted(self, graph.x):
+            return self._engine_for(graph).forward(graph.x)
+        x = graph.x.clone()
+        edge_attr = self.edge_encoder(graph.edge_attr) if self.edge_mlp else graph.edge_attr
+        x_s, x_d = self._split_inputs(x)
+        x_s = self.static_node_encoder(x_s)
+        h = x_d = self.dynamic_node_encoder(x_d)
+        for conv in self.gnn_processor:
+            h = conv(x_s, x_d, graph.edge_index, edge_attr)
+            if self.gnn_activation is not None:
+                h = self.gnn_activation(h)
+            x_d = h
+        h = self.node_decoder(h) + self._add_residual_connection(x)
+        return self._mask_small_WD(torch.relu(h), epsilon=0.0001)
+
+
+class MSGNN(_EngineMixin, BaseFloodModel):
+    """Multi-scale encoder-processor-decoder (models/gnn.py:154-350): a SWEGNN per scale on
+    the way down (fine -> coarse, mean pooling) and up (coarse -> fine, learned unpooling
+    by an intra-scale SWEGNN plus skip connections)."""
+
+    def __init__(self, num_node_features, num_edge_features, num_scales, hid_features=32, K=2,
+                 mlp_layers=2, mlp_activation='prelu', gnn_activation='tanh',
+                 learned_pooling=False, skip_connections=True,
+                 with_WL=False, normalize=True, with_filter_matrix=True, edge_mlp=True,
+                 with_gradient=True, **base_model_kwargs):
+        super().__init__(**base_model_kwargs)
+        self.type_model = "MSGNN"
+        self.hid_features = hid_features
+        self.num_node_features = num_node_features
+        self.edge_mlp = edge_mlp
+        self.with_WL = with_WL
+        self.num_scales = num_scales
+        self.mlp_layers = mlp_layers
+        self.dynamic_node_features = self.previous_t * self.NUM_WATER_VARS
+        self.static_node_features = num_node_features - self.dynamic_node_features + self.with_WL
+        self.learned_pooling = learned_pooling
+        self.skip_connections = skip_connections
+        Ks = [K] * num_scales if isinstance(K, int) else list(K)
+        self.K = Ks + Ks[::-1][1:]
+        assert len(self.K) == num_scales * 2 - 1, \
+            "K must be an int or a list of length num_scales or num_scales*2-1"
+        if edge_mlp:
+            self.edge_encoder = make_mlp(num_edge_features, hid_features, hid_features,
+                                         n_layers=mlp_layers, bias=True, activation=mlp_activation,
+                                         device=self.device)
+            num_edge_features = hid_features
+        self.num_edge_features = num_edge_features
+        self.dynamic_node_encoder = make_mlp(self.dynamic_node_features, hid_features, hid_features,
+                                             n_layers=mlp_layers, activation=mlp_activation,
+                                             device=self.device)
+        self.static_node_encoder = make_mlp(self.static_node_features, hid_features, hid_features,
+                                            n_layers=mlp_layers, bias=True,
+                                            activation=mlp_activation, device=self.device)
+        self.intra_scale_gnn = nn.ModuleList([
+            SWEGNN(hid_features, hid_features, 0, K=1, n_layers=mlp_layers, activation=mlp_activation,
+                   bias=True, normalize=True, with_filter_matrix=False, with_gradient=False,
+                   device=self.device) for _ in range(num_scales - 1)])
+        if learned_pooling:
+            self.pooling_mlp = make_mlp(hid_features * 2, hid_features, hid_features,
+                                        n_layers=mlp_layers, activation=mlp_activation,
+                                        device=self.device)
+        self.gnn_processor = nn.ModuleList([
+            SWEGNN(hid_features, hid_features, num_edge_features, K=k, n_layers=mlp_layers,
+                   activation=mlp_activation, bias=True, normalize=normalize,
+                   with_filter_matrix=with_filter_matrix, with_gradient=with_gradient)
+            for k in self.K])
+        self.gnn_activation = activation_functions(gnn_activation, device=self.device)
+        self.node_decoder = make_mlp(hid_features, self.out_dim, hid_features, n_layers=mlp_layers,
+                                     dropout=0, activation=mlp_activation, device=self.device)
+
+    def _create_scale_mask(self, data):
+        """Scale id per node, e.g. [0, 0, 0, 1, 1, 2, ...] (gnn.py:259-265)."""
+        return create_scale_mask(data.x.size(0), self.num_scales, data.node_ptr, data,
+                                 device=data.x.device)
+
+    def _pooling(self, x, row_fine, col_coarse, reduce='mean', learnable=False):
+        """Mean of the children of every coarse node; rows without children -> 0."""
+        src = self.pooling_mlp(torch.cat((x[row_fine], x[col_coarse]), -1)) if learnable else x[row_fine]
+        out = torch.zeros_like(x).index_add_(0, col_coarse, src)
+        if reduce == 'mean':
+            cnt = torch.zeros(x.shape[0], dtype=x.dtype, device=x.device).index_add_(
+                0, col_coarse, torch.ones_like(col_coarse, dtype=x.dtype))
+            out = out / cnt.clamp(min=1).unsqueeze(1)
+        return out
+
+    def forward(self, graph):
+        if _engine_wanted(self, graph.x):
+            return self._engine_for(graph).forward(graph.x)
+        S = self.num_scales
+        x = graph.x.clone()
+        ei, ep = graph.edge_index, graph.edge_ptr
+        iei, iep = graph.intra_mesh_edge_index, graph.intra_edge_ptr
+        scale = self._create_scale_mask(graph)
+        edge_attr = self.edge_encoder(graph.edge_attr) if self.edge_mlp else graph.edge_attr
+        nst = self.static_node_features - self.with_WL
+        x_s, x_d = x[:, :nst], x[:, nst:]
+        if self.with_WL:
+            x_s = torch.cat((x_s, (x_s[:, -1] + x_d[:, -self.out_dim]).unsqueeze(-1)), 1)
+        x_s = self.static_node_encoder(x_s)
+        x_d = self.dynamic_node_encoder(x_d)
+        x_down = torch.zeros_like(x_d)
+        x_up = torch.zeros_like(x_d)
+        sel = lambda i: (scale == i).unsqueeze(1).to(x_d.dtype)  # noqa: E731
+        for i in range(S - 1):                                  # fine -> coarse
+            x_d = self.gnn_processor[i](x_s, x_d, ei[:, ep[i]:ep[i + 1]], edge_attr[ep[i]:ep[i + 1]])
+            x_down = x_down + x_d * sel(i)
+            coarse, fine = iei[:, iep[i]:iep[i + 1]]
+            x_d = self._pooling(x_d, fine, coarse, 'mean', self.learned_pooling)
+        x_down = x_down + x_d
+        for i in range(S):                                      # coarse -> fine
+            s = S - 1 - i
+            x_d = self.gnn_processor[S - 1 + i](x_s, x_d, ei[:, ep[s]:ep[s + 1]], edge_attr[ep[s]:ep[s + 1]])
+            x_up = x_up + x_d * sel(s)
+            if i < S - 1:
+                x_d = self.intra_scale_gnn[i](x_s, x_d, iei[:, iep[s - 1]:iep[s]])
+                if self.skip_connections:
+                    x_d = x_d + x_down * sel(s - 1)
+        h = x_up if self.gnn_activation is None else self.gnn_activation(x_up)
+        h = self.node_decoder(h) + self._add_residual_connection(x)
+        return self._mask_small_WD(torch.relu(h), epsilon=0.0001)

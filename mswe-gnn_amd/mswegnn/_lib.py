@@ -1,0 +1,118 @@
+"""ctypes binding of the C ABI in include/mswegnn.h (libmswegnn.so, gfx950).
+
+The shared library is built in-tree (mswe-gnn_amd/lib/libmswegnn.so) by
+``python mswe-gnn_amd/build.py`` / ``__graft_entry__.build()``.  There is no fallback:
+if the library is missing, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmswegnn.so")
+
+MSW_OK = 0
+MAX_MLP_LAYERS = 4
+
+ACT = {None: 0, "prelu": 1, "relu": 2, "leakyrelu": 3, "elu": 4, "swish": 5, "sigmoid": 6,
+       "tanh": 7}
+
+c_float_p = C.POINTER(C.c_float)
+c_int64_p = C.POINTER(C.c_int64)
+c_int32_p = C.POINTER(C.c_int32)
+
+
+class MswLinear(C.Structure):
+    _fields_ = [("in_features", C.c_int32), ("out_features", C.c_int32),
+                ("weight", c_float_p), ("bias", c_float_p),
+                ("act", C.c_int32), ("act_param", C.c_float)]
+
+
+class MswMlp(C.Structure):
+    _fields_ = [("n_layers", C.c_int32), ("layer", MswLinear * MAX_MLP_LAYERS)]
+
+
+class MswSwegnn(C.Structure):
+    _fields_ = [("K", C.c_int32), ("normalize", C.c_int32), ("with_filter_matrix", C.c_int32),
+                ("with_gradient", C.c_int32), ("upwind_mode", C.c_int32),
+                ("edge_features", C.c_int32), ("edge_mlp", MswMlp),
+                ("filter", C.POINTER(c_float_p))]
+
+
+class MswModelDesc(C.Structure):
+    _fields_ = [("model_type", C.c_int32), ("hid_features", C.c_int32),
+                ("num_scales", C.c_int32), ("previous_t", C.c_int32),
+                ("num_node_features", C.c_int32), ("with_WL", C.c_int32),
+                ("skip_connections", C.c_int32), ("learned_pooling", C.c_int32),
+                ("gnn_act", C.c_int32), ("gnn_act_param", C.c_float),
+                ("residual_weights", c_float_p), ("edge_mlp", C.c_int32),
+                ("edge_encoder", MswMlp), ("static_encoder", MswMlp),
+                ("dynamic_encoder", MswMlp), ("decoder", MswMlp),
+                ("num_processors", C.c_int32), ("processors", C.POINTER(MswSwegnn)),
+                ("num_unpool", C.c_int32), ("unpool", C.POINTER(MswSwegnn))]
+
+
+class MswGraphDesc(C.Structure):
+    _fields_ = [("num_nodes", C.c_int64), ("num_scales", C.c_int32), ("num_graphs", C.c_int32),
+                ("node_ptr", c_int64_p), ("num_edges", C.c_int64), ("edge_index", c_int64_p),
+                ("edge_attr", c_float_p), ("num_edge_features", C.c_int32),
+                ("edge_ptr", c_int64_p), ("num_intra_edges", C.c_int64),
+                ("intra_edge_index", c_int64_p), ("intra_edge_ptr", c_int64_p)]
+
+
+class MswPlanStats(C.Structure):
+    _fields_ = [("num_nodes", C.c_int64), ("num_edges", C.c_int64), ("num_scales", C.c_int32),
+                ("hid_features", C.c_int32), ("padded_features", C.c_int32),
+                ("kernels_per_step", C.c_int32), ("forward_calls", C.c_int64),
+                ("rollout_steps", C.c_int64), ("device_bytes", C.c_int64),
+                ("graph_captured", C.c_int32)]
+
+
+# (name, restype, argtypes) of every entry point declared in include/mswegnn.h
+SYMBOLS = [
+    ("msw_plan_create", C.c_int, [C.POINTER(MswGraphDesc), C.POINTER(MswModelDesc), C.c_int,
+                                  C.POINTER(C.c_void_p)]),
+    ("msw_plan_destroy", C.c_int, [C.c_void_p]),
+    ("msw_forward", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("msw_rollout", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, c_int32_p, C.c_int32,
+                              C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    ("msw_debug_buffer", C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_void_p]),
+    ("msw_set_graph_capture", C.c_int, [C.c_void_p, C.c_int]),
+    ("msw_plan_get_stats", C.c_int, [C.c_void_p, C.POINTER(MswPlanStats)]),
+    ("msw_last_error", C.c_char_p, []),
+    ("msw_abi_version", C.c_int, []),
+    ("msw_struct_size", C.c_int64, [C.c_char_p]),
+]
+
+STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,
+           "msw_model_desc": MswModelDesc, "msw_graph_desc": MswGraphDesc,
+           "msw_plan_stats": MswPlanStats}
+
+_lib = None
+
+
+def lib():
+    """Load libmswegnn.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"mSWE-GNN HIP engine not built: {LIB_PATH} is missing "
+                "(run `python mswe-gnn_amd/build.py` or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SYMBOLS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.msw_abi_version() != 1:
+            raise RuntimeError("libmswegnn.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != MSW_OK:
+        msg = lib().msw_last_error().decode(errors="replace")
+        raise RuntimeError(f"mswegnn error {rc}: {msg}")
+    return rc

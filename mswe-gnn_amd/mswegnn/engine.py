@@ -1,0 +1,291 @@
+"""Host side of the HIP engine: model/graph descriptors -> msw_plan, forward and rollout.
+
+This is the Python mirror of the reference's operator interface for the hot path
+(``MSGNN.forward`` / ``GNN.forward``, models/gnn.py:102-152, 267-350, and ``rollout_test``,
+training/train.py:67-95).  All numerical work runs in libmswegnn.so (gfx950 kernels);
+this module only describes the model and the graph to it, and passes device pointers of
+torch tensors plus the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+
+__all__ = ["EnginePlan", "plan_for", "describe_model"]
+
+
+# ------------------------------------------------------------------ model description
+def _f32(keep, t):
+    a = np.ascontiguousarray(t.detach().to("cpu", torch.float32).numpy())
+    keep.append(a)
+    return a.ctypes.data_as(L.c_float_p)
+
+
+def _act_of(mod):
+    """(code, param) of an activation module."""
+    if mod is None:
+        return 0, 0.0
+    if isinstance(mod, nn.PReLU):
+        if mod.weight.numel() != 1:
+            raise NotImplementedError("PReLU with more than one parameter")
+        return L.ACT["prelu"], float(mod.weight.detach().reshape(-1)[0])
+    for name, cls in (("relu", nn.ReLU), ("elu", nn.ELU), ("swish", nn.SiLU),
+                      ("sigmoid", nn.Sigmoid), ("tanh", nn.Tanh)):
+        if isinstance(mod, cls):
+            return L.ACT[name], 0.0
+    if isinstance(mod, nn.LeakyReLU):
+        if abs(mod.negative_slope - 0.1) > 1e-12:
+            raise NotImplementedError("LeakyReLU slope other than 0.1")
+        return L.ACT["leakyrelu"], 0.0
+    raise NotImplementedError(f"activation {type(mod).__name__}")
+
+
+def _mlp(keep, seq):
+    """make_mlp Sequential -> MswMlp (Linear, [Dropout (eval: identity)], activation)."""
+    layers = []
+    for m in seq:
+        if isinstance(m, nn.Linear):
+            layers.append([m, None])
+        elif isinstance(m, nn.Dropout):
+            continue
+        elif isinstance(m, nn.LayerNorm):
+            raise NotImplementedError("layer_norm MLPs are not used by any shipped config")
+        else:
+            layers[-1][1] = m
+    if not 1 <= len(layers) <= L.MAX_MLP_LAYERS:
+        raise NotImplementedError(f"MLP with {len(layers)} layers")
+    d = L.MswMlp()
+    d.n_layers = len(layers)
+    for i, (lin, act) in enumerate(layers):
+        e = d.layer[i]
+        e.in_features, e.out_features = lin.in_features, lin.out_features
+        e.weight = _f32(keep, lin.weight)
+        e.bias = _f32(keep, lin.bias) if lin.bias is not None else None
+        e.act, e.act_param = _act_of(act)
+    return d
+
+
+def _swegnn(keep, g):
+    d = L.MswSwegnn()
+    d.K = g.K
+    d.normalize = int(bool(g.normalize))
+    d.with_filter_matrix = int(bool(g.with_filter_matrix))
+    d.with_gradient = int(bool(g.with_gradient))
+    d.upwind_mode = int(bool(g.upwind_mode))
+    d.edge_features = g.edge_features
+    d.edge_mlp = _mlp(keep, g.edge_mlp)
+    if g.with_filter_matrix:
+        arr = (L.c_float_p * (g.K + 1))(*[_f32(keep, f.weight) for f in g.filter_matrix])
+        keep.append(arr)
+        d.filter = C.cast(arr, C.POINTER(L.c_float_p))
+    else:
+        d.filter = None
+    return d
+
+
+def describe_model(model):
+    """nn.Module (our models.gnn.GNN / MSGNN) -> (MswModelDesc, keepalive list)."""
+    keep = []
+    d = L.MswModelDesc()
+    is_ms = model.type_model == "MSGNN"
+    d.model_type = 0 if is_ms else 1
+    d.hid_features = model.hid_features
+    d.num_scales = model.num_scales if is_ms else 1
+    d.previous_t = model.previous_t
+    d.num_node_features = model.num_node_features
+    d.with_WL = int(bool(model.with_WL))
+    d.skip_connections = int(bool(getattr(model, "skip_connections", False)))
+    d.learned_pooling = int(bool(getattr(model, "learned_pooling", False)))
+    d.gnn_act, d.gnn_act_param = _act_of(model.gnn_activation)
+    M = model._residual_matrix()
+    d.residual_weights = _f32(keep, M) if M is not None else None
+    d.edge_mlp = int(bool(model.edge_mlp))
+    if model.edge_mlp:
+        d.edge_encoder = _mlp(keep, model.edge_encoder)
+    d.static_encoder = _mlp(keep, model.static_node_encoder)
+    d.dynamic_encoder = _mlp(keep, model.dynamic_node_encoder)
+    d.decoder = _mlp(keep, model.node_decoder)
+    procs = (L.MswSwegnn * len(model.gnn_processor))(*[_swegnn(keep, g) for g in model.gnn_processor])
+    keep.append(procs)
+    d.num_processors = len(model.gnn_processor)
+    d.processors = C.cast(procs, C.POINTER(L.MswSwegnn))
+    if is_ms and len(model.intra_scale_gnn):
+        ups = (L.MswSwegnn * len(model.intra_scale_gnn))(*[_swegnn(keep, g) for g in model.intra_scale_gnn])
+        keep.append(ups)
+        d.num_unpool = len(model.intra_scale_gnn)
+        d.unpool = C.cast(ups, C.POINTER(L.MswSwegnn))
+    else:
+        d.num_unpool = 0
+        d.unpool = None
+    return d, keep
+
+
+# ------------------------------------------------------------------ graph description
+def _i64(keep, t):
+    a = np.ascontiguousarray(t.detach().to("cpu", torch.int64).numpy())
+    keep.append(a)
+    return a.ctypes.data_as(L.c_int64_p)
+
+
+def describe_graph(model, graph):
+    keep = []
+    g = L.MswGraphDesc()
+    N = int(graph.x.shape[0])
+    E = int(graph.edge_index.shape[1])
+    g.num_nodes = N
+    g.num_edges = E
+    g.edge_index = _i64(keep, graph.edge_index.reshape(2, E))
+    ea = graph.edge_attr
+    if ea.dim() == 1:
+        ea = ea.unsqueeze(1)
+    g.num_edge_features = int(ea.shape[1])
+    g.edge_attr = _f32(keep, ea)
+    if model.type_model == "MSGNN":
+        S = model.num_scales
+        node_ptr = graph.node_ptr
+        if node_ptr.dim() == 1:
+            node_ptr = node_ptr.reshape(1, -1)
+        g.num_scales = S
+        g.num_graphs = int(node_ptr.shape[0])
+        g.node_ptr = _i64(keep, node_ptr)
+        g.edge_ptr = _i64(keep, graph.edge_ptr.reshape(-1))
+        iei = graph.intra_mesh_edge_index
+        g.num_intra_edges = int(iei.shape[1])
+        g.intra_edge_index = _i64(keep, iei)
+        g.intra_edge_ptr = _i64(keep, graph.intra_edge_ptr.reshape(-1))
+    else:
+        g.num_scales = 1
+        g.num_graphs = 1
+        g.node_ptr = _i64(keep, torch.tensor([0, N]))
+        g.edge_ptr = _i64(keep, torch.tensor([0, E]))
+        g.num_intra_edges = 0
+        g.intra_edge_index = None
+        g.intra_edge_ptr = None
+    return g, keep
+
+
+# ------------------------------------------------------------------ plan
+class EnginePlan:
+    """An msw_plan: the graph (CSR per scale, pooling maps) and packed weights on one GPU."""
+
+    def __init__(self, model, graph, device):
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("the HIP engine needs a GPU device")
+        self.num_nodes = int(graph.x.shape[0])
+        self.nnf = int(graph.x.shape[1])
+        md, k1 = describe_model(model)
+        gd, k2 = describe_graph(model, graph)
+        h = C.c_void_p()
+        lib = L.lib()
+        L.check(lib.msw_plan_create(C.byref(gd), C.byref(md), self.device.index or 0, C.byref(h)))
+        self._h = h
+        del k1, k2
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            L.lib().msw_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _x(self, x):
+        if x.device != self.device or x.dtype != torch.float32:
+            x = x.to(self.device, torch.float32)
+        if x.shape != (self.num_nodes, self.nnf):
+            raise ValueError(f"x has shape {tuple(x.shape)}, plan expects {(self.num_nodes, self.nnf)}")
+        return x.contiguous()
+
+    def forward(self, x):
+        """MSGNN.forward / GNN.forward on the GPU: x [N, nnf] -> y [N, 2]."""
+        x = self._x(x)
+        y = torch.empty(self.num_nodes, 2, device=self.device, dtype=torch.float32)
+        L.check(L.lib().msw_forward(self._h, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                                    self._stream()))
+        return y
+
+    def rollout(self, x0, BC, node_BC, type_BC, T, out=None):
+        """rollout_test on the GPU -> [N, 2, T] (training/train.py:67-95)."""
+        x0 = self._x(x0)
+        T = int(T)
+        if out is None:
+            out = torch.empty(self.num_nodes, 2, T, device=self.device, dtype=torch.float32)
+        nbc = np.ascontiguousarray(torch.as_tensor(node_BC).detach().to("cpu", torch.int32).reshape(-1).numpy())
+        bc = None
+        tstride = 0
+        if nbc.size:
+            bc = BC.to(self.device, torch.float32).contiguous()
+            if bc.dim() != 3 or bc.shape[0] != nbc.size:
+                raise ValueError("BC must be [n_BC, previous_t, T+1]")
+            tstride = int(bc.shape[-1])
+        tb = int(torch.as_tensor(type_BC).reshape(-1)[0])
+        L.check(L.lib().msw_rollout(self._h, C.c_void_p(x0.data_ptr()),
+                                    C.c_void_p(bc.data_ptr() if bc is not None else 0), tstride,
+                                    nbc.ctypes.data_as(L.c_int32_p), int(nbc.size), tb, T,
+                                    C.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def debug_buffer(self, name, F):
+        dst = torch.empty(self.num_nodes, F, device=self.device)
+        L.check(L.lib().msw_debug_buffer(self._h, name.encode(), C.c_void_p(dst.data_ptr()),
+                                         self._stream()))
+        return dst
+
+    def set_graph_capture(self, enable):
+        L.check(L.lib().msw_set_graph_capture(self._h, int(bool(enable))))
+
+    def stats(self):
+        s = L.MswPlanStats()
+        L.check(L.lib().msw_plan_get_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in L.MswPlanStats._fields_}
+
+
+# ------------------------------------------------------------------ cache
+def _graph_key(model, graph):
+    names = ["x", "edge_index", "edge_attr"]
+    if model.type_model == "MSGNN":
+        names += ["node_ptr", "edge_ptr", "intra_mesh_edge_index", "intra_edge_ptr"]
+    key = []
+    for n in names:
+        t = getattr(graph, n)
+        key.append((n, t.data_ptr() if n != "x" else 0, tuple(t.shape), t.device.type,
+                    t._version if n != "x" else 0))
+    key.append(("dev", str(graph.x.device)))
+    return tuple(key)
+
+
+def _weights_key(model):
+    return tuple((p.data_ptr(), p._version) for p in model.parameters())
+
+
+_plans = weakref.WeakKeyDictionary()
+
+
+def plan_for(model, graph):
+    """Cached EnginePlan for (model weights, graph topology)."""
+    per_model = _plans.setdefault(model, {})
+    gk, wk = _graph_key(model, graph), _weights_key(model)
+    ent = per_model.get(gk)
+    if ent is not None and ent[0] == wk:
+        return ent[1]
+    if ent is not None:
+        ent[1].close()
+    if len(per_model) >= 8:  # bound the cache
+        for k in list(per_model)[:4]:
+            per_model.pop(k)[1].close()
+    plan = EnginePlan(model, graph, graph.x.device)
+    per_model[gk] = (wk, plan)
+    return plan

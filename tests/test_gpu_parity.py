@@ -1,0 +1,203 @@
+"""HIP engine (through the C ABI) vs the reference's outputs.
+
+Every test here runs the gfx950 kernels via libmswegnn.so -- ``engine='hip'`` forces the
+native path and the plan statistics prove it ran.  References are the golden fixtures made
+by the reference itself (oracle/gen_golden.py) or, for configurations without a fixture,
+the oracle (bit-identical to the reference on CPU, pinned by test_oracle_golden.py).
+Tolerance: max|ours - ref| / max|ref| <= 1e-4 at every step (BASELINE.json north star).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import (REL_TOL, build_gnn, build_msgnn, golden, manifest, per_step_rel, rel_err,
+                      state_dict_of, weights)
+import msgnn_torch as orc
+from mswegnn.mesh import make_multiscale_mesh, make_single_scale_mesh, wet_state, mesh_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip(model, dev):
+    model = model.to(dev)
+    model.engine = "hip"
+    return model
+
+
+def _stats(model, g):
+    from mswegnn.engine import plan_for
+    return plan_for(model, g).stats()
+
+
+@pytest.mark.parametrize("ck,K,F", [("K4_F32", 4, 32), ("K2_F16", 2, 16)])
+def test_single_step_vs_reference(cuda, ck, K, F):
+    fx = golden(f"fx_tiny_{ck}_step")
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=48), seed=1).to(cuda)
+    m = _hip(build_msgnn(4, F, K, state=weights(ck)), cuda)
+    with torch.no_grad():
+        y = m(g)
+    torch.cuda.synchronize()
+    assert _stats(m, g)["forward_calls"] >= 1
+    # intermediates of the reference (forward hooks) localise any mismatch
+    from mswegnn.engine import plan_for
+    plan = plan_for(m, g)
+    xs = plan.debug_buffer("x_s", F).cpu()
+    xd = plan.debug_buffer("x_d", F).cpu()
+    n0 = int(g.node_ptr[1])
+    assert rel_err(xs, fx["mid__static_node_encoder"]) <= REL_TOL
+    assert rel_err(xd[:n0], fx["mid__dynamic_node_encoder"][:n0]) <= REL_TOL
+    assert rel_err(y.cpu(), fx["y"]) <= REL_TOL, rel_err(y.cpu(), fx["y"])
+
+
+def test_single_step_msgnn3_and_gnn(cuda):
+    fx = golden("fx_small3_msgnn3_wet")
+    g = wet_state(make_multiscale_mesh(**mesh_config("small3"), T=6), seed=3).to(cuda)
+    m = _hip(build_msgnn(3, 32, 4, state=weights("msgnn3_F32_seed666")), cuda)
+    with torch.no_grad():
+        y = m(g)
+    assert rel_err(y.cpu(), fx["y"]) <= REL_TOL
+    r = m.rollout(g, 6)
+    assert per_step_rel(r.cpu(), torch.from_numpy(fx["rollout"])) <= REL_TOL
+
+    fx = golden("fx_gnn_small_rollout10")
+    g = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=10), seed=2).to(cuda)
+    m = _hip(build_gnn(state=weights("gnn_F32_seed42")), cuda)
+    with torch.no_grad():
+        y = m(g)
+    assert rel_err(y.cpu(), fx["y"]) <= REL_TOL
+    r = m.rollout(g, 10)
+    assert per_step_rel(r.cpu(), torch.from_numpy(fx["rollout"])) <= REL_TOL
+
+
+@pytest.mark.parametrize("ck,K,F", [("K4_F32", 4, 32), ("K2_F16", 2, 16)])
+def test_rollout48_vs_reference(cuda, ck, K, F):
+    fx = golden(f"fx_small_{ck}_rollout48")
+    g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+    m = _hip(build_msgnn(4, F, K, state=weights(ck)), cuda)
+    r = m.rollout(g)
+    torch.cuda.synchronize()
+    ref = torch.from_numpy(fx["rollout"])
+    assert per_step_rel(r.cpu(), ref) <= REL_TOL, per_step_rel(r.cpu(), ref)
+    st = _stats(m, g)
+    assert st["rollout_steps"] >= 48
+
+
+def test_rollout_zenodo_size_vs_reference(cuda):
+    fx = golden("fx_zenodo4_K4_F32_rollout48")
+    g = make_multiscale_mesh(**mesh_config("zenodo4"), T=48).to(cuda)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    r = m.rollout(g)
+    sel = r[..., fx["steps"]].cpu()
+    assert per_step_rel(sel, torch.from_numpy(fx["rollout_sel"])) <= REL_TOL
+
+
+def test_fused_rollout_matches_step_loop_and_graph_capture(cuda):
+    """Fused msw_rollout (captured hipGraph) == msw_rollout without graph == the
+    reference-style Python loop over the HIP forward (training/train.py semantics)."""
+    from mswegnn.engine import plan_for
+    from utils.dataset import apply_boundary_condition, use_prediction
+    g = make_multiscale_mesh(**mesh_config("small"), T=12).to(cuda)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    plan = plan_for(m, g)
+    plan.set_graph_capture(True)
+    r1 = m.rollout(g).clone()
+    assert plan.stats()["graph_captured"] == 1
+    plan.set_graph_capture(False)
+    r2 = m.rollout(g).clone()
+    assert torch.equal(r1, r2)
+    temp = g.clone()
+    preds = []
+    with torch.no_grad():
+        for t in range(12):
+            temp.x[:, -6:] = apply_boundary_condition(temp.x[:, -6:], temp.BC[:, :, t], temp.node_BC, 2)
+            p = m(temp)
+            temp.x = use_prediction(temp.x, p, 3)
+            preds.append(p)
+    r3 = torch.stack(preds, -1)
+    assert torch.equal(r1, r3)
+
+
+def test_rollout_test_dropin(cuda):
+    from training.train import rollout_test
+    fx = golden("fx_small_K4_F32_rollout48")
+    g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    r = rollout_test(m, g)
+    assert r.shape == (g.num_nodes, 2, 48)
+    assert per_step_rel(r.cpu(), torch.from_numpy(fx["rollout"])) <= REL_TOL
+
+
+def test_hid64_random_init_vs_oracle(cuda):
+    """F=64 (config.yaml default hid_features, checkpoint not shipped): seeded init,
+    wet state, one step and a 4-step rollout vs the oracle."""
+    m = build_msgnn(4, 64, 4)
+    P = state_dict_of(m)
+    cfg = orc.msgnn_config(num_scales=4, hid_features=64, K=4)
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=4), seed=5)
+    ref_y = orc.forward(P, cfg, g)
+    ref_r = orc.rollout(P, cfg, g)
+    m = _hip(m, cuda)
+    gd = g.to(cuda)
+    with torch.no_grad():
+        y = m(gd)
+    assert rel_err(y.cpu(), ref_y) <= REL_TOL
+    assert per_step_rel(m.rollout(gd).cpu(), ref_r) <= REL_TOL
+
+
+def test_variants_vs_oracle(cuda):
+    """Less common constructor options: mlp_layers=2, K per scale, no filter matrix,
+    learned_residuals='all' / False, gnn_activation='prelu', K=1 GNN with 3 layers."""
+    g = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=3, T=3), seed=7)
+    cases = [
+        dict(mlp_layers=2, K=[2, 3, 1]),
+        dict(with_filter_matrix=False, learned_residuals="all"),
+        dict(gnn_activation="prelu", learned_residuals=False, skip_connections=False),
+    ]
+    for kw in cases:
+        m = build_msgnn(3, 32, kw.pop("K", 2), mlp_layers=kw.pop("mlp_layers", 3), **kw)
+        cfg = orc.msgnn_config(num_scales=3, hid_features=32, K=m.K[:3], mlp_layers=m.mlp_layers,
+                               with_filter_matrix=m.gnn_processor[0].with_filter_matrix,
+                               learned_residuals=m.learned_residuals,
+                               gnn_activation="prelu" if isinstance(m.gnn_activation, torch.nn.PReLU) else "tanh",
+                               skip_connections=m.skip_connections)
+        P = state_dict_of(m)
+        ref = orc.rollout(P, cfg, g)
+        m = _hip(m, cuda)
+        r = m.rollout(g.to(cuda))
+        assert per_step_rel(r.cpu(), ref) <= REL_TOL, kw
+    gs = wet_state(make_single_scale_mesh(n_coarse=2, refinements=2, T=3), seed=8)
+    m = build_gnn(hid=32, K=1, n_layers=3, mlp_layers=2)
+    cfg = orc.gnn_config(hid_features=32, K=1, n_GNN_layers=3, mlp_layers=2)
+    ref = orc.rollout(state_dict_of(m), cfg, gs)
+    m = _hip(m, cuda)
+    assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL
+
+
+def test_batched_graphs_match_individual(cuda):
+    """Two simulations as one disjoint-union batch (update_batch_multiscale layout,
+    training/train.py:31-65) give the same rollouts as each alone."""
+    from mswegnn.batch import collate
+    ga = make_multiscale_mesh(n_coarse=2, num_scales=4, seed=1, T=8)
+    gb = make_multiscale_mesh(n_coarse=3, num_scales=4, seed=2, T=8)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    ra = m.rollout(ga.to(cuda)).cpu()
+    rb = m.rollout(gb.to(cuda)).cpu()
+    bt = collate([ga, gb])
+    from training.train import rollout_test
+    r = rollout_test(m, bt.to(cuda)).cpu()
+    na = ga.num_nodes
+    assert per_step_rel(r[:na], ra) <= REL_TOL
+    assert per_step_rel(r[na:], rb) <= REL_TOL
+
+
+def test_edge_cases(cuda):
+    """T = 0, no BC node, and a dry graph (every active-edge predicate false)."""
+    g = make_multiscale_mesh(**mesh_config("tiny"), T=4).to(cuda)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    assert m.rollout(g, 0).shape == (g.num_nodes, 2, 0)
+    g2 = g.clone()
+    g2.node_BC = g2.node_BC[:0]
+    g2.BC = g2.BC[:0]
+    cfg = manifest()["weights_K4_F32_cfg"]
+    ref = orc.rollout(weights("K4_F32"), cfg, g2.to("cpu"))
+    assert per_step_rel(m.rollout(g2).cpu(), ref) <= REL_TOL
