@@ -173,6 +173,15 @@ int msw_set_graph_capture(msw_plan* plan, int enable);
 
 int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
 
+/* Re-launch one kernel of the step `iters` times on `stream` (benchmark / roofline hook;
+ * call after a forward or rollout: it reuses the plan's workspaces and overwrites scratch).
+ *   kernel: 0 = hop (first processor on `scale`), 1 = edge MLP (same processor),
+ *           2 = node projection (same processor), 3 = pooling into `scale` (scale >= 1),
+ *           4 = node encoders, 5 = decoder.
+ * units_out (optional) receives {rows, edges} processed by ONE launch. */
+int msw_bench_kernel(msw_plan* plan, int32_t kernel, int32_t scale, int32_t iters,
+                     int64_t* units_out, void* stream);
+
 /* sizeof() of a descriptor struct ("msw_linear", "msw_mlp", "msw_swegnn",
  * "msw_model_desc", "msw_graph_desc", "msw_plan_stats"); -1 if unknown.  Pure host code:
  * lets FFI bindings verify their struct layouts without a GPU. */

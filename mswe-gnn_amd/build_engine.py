@@ -1,8 +1,8 @@
 """Build libmswegnn.so in-tree for gfx950 (hipcc, no torch involvement).
 
-    python mswe-gnn_amd/build.py [--force]
+    python mswe-gnn_amd/build_engine.py [--force]
 
-Objects go to mswe-gnn_amd/build/, the library to mswe-gnn_amd/lib/libmswegnn.so.
+Objects go to mswe-gnn_amd/_obj/, the library to mswe-gnn_amd/lib/libmswegnn.so.
 Rebuilds an object only when its source or a header is newer.
 """
 import os
@@ -23,13 +23,13 @@ def _newer(a, b):
 
 
 def build(force=False, verbose=True):
-    os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, "_obj"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     objs = []
     hdr_t = max(os.path.getmtime(h if os.path.isabs(h) else os.path.join(HERE, h)) for h in HDR)
     for s in SRC:
         src = os.path.join(HERE, s)
-        obj = os.path.join(HERE, "build", os.path.basename(s) + ".o")
+        obj = os.path.join(HERE, "_obj", os.path.basename(s) + ".o")
         objs.append(obj)
         stale = force or _newer(src, obj) or (os.path.exists(obj) and hdr_t > os.path.getmtime(obj))
         if stale:

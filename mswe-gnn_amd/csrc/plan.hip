@@ -546,6 +546,74 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
 
 }  // namespace
 
+namespace {
+template <int FP>
+int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
+  if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
+  const Proc* pr = nullptr;
+  for (auto& q : P->procs)
+    if (q.scale == scale) { pr = &q; break; }
+  const ScaleCSR& g = P->sc[scale];
+  int64_t rows = 0, edges = 0;
+  for (int it = 0; it < iters; ++it) {
+    if (kernel == 0 || kernel == 1 || kernel == 2) {
+      if (!pr) return fail(MSW_ERR_INVALID, "no processor on that scale");
+      if (kernel == 0) {
+        HopArgs h{};
+        h.n0 = g.n0; h.R = g.ns; h.rowptr = g.rowptr; h.src = g.src; h.s = P->s; h.in = P->bufA;
+        h.out = P->bufB; h.WT = pr->wt_off.empty() ? nullptr : P->dW + pr->wt_off[0];
+        h.grad = pr->with_gradient; h.upwind = pr->upwind;
+        HIP_TRY(launch_hop<FP>(h, st));
+        rows = g.ns; edges = g.E;
+      } else if (kernel == 1) {
+        EdgeMlpArgs em{};
+        em.E = g.E; em.src = g.src; em.dst = g.dst; em.U = P->U; em.V = P->V; em.Pe = pr->Pe;
+        em.b1 = P->dW + pr->b1_off; em.h1t = pr->h1t; em.act1 = pr->act1; em.slope1 = pr->slope1;
+        em.rest = pr->rest; em.W = P->dW + pr->rest_base; em.w_count = pr->rest_count;
+        em.normalize = pr->normalize; em.s = P->s;
+        HIP_TRY(launch_edge_mlp<FP>(em, st));
+        rows = 0; edges = g.E;
+      } else {
+        NodeProjArgs np{};
+        np.r0 = g.n0; np.R = g.ns; np.xs = P->xs; np.xin = P->xin;
+        np.a_u = pr->a_u; np.a_v = pr->a_v; np.a_o = pr->a_o; np.W = P->dW;
+        np.U = P->U; np.V = P->V; np.O = P->bufA; np.h1t = pr->h1t;
+        HIP_TRY(launch_node_proj<FP>(np, st));
+        rows = g.ns; edges = 0;
+      }
+    } else if (kernel == 3) {
+      if (scale < 1) return fail(MSW_ERR_INVALID, "pooling targets scale >= 1");
+      PoolArgs pa{};
+      pa.n0 = g.n0; pa.R = g.ns; pa.rowptr = P->lv[scale - 1].pool_rowptr;
+      pa.child = P->lv[scale - 1].pool_child; pa.in = P->xdown; pa.out = P->bufB;
+      HIP_TRY(launch_pool<FP>(pa, st));
+      rows = g.ns; edges = P->lv[scale - 1].I;
+    } else if (kernel == 4) {
+      EncodeArgs ea{};
+      ea.x = P->X; ea.perm = nullptr; ea.N = P->N; ea.nnf = P->nnf; ea.nstat_raw = P->nstat_raw;
+      ea.with_wl = P->with_wl; ea.dyn = P->dyn; ea.stat = P->stat; ea.dynm = P->dynm; ea.W = P->dW;
+      ea.xs = P->bufA; ea.xd = P->bufB; ea.xd_rows = P->sc[0].n0 + P->sc[0].ns; ea.io = nullptr;
+      HIP_TRY(launch_encode<FP>(ea, st));
+      rows = P->N; edges = 0;
+    } else if (kernel == 5) {
+      DecodeArgs da{};
+      da.N = P->N; da.nnf = P->nnf; da.dyn = P->dyn; da.p = P->p; da.xup = P->xup;
+      da.pre_act = P->gnn_act; da.pre_slope = P->gnn_slope; da.dec = P->dec; da.W = P->dW;
+      da.resw = P->resw_off >= 0 ? P->dW + P->resw_off : nullptr;
+      da.X = P->X; da.perm = P->identity ? nullptr : P->perm_d; da.y = P->bufB; da.io = nullptr;
+      da.bc_slot = P->bc_slot_d;
+      HIP_TRY(launch_decode<FP>(da, st));
+      rows = P->N; edges = 0;
+    } else {
+      return fail(MSW_ERR_INVALID, "unknown kernel id");
+    }
+  }
+  if (units) { units[0] = rows; units[1] = edges; }
+  return MSW_OK;
+}
+
+}  // namespace
+
 // ============================================================================ C ABI
 extern "C" {
 
@@ -812,6 +880,15 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
   P->rollout_steps += T;
   P->forward_calls += T;
   return MSW_OK;
+}
+
+int msw_bench_kernel(msw_plan* P, int32_t kernel, int32_t scale, int32_t iters, int64_t* units,
+                     void* stream) {
+  if (!P || iters < 0) return fail(MSW_ERR_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(P->device));
+  hipStream_t st = (hipStream_t)stream;
+  return P->FP == 32 ? bench_kernel<32>(P, kernel, scale, iters, units, st)
+                     : bench_kernel<64>(P, kernel, scale, iters, units, st);
 }
 
 int msw_debug_buffer(msw_plan* P, const char* name, float* dst, void* stream) {

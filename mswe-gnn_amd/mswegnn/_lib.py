@@ -1,7 +1,7 @@
 """ctypes binding of the C ABI in include/mswegnn.h (libmswegnn.so, gfx950).
 
 The shared library is built in-tree (mswe-gnn_amd/lib/libmswegnn.so) by
-``python mswe-gnn_amd/build.py`` / ``__graft_entry__.build()``.  There is no fallback:
+``python mswe-gnn_amd/build_engine.py`` / ``__graft_entry__.build()``.  There is no fallback:
 if the library is missing, :func:`lib` raises.
 """
 from __future__ import annotations
@@ -83,6 +83,8 @@ SYMBOLS = [
     ("msw_last_error", C.c_char_p, []),
     ("msw_abi_version", C.c_int, []),
     ("msw_struct_size", C.c_int64, [C.c_char_p]),
+    ("msw_bench_kernel", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_int64_p,
+                                   C.c_void_p]),
 ]
 
 STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,
@@ -99,7 +101,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"mSWE-GNN HIP engine not built: {LIB_PATH} is missing "
-                "(run `python mswe-gnn_amd/build.py` or __graft_entry__.build())")
+                "(run `python mswe-gnn_amd/build_engine.py` or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, res, args in SYMBOLS:
             f = getattr(L, name)

@@ -244,6 +244,16 @@ class EnginePlan:
                                          self._stream()))
         return dst
 
+    KERNELS = {"hop": 0, "edge_mlp": 1, "node_proj": 2, "pool": 3, "encode": 4, "decode": 5}
+
+    def bench_kernel(self, kernel, scale, iters):
+        """Enqueue `iters` launches of one kernel on the current stream -> units (rows, edges)
+        of one launch.  Bracket with events on torch.cuda.current_stream() to time it."""
+        units = (C.c_int64 * 2)()
+        L.check(L.lib().msw_bench_kernel(self._h, self.KERNELS[kernel], int(scale), int(iters),
+                                         units, self._stream()))
+        return int(units[0]), int(units[1])
+
     def set_graph_capture(self, enable):
         L.check(L.lib().msw_set_graph_capture(self._h, int(bool(enable))))
 

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU session: smoke, GPU parity tests, bench, rocprofv3 kernel trace of the bench.
+# Every GPU step has its own time limit; a fault / abort / timeout ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out
+mkdir -p $OUT
+: > $OUT/steps.log
+step() {  # step NAME SECONDS CMD...  (exit codes 0/1 continue; anything else stops)
+  local name=$1 secs=$2; shift 2
+  local t0=$(date +%s)
+  timeout -k 10 "$secs" "$@"
+  local rc=$?
+  echo "$name rc=$rc $(( $(date +%s) - t0 ))s" >> $OUT/steps.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >> $OUT/steps.log; exit $rc; fi
+}
+MODE=${1:-all}
+if [[ $MODE == all || $MODE == tests ]]; then
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+  step gputests 900 python -m pytest tests -m gpu -q > $OUT/gpu_tests.log 2>&1
+fi
+if [[ $MODE == all || $MODE == bench ]]; then
+  step bench 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+fi
+if [[ $MODE == all || $MODE == prof ]]; then
+  export TMPDIR=/tmp
+  rm -rf $OUT/prof
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+fi
+echo done >> $OUT/steps.log
