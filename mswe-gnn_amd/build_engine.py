@@ -8,11 +8,13 @@ Rebuilds an object only when its source or a header is newer.
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = ["csrc/kernels.hip", "csrc/plan.hip"]
-HDR = ["csrc/engine.h", os.path.join(ROOT, "include", "mswegnn.h")]
+SRC = ["csrc/kernels_nt1.hip", "csrc/kernels_nt2.hip", "csrc/kernels_nt4.hip",
+       "csrc/kernels_common.hip", "csrc/plan.hip"]
+HDR = ["csrc/engine.h", "csrc/kernels_impl.h", os.path.join(ROOT, "include", "mswegnn.h")]
 ARCH = os.environ.get("MSW_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
          "-I", os.path.join(ROOT, "include")]
@@ -25,7 +27,7 @@ def _newer(a, b):
 def build(force=False, verbose=True):
     os.makedirs(os.path.join(HERE, "_obj"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     hdr_t = max(os.path.getmtime(h if os.path.isabs(h) else os.path.join(HERE, h)) for h in HDR)
     for s in SRC:
         src = os.path.join(HERE, s)
@@ -33,10 +35,15 @@ def build(force=False, verbose=True):
         objs.append(obj)
         stale = force or _newer(src, obj) or (os.path.exists(obj) and hdr_t > os.path.getmtime(obj))
         if stale:
-            cmd = ["hipcc", *FLAGS, "-c", src, "-o", obj]
+            cmds.append(["hipcc", *FLAGS, "-c", src, "-o", obj])
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    with ThreadPoolExecutor(jobs) as ex:  # one hipcc per translation unit, in parallel
+        for cmd in cmds:
             if verbose:
                 print(" ".join(cmd), flush=True)
-            subprocess.run(cmd, check=True)
+        for r in list(ex.map(lambda c: subprocess.run(c, check=False), cmds)):
+            if r.returncode != 0:
+                raise subprocess.CalledProcessError(r.returncode, r.args)
     out = os.path.join(HERE, "lib", "libmswegnn.so")
     if force or any(_newer(o, out) for o in objs):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs]

@@ -35,12 +35,8 @@ int fail(int code, const std::string& msg) {
       return fail(MSW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));     \
   } while (0)
 
-inline int tiles(int n) { return (n + 31) / 32; }
+inline int tiles(int n) { return (n + 15) / 16; }
 
-// Packed-operand row permutation: accumulator register r of lane half h in output tile
-// `to` holds MFMA row i = (r&3) + 8(r>>2) + 4h; we want it to hold output feature
-// 32to + 16h + r, so MFMA row i takes feature q(i).
-inline int q_of_row(int i) { return 16 * ((i >> 2) & 1) + 4 * (i >> 3) + (i & 3); }
 
 struct Blob {
   std::vector<float> h;
@@ -51,32 +47,32 @@ struct Blob {
   }
 };
 
-// Pack W (original [out_dim][in_dim]) as the MFMA A operand [tout][tin][r4][lane][4].
+// Pack W (original [out_dim][in_dim]) as the A operand of v_mfma_f32_16x16x4_f32,
+// [tout][tin][lane][4]: lane l, k-step r of input tile ti for output tile to holds
+// W[16 to + (l & 15)][16 ti + 4 (l >> 4) + r] (see kernels_impl.h for the register layout).
 // in_map(k) / out_map(o) give the original column / row of packed input feature k /
 // output feature o, or -1 for a zero pad.
 template <class InMap, class OutMap>
 int pack_operand(Blob& B, const float* W, int in_dim, int tout, int tin, InMap in_map,
                  OutMap out_map) {
-  const int off = B.alloc((size_t)tout * tin * 16 * 64);
+  const int off = B.alloc((size_t)tout * tin * 64 * 4);
   float* A = B.h.data() + off;
   for (int to = 0; to < tout; ++to)
     for (int ti = 0; ti < tin; ++ti)
-      for (int r4 = 0; r4 < 4; ++r4)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int q = 0; q < 4; ++q) {
-            const int r = 4 * r4 + q, i = lane & 31, h = lane >> 5;
-            const int o = out_map(32 * to + q_of_row(i));
-            const int k = in_map(32 * ti + 16 * h + r);
-            float v = 0.f;
-            if (o >= 0 && k >= 0) v = W[(size_t)o * in_dim + k];
-            A[((((size_t)to * tin + ti) * 4 + r4) * 64 + lane) * 4 + q] = v;
-          }
+      for (int lane = 0; lane < 64; ++lane)
+        for (int r = 0; r < 4; ++r) {
+          const int o = out_map(16 * to + (lane & 15));
+          const int k = in_map(16 * ti + 4 * (lane >> 4) + r);
+          float v = 0.f;
+          if (o >= 0 && k >= 0) v = W[(size_t)o * in_dim + k];
+          A[(((size_t)to * tin + ti) * 64 + lane) * 4 + r] = v;
+        }
   return off;
 }
 
 int pack_bias(Blob& B, const float* b, int out_dim, int tout) {
   if (!b) return -1;
-  const int off = B.alloc((size_t)32 * tout);
+  const int off = B.alloc((size_t)16 * tout);
   for (int o = 0; o < out_dim; ++o) B.h[off + o] = b[o];
   return off;
 }
@@ -126,6 +122,14 @@ int upload(T** p, const std::vector<T>& v, int64_t& counter) {
 
 }  // namespace
 
+hipError_t rowmlp_dispatch(int NT, const RowMlpArgs& ra) {
+  switch (NT) {
+    case 1: return launch_rowmlp<1>(ra, nullptr);
+    case 2: return launch_rowmlp<2>(ra, nullptr);
+    default: return launch_rowmlp<4>(ra, nullptr);
+  }
+}
+
 // ============================================================================ plan
 struct ScaleCSR {
   int n0 = 0, ns = 0;     // internal node range
@@ -156,12 +160,13 @@ struct Proc {                 // one SWEGNN layer bound to a scale (or intra lev
   float slope1 = 0.f;
   MlpDev rest{};              // layers 2..L, offsets relative to rest_base
   int rest_base = 0, rest_count = 0;
-  std::vector<int> wt_off;    // transposed filters 1..K (blob offsets)
+  std::vector<int> wt_off;    // packed filters 1..K (blob offsets)
+  int prelu = 0;              // every edge-MLP activation is PReLU
 };
 
 struct msw_plan {
   int device = 0;
-  int model_type = 0, F = 32, FP = 32, T = 1, S = 1, p = 3, nnf = 8, dyn = 6, nstat_raw = 2;
+  int model_type = 0, F = 32, NT = 2, S = 1, p = 3, nnf = 8, dyn = 6, nstat_raw = 2;
   int with_wl = 1, skip = 1, ef = 1;
   int N = 0;
   int64_t E = 0;
@@ -173,6 +178,7 @@ struct msw_plan {
   MlpDev stat{}, dynm{}, dec{}, edge_enc{};
   int gnn_act = 0;
   float gnn_slope = 0.f;
+  int enc_prelu = 0, dec_prelu = 0;
   int resw_off = -1;
   Blob blob;
   float* dW = nullptr;
@@ -227,7 +233,7 @@ void csr_build(int nkeys, const std::vector<int>& key, std::vector<int>& rowptr,
 
 // SWEGNN layer -> packed Proc.  edge_in: width of the per-edge features it consumes.
 int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr) {
-  const int F = P->F, FP = P->FP;
+  const int F = P->F;
   pr.scale = scale;
   pr.K = g.K;
   pr.normalize = g.normalize;
@@ -242,6 +248,10 @@ int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr
   const int ef = g.edge_features;
   if (L1.in_features != 4 * F + ef) return fail(MSW_ERR_INVALID, "edge MLP input width != 4F + edge_features");
   const int H1 = L1.out_features;
+  if (H1 != (m.n_layers > 1 ? 2 * F : F)) return fail(MSW_ERR_UNSUPPORTED, "edge MLP hidden width must be 2F");
+  for (int i = 1; i < m.n_layers; ++i)
+    if (m.layer[i].in_features != 2 * F || m.layer[i].out_features != (i == m.n_layers - 1 ? F : 2 * F))
+      return fail(MSW_ERR_UNSUPPORTED, "edge MLP layer widths must be 2F -> ... -> F");
   pr.h1t = tiles(H1);
   P->h1t_max = std::max(P->h1t_max, pr.h1t);
   const int din = L1.in_features;
@@ -249,43 +259,40 @@ int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr
   auto outm = [&](int o) { return o < H1 ? o : -1; };
   // U: [x_s (tiles 0..T-1) | x_d (tiles T..2T-1)] of the ROW (source) node
   auto in_u = [&](int k) {
-    if (k < FP) return k < F ? k : -1;                       // x_s[row]  cols [0, F)
-    return (k - FP) < F ? 2 * F + (k - FP) : -1;             // x_d[row]  cols [2F, 3F)
+    if (k < F) return k;                                     // x_s[row]  cols [0, F)
+    return k < 2 * F ? 2 * F + (k - F) : -1;                 // x_d[row]  cols [2F, 3F)
   };
   auto in_v = [&](int k) {
-    if (k < FP) return k < F ? F + k : -1;                   // x_s[col]  cols [F, 2F)
-    return (k - FP) < F ? 3 * F + (k - FP) : -1;             // x_d[col]  cols [3F, 4F)
+    if (k < F) return F + k;                                 // x_s[col]  cols [F, 2F)
+    return k < 2 * F ? 3 * F + (k - F) : -1;                 // x_d[col]  cols [3F, 4F)
   };
-  pr.a_u = pack_operand(P->blob, W1, din, pr.h1t, 2 * P->T, in_u, outm);
-  pr.a_v = pack_operand(P->blob, W1, din, pr.h1t, 2 * P->T, in_v, outm);
+  pr.a_u = pack_operand(P->blob, W1, din, pr.h1t, 2 * P->NT, in_u, outm);
+  pr.a_v = pack_operand(P->blob, W1, din, pr.h1t, 2 * P->NT, in_v, outm);
   pr.act1 = L1.act;
   pr.slope1 = L1.act_param;
   if (L1.bias) {
-    pr.b1_off = P->blob.alloc(32 * pr.h1t);
+    pr.b1_off = P->blob.alloc(16 * pr.h1t);
     for (int o = 0; o < H1; ++o) P->blob.h[pr.b1_off + o] = L1.bias[o];
   } else {
-    pr.b1_off = P->blob.alloc(32 * pr.h1t);  // zeros
+    pr.b1_off = P->blob.alloc(16 * pr.h1t);  // zeros
   }
   if (g.with_filter_matrix && !intra) {
     if (!g.filter) return fail(MSW_ERR_INVALID, "with_filter_matrix but no filter weights");
     // filter 0 as an MFMA operand over the x_in tiles: O = W0 . x_in
-    pr.a_o = pack_operand(P->blob, g.filter[0], F, P->T, P->T,
+    pr.a_o = pack_operand(P->blob, g.filter[0], F, P->NT, P->NT,
                           [&](int k) { return k < F ? k : -1; },
                           [&](int o) { return o < F ? o : -1; });
-    for (int k = 1; k <= g.K; ++k) {
-      const int off = P->blob.alloc((size_t)FP * FP);
-      const float* Wk = g.filter[k];
-      for (int i = 0; i < F; ++i)
-        for (int o = 0; o < F; ++o) P->blob.h[off + i * FP + o] = Wk[(size_t)o * F + i];
-      pr.wt_off.push_back(off);
-    }
+    for (int k = 1; k <= g.K; ++k)  // filters 1..K as MFMA operands of the hop kernel
+      pr.wt_off.push_back(pack_operand(P->blob, g.filter[k], F, P->NT, P->NT,
+                                       [&](int q) { return q < F ? q : -1; },
+                                       [&](int o) { return o < F ? o : -1; }));
   } else if (g.with_filter_matrix && intra) {
     return fail(MSW_ERR_UNSUPPORTED, "intra-scale SWEGNN with filter matrix");
   } else if (!intra) {
     // out = x_d.clone() (gnn.py:404): identity operand, exact (1*x + 0*y sums)
     std::vector<float> I((size_t)F * F, 0.f);
     for (int i = 0; i < F; ++i) I[(size_t)i * F + i] = 1.f;
-    pr.a_o = pack_operand(P->blob, I.data(), F, P->T, P->T,
+    pr.a_o = pack_operand(P->blob, I.data(), F, P->NT, P->NT,
                           [&](int k) { return k < F ? k : -1; },
                           [&](int o) { return o < F ? o : -1; });
   }
@@ -306,6 +313,8 @@ int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr
     pr.rest.l[i - 1].slope = L.act_param;
   }
   if (m.layer[m.n_layers - 1].out_features != F) return fail(MSW_ERR_INVALID, "edge MLP output != F");
+  pr.prelu = 1;
+  for (int i = 0; i < m.n_layers; ++i) pr.prelu &= (m.layer[i].act == MSW_ACT_PRELU);
   pr.rest_count = (int)((rb.h.size() + 3) / 4 * 4);
   pr.rest_base = P->blob.alloc(pr.rest_count);
   std::copy(rb.h.begin(), rb.h.end(), P->blob.h.begin() + pr.rest_base);
@@ -314,7 +323,7 @@ int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr
   return MSW_OK;
 }
 
-template <int FP>
+template <int NT>
 int run_proc(msw_plan* P, const Proc& pr, const float* xin, float* out, int post_act,
              float post_slope, hipStream_t st, int& nk) {
   const ScaleCSR& g = P->sc[pr.scale];
@@ -322,29 +331,29 @@ int run_proc(msw_plan* P, const Proc& pr, const float* xin, float* out, int post
   np.r0 = g.n0; np.R = g.ns; np.xs = P->xs; np.xin = xin;
   np.a_u = pr.a_u; np.a_v = pr.a_v; np.a_o = pr.a_o; np.W = P->dW;
   np.U = P->U; np.V = P->V; np.O = P->bufA; np.h1t = pr.h1t;
-  HIP_TRY(launch_node_proj<FP>(np, st)); ++nk;
+  HIP_TRY(launch_node_proj<NT>(np, st)); ++nk;
   EdgeMlpArgs em{};
   em.E = g.E; em.src = g.src; em.dst = g.dst; em.U = P->U; em.V = P->V; em.Pe = pr.Pe;
   em.b1 = P->dW + pr.b1_off; em.h1t = pr.h1t; em.act1 = pr.act1; em.slope1 = pr.slope1;
   em.rest = pr.rest; em.W = P->dW + pr.rest_base; em.w_count = pr.rest_count;
-  em.normalize = pr.normalize; em.s = P->s;
-  HIP_TRY(launch_edge_mlp<FP>(em, st)); ++nk;
+  em.normalize = pr.normalize; em.s = P->s; em.prelu_only = pr.prelu;
+  HIP_TRY(launch_edge_mlp<NT>(em, st)); ++nk;
   const float* cur = P->bufA;
   for (int k = 1; k <= pr.K; ++k) {
     float* nxt = (k == pr.K) ? out : (cur == P->bufA ? P->bufB : P->bufA);
     HopArgs h{};
     h.n0 = g.n0; h.R = g.ns; h.rowptr = g.rowptr; h.src = g.src; h.s = P->s; h.in = cur;
-    h.out = nxt; h.WT = pr.wt_off.empty() ? nullptr : P->dW + pr.wt_off[k - 1]; h.skip = nullptr; h.own_zero = 0;
+    h.out = nxt; h.A = pr.wt_off.empty() ? nullptr : P->dW + pr.wt_off[k - 1]; h.skip = nullptr; h.own_zero = 0;
     h.grad = pr.with_gradient; h.upwind = pr.upwind;
     h.post_act = (k == pr.K) ? post_act : 0; h.post_slope = post_slope;
-    HIP_TRY(launch_hop<FP>(h, st)); ++nk;
+    HIP_TRY(launch_hop<NT>(h, st)); ++nk;
     cur = nxt;
   }
   return MSW_OK;
 }
 
 // intra_scale_gnn[i] on level l: coarse rows (scale l+1) of `xo` -> fine rows of `dst`
-template <int FP>
+template <int NT>
 int run_unpool(msw_plan* P, const Proc& pr, int l, const float* xo, float* dst, hipStream_t st,
                int& nk) {
   const ScaleCSR& cs = P->sc[l + 1];
@@ -353,26 +362,26 @@ int run_unpool(msw_plan* P, const Proc& pr, int l, const float* xo, float* dst, 
   NodeProjArgs np{};
   np.xs = P->xs; np.W = P->dW; np.U = P->U; np.V = P->V; np.O = nullptr; np.h1t = pr.h1t;
   np.r0 = cs.n0; np.R = cs.ns; np.xin = xo; np.a_u = pr.a_u; np.a_v = -1; np.a_o = -1;
-  HIP_TRY(launch_node_proj<FP>(np, st)); ++nk;
+  HIP_TRY(launch_node_proj<NT>(np, st)); ++nk;
   np.r0 = fs.n0; np.R = fs.ns; np.xin = nullptr; np.a_u = -1; np.a_v = pr.a_v;
-  HIP_TRY(launch_node_proj<FP>(np, st)); ++nk;
+  HIP_TRY(launch_node_proj<NT>(np, st)); ++nk;
   EdgeMlpArgs em{};
   em.E = m.I; em.src = m.un_src; em.dst = m.un_dst; em.U = P->U; em.V = P->V; em.Pe = nullptr;
   em.b1 = P->dW + pr.b1_off; em.h1t = pr.h1t; em.act1 = pr.act1; em.slope1 = pr.slope1;
   em.rest = pr.rest; em.W = P->dW + pr.rest_base; em.w_count = pr.rest_count;
-  em.normalize = pr.normalize; em.s = P->s;
-  HIP_TRY(launch_edge_mlp<FP>(em, st)); ++nk;
+  em.normalize = pr.normalize; em.s = P->s; em.prelu_only = pr.prelu;
+  HIP_TRY(launch_edge_mlp<NT>(em, st)); ++nk;
   HopArgs h{};
   h.n0 = fs.n0; h.R = fs.ns; h.rowptr = m.un_rowptr; h.src = m.un_src; h.s = P->s; h.in = xo;
-  h.out = dst; h.WT = nullptr; h.skip = P->skip ? P->xdown : nullptr; h.own_zero = 1;
+  h.out = dst; h.A = nullptr; h.skip = P->skip ? P->xdown : nullptr; h.own_zero = 1;
   h.grad = pr.with_gradient; h.upwind = pr.upwind; h.post_act = 0; h.post_slope = 0.f;
-  HIP_TRY(launch_hop<FP>(h, st)); ++nk;
+  HIP_TRY(launch_hop<NT>(h, st)); ++nk;
   return MSW_OK;
 }
 
 // One forward.  x_src/perm: input rows (forward mode: graph rows via perm; rollout: the
 // internal state X with perm = null).  y: forward-mode output (null in rollout mode).
-template <int FP>
+template <int NT>
 int enqueue_step(msw_plan* P, const float* x_src, const int* perm, float* y, bool rollout,
                  hipStream_t st) {
   int nk = 0;
@@ -381,7 +390,8 @@ int enqueue_step(msw_plan* P, const float* x_src, const int* perm, float* y, boo
   ea.with_wl = P->with_wl; ea.dyn = P->dyn; ea.stat = P->stat; ea.dynm = P->dynm; ea.W = P->dW;
   ea.xs = P->xs; ea.xd = P->xd0; ea.xd_rows = P->sc[0].n0 + P->sc[0].ns;
   ea.io = rollout ? P->io_d : nullptr;
-  HIP_TRY(launch_encode<FP>(ea, st)); ++nk;
+  ea.prelu_only = P->enc_prelu;
+  HIP_TRY(launch_encode<NT>(ea, st)); ++nk;
   const float* dec_in = nullptr;
   int pre_act = 0;
   float pre_slope = 0.f;
@@ -389,21 +399,21 @@ int enqueue_step(msw_plan* P, const float* x_src, const int* perm, float* y, boo
   if (P->model_type == 0) {
     const int S = P->S;
     for (int i = 0; i < S - 1; ++i) {
-      rc = run_proc<FP>(P, P->procs[i], i == 0 ? P->xd0 : P->xin, P->xdown, 0, 0.f, st, nk);
+      rc = run_proc<NT>(P, P->procs[i], i == 0 ? P->xd0 : P->xin, P->xdown, 0, 0.f, st, nk);
       if (rc) return rc;
       PoolArgs pa{};
       pa.n0 = P->sc[i + 1].n0; pa.R = P->sc[i + 1].ns; pa.rowptr = P->lv[i].pool_rowptr;
       pa.child = P->lv[i].pool_child; pa.in = P->xdown; pa.out = P->xin;
-      HIP_TRY(launch_pool<FP>(pa, st)); ++nk;
+      HIP_TRY(launch_pool<NT>(pa, st)); ++nk;
     }
     for (int i = 0; i < S; ++i) {
       const int j = S - 1 + i;
       const float* in = (S == 1) ? P->xd0 : P->xin;
-      rc = run_proc<FP>(P, P->procs[j], in, P->xup, 0, 0.f, st, nk);
+      rc = run_proc<NT>(P, P->procs[j], in, P->xup, 0, 0.f, st, nk);
       if (rc) return rc;
       if (i < S - 1) {
         const int l = S - 2 - i;
-        rc = run_unpool<FP>(P, P->unpools[i], l, P->xup, P->xin, st, nk);
+        rc = run_unpool<NT>(P, P->unpools[i], l, P->xup, P->xin, st, nk);
         if (rc) return rc;
       }
     }
@@ -414,7 +424,7 @@ int enqueue_step(msw_plan* P, const float* x_src, const int* perm, float* y, boo
     const float* cur = P->xd0;
     for (size_t j = 0; j < P->procs.size(); ++j) {
       float* out = P->gnnbuf[j & 1];
-      rc = run_proc<FP>(P, P->procs[j], cur, out, P->gnn_act, P->gnn_slope, st, nk);
+      rc = run_proc<NT>(P, P->procs[j], cur, out, P->gnn_act, P->gnn_slope, st, nk);
       if (rc) return rc;
       cur = out;
     }
@@ -427,15 +437,19 @@ int enqueue_step(msw_plan* P, const float* x_src, const int* perm, float* y, boo
   da.X = const_cast<float*>(x_src);
   da.perm = P->identity ? nullptr : P->perm_d;
   da.y = y; da.io = rollout ? P->io_d : nullptr; da.bc_slot = P->bc_slot_d;
-  HIP_TRY(launch_decode<FP>(da, st)); ++nk;
+  da.prelu_only = P->dec_prelu;
+  HIP_TRY(launch_decode<NT>(da, st)); ++nk;
   P->kernels_per_step = nk;
   return MSW_OK;
 }
 
 int step_dispatch(msw_plan* P, const float* x_src, const int* perm, float* y, bool rollout,
                   hipStream_t st) {
-  return P->FP == 32 ? enqueue_step<32>(P, x_src, perm, y, rollout, st)
-                     : enqueue_step<64>(P, x_src, perm, y, rollout, st);
+  switch (P->NT) {
+    case 1: return enqueue_step<1>(P, x_src, perm, y, rollout, st);
+    case 2: return enqueue_step<2>(P, x_src, perm, y, rollout, st);
+    default: return enqueue_step<4>(P, x_src, perm, y, rollout, st);
+  }
 }
 
 int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
@@ -547,7 +561,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
 }  // namespace
 
 namespace {
-template <int FP>
+template <int NT>
 int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
   if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
   const Proc* pr = nullptr;
@@ -561,24 +575,24 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
       if (kernel == 0) {
         HopArgs h{};
         h.n0 = g.n0; h.R = g.ns; h.rowptr = g.rowptr; h.src = g.src; h.s = P->s; h.in = P->bufA;
-        h.out = P->bufB; h.WT = pr->wt_off.empty() ? nullptr : P->dW + pr->wt_off[0];
+        h.out = P->bufB; h.A = pr->wt_off.empty() ? nullptr : P->dW + pr->wt_off[0];
         h.grad = pr->with_gradient; h.upwind = pr->upwind;
-        HIP_TRY(launch_hop<FP>(h, st));
+        HIP_TRY(launch_hop<NT>(h, st));
         rows = g.ns; edges = g.E;
       } else if (kernel == 1) {
         EdgeMlpArgs em{};
         em.E = g.E; em.src = g.src; em.dst = g.dst; em.U = P->U; em.V = P->V; em.Pe = pr->Pe;
         em.b1 = P->dW + pr->b1_off; em.h1t = pr->h1t; em.act1 = pr->act1; em.slope1 = pr->slope1;
         em.rest = pr->rest; em.W = P->dW + pr->rest_base; em.w_count = pr->rest_count;
-        em.normalize = pr->normalize; em.s = P->s;
-        HIP_TRY(launch_edge_mlp<FP>(em, st));
+        em.normalize = pr->normalize; em.s = P->s; em.prelu_only = pr->prelu;
+        HIP_TRY(launch_edge_mlp<NT>(em, st));
         rows = 0; edges = g.E;
       } else {
         NodeProjArgs np{};
         np.r0 = g.n0; np.R = g.ns; np.xs = P->xs; np.xin = P->xin;
         np.a_u = pr->a_u; np.a_v = pr->a_v; np.a_o = pr->a_o; np.W = P->dW;
         np.U = P->U; np.V = P->V; np.O = P->bufA; np.h1t = pr->h1t;
-        HIP_TRY(launch_node_proj<FP>(np, st));
+        HIP_TRY(launch_node_proj<NT>(np, st));
         rows = g.ns; edges = 0;
       }
     } else if (kernel == 3) {
@@ -586,14 +600,15 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
       PoolArgs pa{};
       pa.n0 = g.n0; pa.R = g.ns; pa.rowptr = P->lv[scale - 1].pool_rowptr;
       pa.child = P->lv[scale - 1].pool_child; pa.in = P->xdown; pa.out = P->bufB;
-      HIP_TRY(launch_pool<FP>(pa, st));
+      HIP_TRY(launch_pool<NT>(pa, st));
       rows = g.ns; edges = P->lv[scale - 1].I;
     } else if (kernel == 4) {
       EncodeArgs ea{};
       ea.x = P->X; ea.perm = nullptr; ea.N = P->N; ea.nnf = P->nnf; ea.nstat_raw = P->nstat_raw;
       ea.with_wl = P->with_wl; ea.dyn = P->dyn; ea.stat = P->stat; ea.dynm = P->dynm; ea.W = P->dW;
       ea.xs = P->bufA; ea.xd = P->bufB; ea.xd_rows = P->sc[0].n0 + P->sc[0].ns; ea.io = nullptr;
-      HIP_TRY(launch_encode<FP>(ea, st));
+      ea.prelu_only = P->enc_prelu;
+      HIP_TRY(launch_encode<NT>(ea, st));
       rows = P->N; edges = 0;
     } else if (kernel == 5) {
       DecodeArgs da{};
@@ -601,8 +616,8 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
       da.pre_act = P->gnn_act; da.pre_slope = P->gnn_slope; da.dec = P->dec; da.W = P->dW;
       da.resw = P->resw_off >= 0 ? P->dW + P->resw_off : nullptr;
       da.X = P->X; da.perm = P->identity ? nullptr : P->perm_d; da.y = P->bufB; da.io = nullptr;
-      da.bc_slot = P->bc_slot_d;
-      HIP_TRY(launch_decode<FP>(da, st));
+      da.bc_slot = P->bc_slot_d; da.prelu_only = P->dec_prelu;
+      HIP_TRY(launch_decode<NT>(da, st));
       rows = P->N; edges = 0;
     } else {
       return fail(MSW_ERR_INVALID, "unknown kernel id");
@@ -644,8 +659,7 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   P->device = device;
   P->model_type = m->model_type;
   P->F = m->hid_features;
-  P->FP = P->F <= 32 ? 32 : 64;
-  P->T = P->FP / 32;
+  P->NT = P->F / 16;
   P->S = m->model_type == 0 ? m->num_scales : 1;
   P->p = m->previous_t;
   P->nnf = m->num_node_features;
@@ -656,7 +670,7 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   P->gnn_act = m->gnn_act;
   P->gnn_slope = m->gnn_act_param;
   if (P->S < 1) return fail(MSW_ERR_INVALID, "num_scales < 1");
-  if (P->nstat_raw < 1 || P->nstat_raw + P->with_wl > 32 || P->dyn > 32)
+  if (P->nstat_raw < 1 || P->nstat_raw + P->with_wl > 16 || P->dyn > 16)
     return fail(MSW_ERR_UNSUPPORTED, "node feature layout (static / dynamic widths)");
   if (m->model_type == 0 && m->num_processors != 2 * P->S - 1)
     return fail(MSW_ERR_INVALID, "MSGNN needs 2S-1 processors");
@@ -666,12 +680,32 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
 
   int rc = build_graph_plan(P.get(), g);
   if (rc) return rc;
-  const int F = P->F, FP = P->FP, N = P->N;
+  const int F = P->F, N = P->N;
 
   // ---- weights
   if ((rc = pack_mlp(P->blob, m->static_encoder, P->stat))) return rc;
   if ((rc = pack_mlp(P->blob, m->dynamic_encoder, P->dynm))) return rc;
   if ((rc = pack_mlp(P->blob, m->decoder, P->dec))) return rc;
+  {
+    auto all_prelu = [](const msw_mlp& mm) {
+      for (int i = 0; i < mm.n_layers; ++i)
+        if (mm.layer[i].act != MSW_ACT_PRELU) return 0;
+      return 1;
+    };
+    P->enc_prelu = all_prelu(m->static_encoder) & all_prelu(m->dynamic_encoder);
+    P->dec_prelu = all_prelu(m->decoder);
+  }
+  auto chain_ok = [&](const msw_mlp& mm, int last_out) {
+    for (int i = 0; i < mm.n_layers; ++i) {
+      const int want = (i == mm.n_layers - 1) ? last_out : F;
+      if (mm.layer[i].out_features != want) return false;
+      if (i > 0 && mm.layer[i].in_features != F) return false;
+    }
+    return true;
+  };
+  if (!chain_ok(m->static_encoder, F) || !chain_ok(m->dynamic_encoder, F) || !chain_ok(m->decoder, 2) ||
+      (m->edge_mlp && !chain_ok(m->edge_encoder, F)) || m->decoder.layer[0].in_features != F)
+    return fail(MSW_ERR_UNSUPPORTED, "encoder/decoder hidden widths must equal hid_features");
   if (m->static_encoder.layer[0].in_features != P->nstat_raw + P->with_wl)
     return fail(MSW_ERR_INVALID, "static encoder input width");
   if (m->dynamic_encoder.layer[0].in_features != P->dyn) return fail(MSW_ERR_INVALID, "dynamic encoder input width");
@@ -684,9 +718,9 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   if (m->edge_mlp) {
     if ((rc = pack_mlp(P->blob, m->edge_encoder, P->edge_enc))) return rc;
     if (m->edge_encoder.layer[0].in_features != ef_raw) return fail(MSW_ERR_INVALID, "edge encoder input width");
-    if (ef_raw > 32) return fail(MSW_ERR_UNSUPPORTED, "more than 32 raw edge features");
-  } else if (ef_raw > 32) {
-    return fail(MSW_ERR_UNSUPPORTED, "more than 32 raw edge features");
+    if (ef_raw > 16) return fail(MSW_ERR_UNSUPPORTED, "more than 16 raw edge features");
+  } else if (ef_raw > F) {
+    return fail(MSW_ERR_UNSUPPORTED, "more raw edge features than F");
   }
   const int ef = m->edge_mlp ? F : ef_raw;
   P->procs.resize(m->num_processors);
@@ -712,8 +746,8 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   int Emax = 1;
   for (auto& c : P->sc) Emax = std::max(Emax, c.E);
   for (auto& l : P->lv) Emax = std::max(Emax, l.I);
-  const size_t NF = (size_t)N * FP;
-  const size_t NH = (size_t)N * 32 * P->h1t_max;
+  const size_t NF = (size_t)N * F;
+  const size_t NH = (size_t)N * 16 * P->h1t_max;
   float** bufs[] = {&P->xs, &P->xd0, &P->bufA, &P->bufB, &P->xin, &P->xdown, &P->xup};
   for (float** b : bufs) {
     if ((rc = palloc(P.get(), b, NF))) return rc;
@@ -724,7 +758,7 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     P->gnnbuf[1] = P->xdown;
   }
   if ((rc = palloc(P.get(), &P->U, NH)) || (rc = palloc(P.get(), &P->V, NH))) return rc;
-  if ((rc = palloc(P.get(), &P->s, (size_t)Emax * FP))) return rc;
+  if ((rc = palloc(P.get(), &P->s, (size_t)Emax * F))) return rc;
   if ((rc = palloc(P.get(), &P->X, (size_t)N * P->nnf))) return rc;
 
   // ---- static per-edge features: edge encoder + edge part of each processor's layer 1
@@ -745,12 +779,13 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     const float* feat = ea_d;
     int feat_stride = ef_raw, feat_dim = ef_raw;
     if (m->edge_mlp) {
-      if ((rc = dalloc(&enc_d, (size_t)E * FP, tmp_bytes))) return rc;
+      if ((rc = dalloc(&enc_d, (size_t)E * F, tmp_bytes))) return rc;
       RowMlpArgs ra{};
+      ra.mode = 0;
       ra.in = ea_d; ra.in_stride = ef_raw; ra.in_dim = ef_raw; ra.R = (int)E; ra.m = P->edge_enc;
-      ra.W = P->dW; ra.out = enc_d; ra.out_stride = FP;
-      HIP_TRY(FP == 32 ? launch_rowmlp<32>(ra, nullptr) : launch_rowmlp<64>(ra, nullptr));
-      feat = enc_d; feat_stride = FP; feat_dim = F;
+      ra.W = P->dW; ra.out = enc_d; ra.out_stride = F; ra.out_tiles = P->NT;
+      HIP_TRY(rowmlp_dispatch(P->NT, ra));
+      feat = enc_d; feat_stride = F; feat_dim = F;
     }
     for (size_t j = 0; j < P->procs.size(); ++j) {
       Proc& pr = P->procs[j];
@@ -760,22 +795,27 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
       Blob tb;
       MlpDev md{};
       md.n = 1;
-      md.l[0].tin = tiles(feat_dim);
-      md.l[0].tout = pr.h1t;
-      md.l[0].a_off = pack_operand(tb, L1.weight, L1.in_features, pr.h1t, md.l[0].tin,
+      md.l[0].tin = P->NT;       // k_rowmlp<NT, 1>: one NT -> 2NT layer (zero padded)
+      md.l[0].tout = 2 * P->NT;
+      md.l[0].a_off = pack_operand(tb, L1.weight, L1.in_features, 2 * P->NT, P->NT,
                                    [&](int k) { return k < feat_dim ? 4 * F + k : -1; },
                                    [&](int o) { return o < H1 ? o : -1; });
-      md.l[0].b_off = pack_bias(tb, L1.bias, H1, pr.h1t);
+      md.l[0].b_off = -1;
+      if (L1.bias) {
+        md.l[0].b_off = tb.alloc(16 * 2 * P->NT);
+        for (int o = 0; o < H1; ++o) tb.h[md.l[0].b_off + o] = L1.bias[o];
+      }
       md.l[0].act = 0;
       float* tw = nullptr;
       if ((rc = upload(&tw, tb.h, tmp_bytes))) return rc;
       const ScaleCSR& c = P->sc[pr.scale];
-      if ((rc = palloc(P.get(), &pr.Pe, (size_t)std::max(c.E, 1) * 32 * pr.h1t))) return rc;
+      if ((rc = palloc(P.get(), &pr.Pe, (size_t)std::max(c.E, 1) * 16 * pr.h1t))) return rc;
       RowMlpArgs ra{};
+      ra.mode = 1;
       ra.in = feat + (size_t)sbase[pr.scale] * feat_stride; ra.in_stride = feat_stride;
       ra.in_dim = feat_dim; ra.R = c.E; ra.m = md; ra.W = tw;
-      ra.out = pr.Pe; ra.out_stride = 32 * pr.h1t;
-      HIP_TRY(FP == 32 ? launch_rowmlp<32>(ra, nullptr) : launch_rowmlp<64>(ra, nullptr));
+      ra.out = pr.Pe; ra.out_stride = 16 * pr.h1t; ra.out_tiles = pr.h1t;
+      HIP_TRY(rowmlp_dispatch(P->NT, ra));
       HIP_TRY(hipDeviceSynchronize());
       HIP_TRY(hipFree(tw));
     }
@@ -887,8 +927,11 @@ int msw_bench_kernel(msw_plan* P, int32_t kernel, int32_t scale, int32_t iters, 
   if (!P || iters < 0) return fail(MSW_ERR_INVALID, "bad argument");
   HIP_TRY(hipSetDevice(P->device));
   hipStream_t st = (hipStream_t)stream;
-  return P->FP == 32 ? bench_kernel<32>(P, kernel, scale, iters, units, st)
-                     : bench_kernel<64>(P, kernel, scale, iters, units, st);
+  switch (P->NT) {
+    case 1: return bench_kernel<1>(P, kernel, scale, iters, units, st);
+    case 2: return bench_kernel<2>(P, kernel, scale, iters, units, st);
+    default: return bench_kernel<4>(P, kernel, scale, iters, units, st);
+  }
 }
 
 int msw_debug_buffer(msw_plan* P, const char* name, float* dst, void* stream) {
@@ -900,10 +943,9 @@ int msw_debug_buffer(msw_plan* P, const char* name, float* dst, void* stream) {
   else if (!strcmp(name, "x_in")) src = P->xin;
   else if (!strcmp(name, "x_up")) src = P->model_type == 0 ? P->xup : nullptr;
   if (!src) return fail(MSW_ERR_INVALID, std::string("unknown buffer ") + name);
-  // copy rows (internal -> graph numbering), trimming the FP padding to F
   if (!P->identity) return fail(MSW_ERR_UNSUPPORTED, "debug buffers only for identity numbering");
   hipStream_t st = (hipStream_t)stream;
-  HIP_TRY(hipMemcpy2DAsync(dst, P->F * sizeof(float), src, P->FP * sizeof(float), P->F * sizeof(float),
+  HIP_TRY(hipMemcpy2DAsync(dst, P->F * sizeof(float), src, P->F * sizeof(float), P->F * sizeof(float),
                            P->N, hipMemcpyDeviceToDevice, st));
   return MSW_OK;
 }
@@ -914,7 +956,7 @@ int msw_plan_get_stats(const msw_plan* P, msw_plan_stats* s) {
   s->num_edges = P->E;
   s->num_scales = P->S;
   s->hid_features = P->F;
-  s->padded_features = P->FP;
+  s->padded_features = P->F;
   s->kernels_per_step = P->kernels_per_step;
   s->forward_calls = P->forward_calls;
   s->rollout_steps = P->rollout_steps;
