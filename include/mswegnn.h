@@ -175,12 +175,17 @@ int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
 
 /* Re-launch one kernel of the step `iters` times on `stream` (benchmark / roofline hook;
  * call after a forward or rollout: it reuses the plan's workspaces and overwrites scratch).
- *   kernel: 0 = hop (first processor on `scale`), 1 = edge MLP (same processor),
- *           2 = node projection (same processor), 3 = pooling into `scale` (scale >= 1),
- *           4 = node encoders, 5 = decoder.
+ *   kernel: 0 = middle hop (first processor on `scale`), 1 = fused edge MLP + hop 1
+ *           (same processor), 2 = mean pooling + projection into `scale` (scale >= 1),
+ *           3 = node encoders (+ projection of processor 0).
  * units_out (optional) receives {rows, edges} processed by ONE launch. */
 int msw_bench_kernel(msw_plan* plan, int32_t kernel, int32_t scale, int32_t iters,
                      int64_t* units_out, void* stream);
+
+/* Diagnostics: route per-phase timestamps of wave 0 of workgroup 0 of every launch to the
+ * device buffer `buf` (uint64[20]: {shader clock, 100 MHz clock} for phase marks 0..9).
+ * Only builds compiled with -DMSW_TRACE record anything; NULL disables. */
+int msw_set_trace(msw_plan* plan, uint64_t* buf);
 
 /* sizeof() of a descriptor struct ("msw_linear", "msw_mlp", "msw_swegnn",
  * "msw_model_desc", "msw_graph_desc", "msw_plan_stats"); -1 if unknown.  Pure host code:

@@ -24,18 +24,21 @@ def _newer(a, b):
     return not os.path.exists(b) or os.path.getmtime(a) > os.path.getmtime(b)
 
 
-def build(force=False, verbose=True):
-    os.makedirs(os.path.join(HERE, "_obj"), exist_ok=True)
+def build(force=False, verbose=True, variant=""):
+    """variant "trace": diagnostic library lib/libmswegnn_trace.so (-DMSW_TRACE)."""
+    odir = os.path.join(HERE, "_obj" + (f"_{variant}" if variant else ""))
+    extra = ["-DMSW_TRACE"] if variant == "trace" else []
+    os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     objs, cmds = [], []
     hdr_t = max(os.path.getmtime(h if os.path.isabs(h) else os.path.join(HERE, h)) for h in HDR)
     for s in SRC:
         src = os.path.join(HERE, s)
-        obj = os.path.join(HERE, "_obj", os.path.basename(s) + ".o")
+        obj = os.path.join(odir, os.path.basename(s) + ".o")
         objs.append(obj)
         stale = force or _newer(src, obj) or (os.path.exists(obj) and hdr_t > os.path.getmtime(obj))
         if stale:
-            cmds.append(["hipcc", *FLAGS, "-c", src, "-o", obj])
+            cmds.append(["hipcc", *FLAGS, *extra, "-c", src, "-o", obj])
     jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
     with ThreadPoolExecutor(jobs) as ex:  # one hipcc per translation unit, in parallel
         for cmd in cmds:
@@ -44,7 +47,7 @@ def build(force=False, verbose=True):
         for r in list(ex.map(lambda c: subprocess.run(c, check=False), cmds)):
             if r.returncode != 0:
                 raise subprocess.CalledProcessError(r.returncode, r.args)
-    out = os.path.join(HERE, "lib", "libmswegnn.so")
+    out = os.path.join(HERE, "lib", f"libmswegnn_{variant}.so" if variant else "libmswegnn.so")
     if force or any(_newer(o, out) for o in objs):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs]
         if verbose:
@@ -54,4 +57,4 @@ def build(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, variant="trace" if "--trace" in sys.argv else "")

@@ -1,4 +1,5 @@
-// Internal interface between the host plan (plan.hip) and the gfx950 kernels (kernels.hip).
+// Internal interface between the host plan (plan.hip) and the gfx950 kernels
+// (kernels_impl.h, instantiated per F in kernels_nt*.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -10,10 +11,11 @@ constexpr int kMaxLayers = 4;
 constexpr int kRowsPerWave = 16;  // v_mfma_f32_16x16x4_f32: 16 rows (nodes / edges) per wave
 constexpr int kWaves = 4;         // waves per 256-thread block
 constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
+constexpr int kMaxScales = 8;
 
 // One packed layer of an MFMA chain.  `a_off` indexes the packed A operand
-// [tout][tin][lane][4] (floats, 16-feature tiles) in a weight blob, `b_off` a bias padded
-// to 16*tout (-1 = none).
+// [tout][tin][lane][4] (floats, 16-feature tiles) in the weight blob, `b_off` a bias
+// padded to 16*tout (-1 = none).
 struct LayerDev {
   int tin, tout;
   int a_off, b_off;
@@ -24,6 +26,14 @@ struct MlpDev {
   int n;
   LayerDev l[kMaxLayers];
 };
+
+// Weight region of one launch: blob floats [off, off+len) (len % 4 == 0) copied into LDS
+// by every workgroup before use; the operand offsets in that launch's arguments are then
+// LDS offsets (plan.hip: relocate).  F = 64 launches read the blob in place (len = 0).
+struct WReg {
+  int off, len;
+};
+template <int NT> constexpr bool kStaged = NT <= 2;
 
 // Device-resident rollout I/O record: kernels read it so that one captured step graph
 // can be replayed for every time step and every rollout call.
@@ -36,91 +46,132 @@ struct RolloutIO {
   int step;         // current step, advanced by the encoder kernel of each step
 };
 
-struct EncodeArgs {
-  const float* x;      // [N][nnf] rows; row of internal node i is perm ? perm[i] : i
-  const int* perm;
-  int N, nnf, nstat_raw, with_wl, dyn;
-  MlpDev stat, dynm;
-  const float* W;
-  float* xs;  // [N][F]
-  float* xd;  // [N][F]
-  int xd_rows;  // dynamic encoder only needed for the first `xd_rows` internal rows
-  RolloutIO* io;  // non-null in rollout mode: advance io->step
-  int prelu_only; // every MLP activation is PReLU: compile-time activation kernel
-};
-
-struct RowMlpArgs {
-  int mode;  // 0: edge encoder chain (<= 16 raw features -> F ... -> F); 1: one F -> 2F layer
-  const float* in; int in_stride, in_dim;
-  int R;
-  MlpDev m;
-  const float* W;
-  float* out; int out_stride, out_tiles;
-};
-
-// Node-side part of a SWEGNN layer's first edge-MLP layer and filter 0.  Output tiles are
-// enumerated [U (h1t) | V (h1t) | O (T)]; blockIdx.y selects a pair of them.
-struct NodeProjArgs {
-  int r0, R;                 // internal rows [r0, r0+R)
-  const float* xs;           // [N][F]
-  const float* xin;          // [N][F] or null (zeros)
-  int a_u, a_v, a_o;         // packed operand offsets (-1 = output not wanted)
-  const float* W;
-  float* U; float* V;        // [N][16*h1t]
-  float* O;                  // [N][F]
-  int h1t;                   // 16-feature tiles of U / V
-};
-
-struct EdgeMlpArgs {
-  int E;
-  const int* src; const int* dst;  // CSR order
-  const float* U; const float* V;  // [N][16*h1t]
-  const float* Pe;                 // [E][16*h1t] (edge part of layer 1 incl. its bias) or null
-  const float* b1;                 // layer-1 bias [16*h1t] used when Pe is null
+// Node projection of one SWEGNN layer from [x_s ; x_in] of a node tile:
+//   U = W1[:, x_s(row) | x_d(row)] [x_s; x_in]   (gnn.py:414-417, row = source node)
+//   V = W1[:, x_s(col) | x_d(col)] [x_s; x_in]   (col = receiving node)
+//   O = filter_matrix[0] x_in                    (gnn.py:401-402; identity without filter)
+// An offset < 0 = that output is not produced.
+struct NpDesc {
+  int a_u, a_v, a_o;
   int h1t;
-  int act1; float slope1;
-  MlpDev rest;                     // layers 2..L (offsets relative to W)
-  const float* W;                  // blob base of `rest` (staged to LDS)
-  int w_count;                     // floats of W to stage
-  int normalize;
-  int prelu_only;
-  float* s;                        // [E][F]
+  float* U; float* V; float* O;
 };
 
-struct HopArgs {
-  int n0, R;               // destination rows [n0, n0+R)
-  const int* rowptr;       // [R+1] into src / s
-  const int* src;
-  const float* s;          // [E][F]
-  const float* in;         // [N][F]
-  float* out;              // [N][F]
-  const float* A;          // packed filter W_{k+1} [T][T] operand, or null (no filter)
-  const float* skip;       // [N][F] or null
-  int own_zero;            // destination rows read as zero (intra_scale_gnn fine rows)
-  int grad, upwind, post_act; float post_slope;
-};
-
-struct PoolArgs {
-  int n0, R;
-  const int* rowptr;
-  const int* child;
-  const float* in;
-  float* out;
-};
-
-struct DecodeArgs {
-  int N, nnf, dyn, p;
-  const float* xup;        // [N][F]
+// Decoder + rollout bookkeeping for a node tile (gnn.py:335-348, models.py:50-91,
+// dataset.py:486-529, train.py:88-95).
+struct DecDesc {
+  int on;
   int pre_act; float pre_slope;
   MlpDev dec;
-  const float* W;
-  const float* resw;       // [p][2] or null
-  float* X;                // state rows (residual source); internal rows, or external via perm
-  const int* perm;         // internal -> graph numbering
-  float* y;                // forward mode: [N][2] graph numbering (null in rollout mode)
-  RolloutIO* io;           // rollout mode
-  const int* bc_slot;      // [N] internal -> BC row or -1
-  int prelu_only;
+  int resw_off;            // [p][2] residual matrix in the blob, -1 = none
+  const float* X;          // residual source: rollout state (internal rows) or forward input
+  int x_internal;          // X rows are internal (rollout) or graph rows (forward, via perm)
+  float* y;                // forward mode: [N][2] graph numbering
+  RolloutIO* io;           // rollout mode (X internal rows, updated in place)
+  const int* bc_slot;      // [Npad] internal -> BC row or -1
+};
+
+struct Common {
+  const float* W;          // weight blob
+  const int* perm;         // internal -> graph numbering (-1 = padding row)
+  int nnf, dyn, p, nstat_raw, with_wl;
+  int prelu;               // every MLP activation is PReLU (compile-time activation path)
+  unsigned long long* trace;  // diagnostic builds (-DMSW_TRACE): per-phase timestamps of wave 0
+};
+
+// Encoder.  Scale ranges start at multiples of 64 rows, so a workgroup has one scale.
+struct EncodeArgs {
+  Common c;
+  WReg reg;                // static encoder (every scale)
+  WReg sreg[kMaxScales];   // + per scale: dynamic encoder & projection 0 (s = 0), unpool V
+  int lds_floats;          // max over s of reg.len + sreg[s].len
+  const float* x;          // input rows (forward: graph rows via perm; rollout: X)
+  int x_internal;
+  int Npad;
+  int S;
+  int n0[kMaxScales + 1];  // padded scale starts, n0[S] = Npad
+  int ns[kMaxScales];      // valid rows per scale
+  MlpDev stat, dynm;
+  float* xs;               // [Npad][F]
+  float* xd;               // [Npad][F] (scale-0 rows)
+  NpDesc np0;              // projection of processor 0 (scale 0, x_in = x_d)
+  int vu_a[kMaxScales];    // unpool V (x_s part) for fine rows of level s, -1 = none
+  int vu_h1t;
+  float* Vu;
+  RolloutIO* io;           // rollout mode: advance io->step
+};
+
+// Edge tile: whole destination neighbourhoods, <= 16 edges and <= 16 destinations.
+struct TileRange {
+  int node0, nnode, edge0, nedge;  // local node index / local CSR edge index
+};
+
+struct Epilogue {
+  int post_act; float post_slope;  // GNN: gnn_activation after every SWEGNN layer
+  NpDesc np;                       // projection of the next layer from [x_s; out]
+  int uu_a; int uu_h1t; float* Uu; // unpool U from [x_s; out] (coarse rows)
+  DecDesc dec;
+};
+
+// Fused: edge MLP (s_ij for every edge, stored for the later hops) + hop 1
+// (+ epilogue when the layer has K = 1; intra-scale unpooling is such a layer).
+struct EdgeHopArgs {
+  Common c;
+  WReg reg;
+  int n0;                          // first internal row of the destination scale
+  const TileRange* tiles; int ntiles;
+  const int* rowptr;               // [ns+1] local CSR (by destination)
+  const int* src;                  // [E] internal ids (CSR order)
+  const int* dst;                  // [E] internal ids (CSR order)
+  const float* xs;
+  const float* U; const float* V;  // [Npad][16*h1t]
+  const float* Pe;                 // [E][16*h1t] or null (then bias b1_off)
+  int b1_off;
+  int h1t;
+  int act1; float slope1;
+  MlpDev rest;                     // layers 2..L
+  int normalize;
+  float* s;                        // [E][F] (null: not needed later)
+  const float* in;                 // out_0 rows [Npad][F]
+  int own_zero;                    // destination rows read as zero (intra_scale_gnn)
+  int grad, upwind;
+  int filt_a;                      // packed filter W_1, -1 = none
+  const float* skip;               // + skip rows (unpool), or null
+  float* out;                      // out_1 rows, or null
+  int last;                        // last hop of the layer: run the epilogue
+  Epilogue epi;
+};
+
+// Hops 2..K over the same edge tiles as the fused first hop.
+struct HopArgs {
+  Common c;
+  WReg reg;
+  int n0;                  // first internal row of the scale
+  const TileRange* tiles; int ntiles;
+  const int* rowptr;       // [ns+1] local CSR into src / dst / s
+  const int* src;
+  const int* dst;
+  const float* s;          // [E][F]
+  const float* xs;
+  const float* in;         // [Npad][F]
+  float* out;              // [Npad][F]
+  int filt_a;              // packed filter W_{k+1}, -1 = none
+  int grad, upwind;
+  int last;
+  Epilogue epi;
+};
+
+// Mean pooling into the coarse rows + projection of the next processor.
+struct PoolArgs {
+  Common c;
+  WReg reg;
+  int n0;                  // first internal row of the coarse scale
+  const TileRange* tiles; int ntiles;  // tiles of coarse nodes / their children
+  const int* rowptr;       // [ns+1] local, by coarse node
+  const int* child;
+  const float* in;         // x_down
+  const float* xs;
+  NpDesc np;
 };
 
 struct InitArgs {
@@ -137,17 +188,26 @@ struct SlotArgs {
   int row[kSlotBatch];
   int val[kSlotBatch];
 };
+
+struct RowMlpArgs {
+  int mode;  // 0: edge encoder chain (<= 16 raw features -> F ... -> F); 1: one F -> 2F layer
+  const float* in; int in_stride, in_dim;
+  int R;
+  MlpDev m;
+  const float* W;
+  float* out; int out_stride, out_tiles;
+};
+
 hipError_t launch_set_slots(const SlotArgs& a, hipStream_t st);
 hipError_t launch_set_io(RolloutIO* dst, const RolloutIO& v, hipStream_t st);
+hipError_t launch_init_state(const InitArgs& a, hipStream_t st);
 
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
+template <int NT> hipError_t prepare_kernels();
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
-template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);
-template <int NT> hipError_t launch_node_proj(const NodeProjArgs& a, hipStream_t st);
-template <int NT> hipError_t launch_edge_mlp(const EdgeMlpArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
-template <int NT> hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
-hipError_t launch_init_state(const InitArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);
 
 }  // namespace msw

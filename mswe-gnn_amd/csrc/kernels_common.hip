@@ -10,6 +10,7 @@ __global__ __launch_bounds__(kBlock) void k_init_state(InitArgs a) {
   if (n == 0) a.io->step = -1;
   if (n >= a.N) return;
   const int ext = a.perm ? a.perm[n] : n;
+  if (ext < 0) return;  // padding row of the 16-aligned internal numbering
   float* xr = a.X + (size_t)n * a.nnf;
   const float* src = a.x0 + (size_t)ext * a.nnf;
   for (int k = 0; k < a.nnf; ++k) xr[k] = src[k];

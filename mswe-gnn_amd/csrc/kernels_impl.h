@@ -5,15 +5,18 @@
 //  * every F-wide node / edge vector is fp32, row-major, unpadded (stride F).
 //  * A wave owns 16 ROWS (nodes or edges).  Lane l works on row j = l & 15 and, in lane
 //    group g = l >> 4, holds features 16t + 4g + r (r = 0..3) of every 16-feature tile t
-//    in one f32x4 per tile.  That is exactly the accumulator layout of
-//    v_mfma_f32_16x16x4_f32 with the row on the MFMA column (C/D: col = l & 15,
-//    row = 4(l >> 4) + r) and, register for register, the B operand of the next layer
-//    (k-step (t, r): lane group g supplies feature 16t + 4g + r).  Layers chain in
-//    registers: no LDS, no lane shuffles between layers.  Packed A operand:
-//    A[to][ti][lane][r] = W[16 to + (l & 15)][16 ti + 4 (l >> 4) + r] (host: plan.hip).
+//    in one f32x4 per tile.  That is the accumulator layout of v_mfma_f32_16x16x4_f32 with
+//    the row on the MFMA column (C/D: col = l & 15, row = 4(l >> 4) + r) and, register
+//    for register, the B operand of the next layer (k-step (t, r): lane group g supplies
+//    feature 16t + 4g + r).  Layers chain in registers: no shuffles between layers; the
+//    A operands (weights) of a launch are staged once per workgroup in LDS.  Packed A operand: A[to][ti][lane][r] = W[16 to + (l & 15)][16 ti + 4 (l >> 4) + r].
 //  * f32 in / f32 accumulate MFMA = exact fp32 fma chains (no TF32 on gfx950).
-//  * message passing pulls over CSR-by-destination, 16 destination rows per wave, 16-byte
-//    loads; sums run in the reference's edge order; no atomics (bit-reproducible).
+//  * message passing runs on edge tiles (whole destination neighbourhoods, <= 16 edges):
+//    one lane per edge computes its message, the destination lane sums them from LDS in
+//    the reference's edge order -- no atomics, bit-reproducible run to run.
+//  * one rollout step = encoder (+ projection of processor 0) -> per processor: fused
+//    edge-MLP+hop-1, hops 2..K (the last with an epilogue: next projection / unpool
+//    projection / decoder + rollout update) -> pooling+projection / unpooling+projection.
 #pragma once
 #include "engine.h"
 
@@ -29,6 +32,7 @@ constexpr int kBlock = 64 * kWaves;
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 __device__ __forceinline__ float hsum(f32x4 v) { return (v.x + v.y) + (v.z + v.w); }
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 // sum over the 4 lane groups holding one row (lanes j, j+16, j+32, j+48)
 __device__ __forceinline__ float row_sum(float v) {
@@ -37,15 +41,19 @@ __device__ __forceinline__ float row_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ int wave_row0() { return (blockIdx.x * kWaves + wave_id()) * kRowsPerWave; }
+
+// activation_functions, models/models.py:149-169
 template <int ACT>
 __device__ __forceinline__ float act_static(float x, float slope) {
-  if constexpr (ACT == 1) return x > 0.f ? x : slope * x;
-  else if constexpr (ACT == 2) return x > 0.f ? x : 0.f;
-  else if constexpr (ACT == 3) return x > 0.f ? x : 0.1f * x;
-  else if constexpr (ACT == 4) return x > 0.f ? x : expm1f(x);
-  else if constexpr (ACT == 5) return x / (1.f + expf(-x));
-  else if constexpr (ACT == 6) return 1.f / (1.f + expf(-x));
-  else if constexpr (ACT == 7) return tanhf(x);
+  if constexpr (ACT == 1) return x > 0.f ? x : slope * x;       // PReLU
+  else if constexpr (ACT == 2) return x > 0.f ? x : 0.f;        // ReLU
+  else if constexpr (ACT == 3) return x > 0.f ? x : 0.1f * x;   // LeakyReLU(0.1)
+  else if constexpr (ACT == 4) return x > 0.f ? x : expm1f(x);  // ELU
+  else if constexpr (ACT == 5) return x / (1.f + expf(-x));     // SiLU
+  else if constexpr (ACT == 6) return 1.f / (1.f + expf(-x));   // Sigmoid
+  else if constexpr (ACT == 7) return tanhf(x);                 // Tanh
   else return x;
 }
 template <int ACT, int N>
@@ -55,8 +63,8 @@ __device__ __forceinline__ void act_tiles_static(f32x4 (&v)[N], float slope) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[t][r] = act_static<ACT>(v[t][r], slope);
 }
-// Activation on whole register tiles.  ACT >= 0: fixed at compile time (the PReLU kernels of
-// every shipped configuration); ACT < 0: one wave-uniform switch outside the element loops.
+// ACT >= 0: activation fixed at compile time (PReLU kernels of the shipped configs);
+// ACT < 0: one wave-uniform switch outside the element loops.
 template <int ACT, int N>
 __device__ __forceinline__ void act_tiles(f32x4 (&v)[N], int act, float slope) {
   if constexpr (ACT >= 0) {
@@ -75,16 +83,15 @@ __device__ __forceinline__ void act_tiles(f32x4 (&v)[N], int act, float slope) {
   }
 }
 
-// One nn.Linear (+ bias, + activation) on register tiles, compile-time shape TIN -> TOUT
-// (make_mlp layer, models/models.py:121-146).  The TOUT accumulators are independent
-// chains interleaved per k-step (hides the 40-cycle dependent MFMA latency).
-template <int TIN, int TOUT, int ACT>
-__device__ __forceinline__ void mfma_layer(const f32x4 (&in)[TIN], f32x4 (&out)[TOUT],
-                                           const float* __restrict__ A, const float* __restrict__ b,
-                                           int act, float slope, int lane, int g) {
-  f32x4 acc[TOUT];
+// acc[to] = sum_ti A[to][ti] in[ti]; A packed [TOUT][TIN].  Shapes are compile-time only:
+// a run-time bound here puts a branch after every MFMA (accumulator read-back + s_nop),
+// which measured ~130 cycles per 32-cycle MFMA.  The TOUT accumulators are independent
+// chains interleaved per k-step (40-cycle dependent MFMA latency).
+template <int TIN, int TOUT>
+__device__ __forceinline__ void proj(const f32x4 (&in)[TIN], f32x4 (&acc)[TOUT],
+                                     const float* __restrict__ A, int lane) {
 #pragma unroll
-  for (int to = 0; to < TOUT; ++to) acc[to] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int to = 0; to < TOUT; ++to) acc[to] = zero4();
 #pragma unroll
   for (int ti = 0; ti < TIN; ++ti) {
     f32x4 w[TOUT];
@@ -95,99 +102,550 @@ __device__ __forceinline__ void mfma_layer(const f32x4 (&in)[TIN], f32x4 (&out)[
 #pragma unroll
       for (int to = 0; to < TOUT; ++to) acc[to] = MSW_MFMA(w[to][r], in[ti][r], acc[to]);
   }
-  if (b) {
+}
+
+// nn.Linear (+ bias, + activation), compile-time shape TIN -> TOUT (make_mlp layer,
+// models/models.py:121-146).
+template <int TIN, int TOUT, int ACT>
+__device__ __forceinline__ void mfma_layer(const f32x4 (&in)[TIN], f32x4 (&out)[TOUT],
+                                           const LayerDev& L, const float* __restrict__ W,
+                                           int lane, int g) {
+  f32x4 acc[TOUT];
+  proj<TIN, TOUT>(in, acc, W + L.a_off, lane);
 #pragma unroll
-    for (int to = 0; to < TOUT; ++to) acc[to] = acc[to] + ld4(b + 16 * to + 4 * g);
-  }
-  act_tiles<ACT, TOUT>(acc, act, slope);
+  for (int to = 0; to < TOUT; ++to) acc[to] = acc[to] + ld4(W + L.b_off + 16 * to + 4 * g);  // zeros if bias=False
+  act_tiles<ACT, TOUT>(acc, L.act, L.slope);
 #pragma unroll
   for (int to = 0; to < TOUT; ++to) out[to] = acc[to];
 }
 
-template <int TIN, int TOUT, int ACT = -1>
-__device__ __forceinline__ void run_layer(const f32x4 (&in)[TIN], f32x4 (&out)[TOUT],
-                                          const LayerDev& L, const float* __restrict__ W,
-                                          int lane, int g) {
-  mfma_layer<TIN, TOUT, ACT>(in, out, W + L.a_off, L.b_off >= 0 ? W + L.b_off : nullptr, L.act,
-                        L.slope, lane, g);
-}
-
-// make_mlp chain IN0 -> T -> ... -> T -> TL: the layer count m.n is a run-time value, every
+// make_mlp chain IN0 -> T -> ... -> T -> TL: the layer count is a run-time value, every
 // layer's shape is fixed at compile time (first IN0->T, or IN0->TL if m.n == 1; middle
 // T->T; last T->TL), so all register arrays are statically indexed.
-template <int IN0, int T, int TL, int ACT = -1>
+template <int IN0, int T, int TL, int ACT>
 __device__ __forceinline__ void run_mlp(const f32x4 (&in)[IN0], f32x4 (&out)[TL], const MlpDev& m,
                                         const float* __restrict__ W, int lane, int g) {
   if (m.n == 1) {
-    run_layer<IN0, TL, ACT>(in, out, m.l[0], W, lane, g);
+    mfma_layer<IN0, TL, ACT>(in, out, m.l[0], W, lane, g);
     return;
   }
   f32x4 h[T];
-  run_layer<IN0, T, ACT>(in, h, m.l[0], W, lane, g);
+  mfma_layer<IN0, T, ACT>(in, h, m.l[0], W, lane, g);
   for (int li = 1; li + 1 < m.n; ++li) {
     f32x4 h2[T];
-    run_layer<T, T, ACT>(h, h2, m.l[li], W, lane, g);
+    mfma_layer<T, T, ACT>(h, h2, m.l[li], W, lane, g);
 #pragma unroll
     for (int t = 0; t < T; ++t) h[t] = h2[t];
   }
-  run_layer<T, TL, ACT>(h, out, m.l[m.n - 1], W, lane, g);
+  mfma_layer<T, TL, ACT>(h, out, m.l[m.n - 1], W, lane, g);
 }
 
-__device__ __forceinline__ int wave_row0() {
-  return (blockIdx.x * kWaves + (threadIdx.x >> 6)) * kRowsPerWave;
+template <int N>
+__device__ __forceinline__ void load_row(f32x4 (&v)[N], const float* row, int g) {
+#pragma unroll
+  for (int t = 0; t < N; ++t) v[t] = ld4(row + 16 * t + 4 * g);
+}
+template <int N>
+__device__ __forceinline__ void store_row(float* row, const f32x4 (&v)[N], int ntiles, int g) {
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+    if (t < ntiles) st4(row + 16 * t + 4 * g, v[t]);
 }
 
-// ---------------------------------------------------------------------------- encoders
-// Static / dynamic node encoders incl. the water-level feature
-// (MSGNN.forward models/gnn.py:284-294, GNN.forward :112-123).
+// ---------------------------------------------------------------------------- epilogues
+// Projection of a SWEGNN layer (U, V, O) from [x_s ; x_in] of a node tile; H1T = tiles of
+// the first edge-MLP layer (2F, or F for one-layer MLPs).
+template <int NT, int H1T>
+__device__ __forceinline__ void np_project_t(const f32x4 (&xs)[NT], const f32x4 (&xin)[NT],
+                                             const NpDesc& d, const float* W, size_t n, bool valid,
+                                             int lane, int g) {
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  f32x4 in[T2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    in[t] = xs[t];
+    in[NT + t] = xin[t];
+  }
+  if (d.a_u >= 0) {
+    f32x4 acc[H1T];
+    proj<T2, H1T>(in, acc, W + d.a_u, lane);
+    if (valid) store_row<H1T>(d.U + n * (16 * H1T), acc, H1T, g);
+  }
+  if (d.a_v >= 0) {
+    f32x4 acc[H1T];
+    proj<T2, H1T>(in, acc, W + d.a_v, lane);
+    if (valid) store_row<H1T>(d.V + n * (16 * H1T), acc, H1T, g);
+  }
+  if (d.a_o >= 0) {
+    f32x4 acc[NT];
+    proj<NT, NT>(xin, acc, W + d.a_o, lane);
+    if (valid) store_row<NT>(d.O + n * F, acc, NT, g);
+  }
+}
+template <int NT>
+__device__ __forceinline__ void np_project(const f32x4 (&xs)[NT], const f32x4 (&xin)[NT],
+                                           const NpDesc& d, const float* W, size_t n, bool valid,
+                                           int lane, int g) {
+  if (d.h1t == 2 * NT)
+    np_project_t<NT, 2 * NT>(xs, xin, d, W, n, valid, lane, g);
+  else
+    np_project_t<NT, NT>(xs, xin, d, W, n, valid, lane, g);
+}
+
+// U (or V) = W[:, blocks] [x_s ; x] with H1T output tiles, TIN input tiles.
+template <int TIN, int H1T, int NT>
+__device__ __forceinline__ void side_proj_t(const f32x4 (&in)[TIN], const float* A, float* dst, size_t n,
+                                            bool valid, int lane, int g) {
+  f32x4 acc[H1T];
+  proj<TIN, H1T>(in, acc, A, lane);
+  if (valid) store_row<H1T>(dst + n * (16 * H1T), acc, H1T, g);
+}
+template <int TIN, int NT>
+__device__ __forceinline__ void side_proj(const f32x4 (&in)[TIN], int h1t, const float* A, float* dst,
+                                          size_t n, bool valid, int lane, int g) {
+  if (h1t == 2 * NT)
+    side_proj_t<TIN, 2 * NT, NT>(in, A, dst, n, valid, lane, g);
+  else
+    side_proj_t<TIN, NT, NT>(in, A, dst, n, valid, lane, g);
+}
+
+// tanh(x_up) -> node_decoder -> + learned residual -> ReLU -> small-depth mask
+// (gnn.py:335-348, models.py:50-91); rollout mode: use_prediction + BC of the next step
+// (dataset.py:486-529) and the rollout write (train.py:88-95).
+template <int NT, int ACT>
+__device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDesc& d,
+                                            const Common& c, int n, bool valid, int lane, int g) {
+#pragma clang fp contract(off)
+  f32x4 x0[NT], o[1];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) x0[t] = xup[t];
+  act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
+  run_mlp<NT, NT, 1, ACT>(x0, o, d.dec, c.W, lane, g);
+  if (!valid || g) return;  // lane group 0 holds output features 0 (h) and 1 (|q|)
+  const int ext = c.perm ? c.perm[n] : n;
+  if (ext < 0) return;
+  const float* xr = d.X + (size_t)(d.x_internal ? n : ext) * c.nnf;
+  const int nstat = c.nnf - c.dyn;
+  float h = o[0].x, v = o[0].y;
+  if (d.resw_off >= 0) {
+    const float* rw = c.W + d.resw_off;
+    float rh = xr[nstat] * rw[0];
+    float rv = xr[nstat + 1] * rw[1];
+    for (int tau = 1; tau < c.p; ++tau) {
+      rh = rh + xr[nstat + 2 * tau] * rw[2 * tau];
+      rv = rv + xr[nstat + 2 * tau + 1] * rw[2 * tau + 1];
+    }
+    h = h + rh;
+    v = v + rv;
+  }
+  h = h > 0.f ? h : 0.f;  // torch.relu
+  v = v > 0.f ? v : 0.f;
+  const float hm = h * (fabsf(h) > 1e-4f ? 1.f : 0.f);  // _mask_small_WD(epsilon=1e-4)
+  const float vm = v * (h != 0.f ? 1.f : 0.f);
+  if (!d.io) {
+    d.y[(size_t)ext * 2 + 0] = hm;
+    d.y[(size_t)ext * 2 + 1] = vm;
+    return;
+  }
+  RolloutIO* io = d.io;
+  const int t = io->step;
+  io->out[((size_t)ext * 2 + 0) * io->T + t] = hm;
+  io->out[((size_t)ext * 2 + 1) * io->T + t] = vm;
+  float* xw = const_cast<float*>(xr);
+  for (int k = 0; k + 2 < c.dyn; ++k) xw[nstat + k] = xw[nstat + k + 2];
+  xw[c.nnf - 2] = hm;
+  xw[c.nnf - 1] = vm;
+  const int b = d.bc_slot ? d.bc_slot[n] : -1;
+  if (b >= 0 && t + 1 < io->bc_tstride) {
+    for (int tau = 0; tau < c.p; ++tau)
+      xw[nstat + (io->type_bc - 1) + 2 * tau] = io->bc[((size_t)b * c.p + tau) * io->bc_tstride + t + 1];
+  }
+}
+
+// What follows the last hop of a SWEGNN layer, on the layer's destination rows.
+template <int NT, int ACT>
+__device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& e, const Common& c,
+                                              const float* xs_rows, float* out, int n,
+                                              bool valid, int lane, int g) {
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
+  if (out && valid) store_row<NT>(out + (size_t)n * F, res, NT, g);
+  const bool np = e.np.a_u >= 0 || e.np.a_v >= 0 || e.np.a_o >= 0;
+  if (np || e.uu_a >= 0) {
+    f32x4 xs[NT];
+    load_row<NT>(xs, xs_rows + (size_t)n * F, g);
+    if (np) np_project<NT>(xs, res, e.np, c.W, n, valid, lane, g);
+    if (e.uu_a >= 0) {
+      f32x4 in[T2];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        in[t] = xs[t];
+        in[NT + t] = res[t];
+      }
+      side_proj<T2, NT>(in, e.uu_h1t, c.W + e.uu_a, e.Uu, n, valid, lane, g);
+    }
+  }
+  if (e.dec.on) decode_rows<NT, ACT>(res, e.dec, c, n, valid, lane, g);
+}
+
+// ---------------------------------------------------------------------------- tracing
+// Diagnostic builds only (-DMSW_TRACE, tools/trace_kernels.py): wave 0 of workgroup 0 drains
+// its memory counters and records {shader clock, 100 MHz clock} at each phase mark, so the
+// dependent-latency chain of one launch can be read phase by phase.
+#ifdef MSW_TRACE
+#define MSW_MARK(c, k)                                                          \
+  do {                                                                          \
+    if ((c).trace && blockIdx.x == 0 && threadIdx.x < 64) {                     \
+      __builtin_amdgcn_s_waitcnt(0);                                            \
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();               \
+      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();           \
+      if (threadIdx.x == 0) { (c).trace[2 * (k)] = t0; (c).trace[2 * (k) + 1] = t1; } \
+    }                                                                           \
+  } while (0)
+#else
+#define MSW_MARK(c, k) \
+  do {                 \
+  } while (0)
+#endif
+
+// ---------------------------------------------------------------------------- staging
+// Copy a launch's weight region into LDS (all threads; one batch of independent 16-B loads,
+// so the whole MLP chain then waits on one memory latency instead of one per layer).
+__device__ __forceinline__ void stage_region(float* smem, int dst, const float* __restrict__ W, WReg r) {
+#pragma unroll 4
+  for (int i = 4 * (int)threadIdx.x; i < r.len; i += 4 * kBlock) st4(smem + dst + i, ld4(W + r.off + i));
+}
+
+// ---------------------------------------------------------------------------- encoder
+// Static / dynamic node encoders incl. the water-level feature (MSGNN.forward
+// gnn.py:284-294, GNN.forward :112-123) + projection of processor 0 + the x_s part of
+// every unpooling layer's V.  One workgroup = 64 rows of one scale.
 template <int NT, int ACT>
 __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
   constexpr int F = 16 * NT;
-  const int lane = threadIdx.x & 63, g = lane >> 4;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  MSW_MARK(a.c, 0);
   if (a.io && blockIdx.x == 0 && threadIdx.x == 0) a.io->step += 1;
-  const int r0 = wave_row0();
-  if (r0 >= a.N) return;
-  const int node = r0 + (lane & 15);
-  const bool valid = node < a.N;
-  const float* xr = a.x + (size_t)(a.perm ? a.perm[valid ? node : 0] : (valid ? node : 0)) * a.nnf;
-  f32x4 A[NT];
-  // static input [x_s, WL = DEM + h_t] in tile 0: lane group g holds features 4g..4g+3
-  {
-    f32x4 v;
+  const int rb = blockIdx.x * kRowsPerBlock;
+  int s = 0;
+  while (s + 1 < a.S && rb >= a.n0[s + 1]) ++s;
+  const int n = wave_row0() + j;
+  const bool valid = (n - a.n0[s]) < a.ns[s];
+  const int ext = a.c.perm ? a.c.perm[n] : n;
+  const int xrow = a.x_internal ? (valid ? n : a.n0[s]) : (valid ? ext : 0);
+  const float* xr = a.x + (size_t)xrow * a.c.nnf;
+  const int nstat = a.c.nstat_raw;
+  float raw[4], dyn[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 4 * g + r;
-      float val = 0.f;
-      if (f < a.nstat_raw) val = xr[f];
-      else if (a.with_wl && f == a.nstat_raw) val = xr[a.nstat_raw - 1] + xr[a.nnf - 2];
-      v[r] = val;
-    }
-    const f32x4 in[1] = {v};
-    run_mlp<1, NT, NT, ACT>(in, A, a.stat, a.W, lane, g);
-    if (valid) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.xs + (size_t)node * F + 16 * t + 4 * g, A[t]);
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int f = 4 * g + r;
+    raw[r] = f < nstat ? xr[f] : 0.f;
+    dyn[r] = f < a.c.dyn ? xr[nstat + f] : 0.f;
   }
-  if (r0 >= a.xd_rows) return;
+  const float wlv = xr[nstat - 1] + xr[a.c.nnf - 2];  // water level = bed elevation + depth
+  Common c = a.c;
+  MSW_MARK(c, 1);
+  if constexpr (kStaged<NT>) {
+    stage_region(smem, 0, a.c.W, a.reg);
+    stage_region(smem, a.reg.len, a.c.W, a.sreg[s]);
+    __syncthreads();
+    c.W = smem;
+  }
+  MSW_MARK(c, 2);
+  f32x4 xs[NT];
   {
     f32x4 v;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 4 * g + r;
-      v[r] = f < a.dyn ? xr[a.nstat_raw + f] : 0.f;
-    }
+    for (int r = 0; r < 4; ++r) v[r] = (c.with_wl && 4 * g + r == nstat) ? wlv : raw[r];
     const f32x4 in[1] = {v};
-    run_mlp<1, NT, NT, ACT>(in, A, a.dynm, a.W, lane, g);
-    if (valid && node < a.xd_rows) {
+    run_mlp<1, NT, NT, ACT>(in, xs, a.stat, c.W, lane, g);
+    if (valid) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
+  }
+  MSW_MARK(c, 5);
+  if (s == 0) {
+    f32x4 xd[NT];
+    const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
+    run_mlp<1, NT, NT, ACT>(in, xd, a.dynm, c.W, lane, g);
+    if (valid && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
+    MSW_MARK(c, 6);
+    np_project<NT>(xs, xd, a.np0, c.W, n, valid, lane, g);
+  }
+  MSW_MARK(c, 8);
+  if (a.vu_a[s] >= 0) side_proj<NT, NT>(xs, a.vu_h1t, c.W + a.vu_a[s], a.Vu, n, valid, lane, g);
+  MSW_MARK(c, 9);
+}
+
+// ---------------------------------------------------------------------------- message passing
+// One wave = one tile of whole destination neighbourhoods (<= 16 edges, <= 16 nodes):
+// lane j is edge tr.edge0 + j in the edge phase and node tr.node0 + j in the node phase;
+// the messages cross lanes through the wave's LDS slab (no atomics, reference edge order).
+struct TileLanes {
+  bool ev, anye, nv;
+  int e, ln, n, q0, q1;
+  size_t sr, dc;
+};
+__device__ __forceinline__ TileLanes tile_lanes(const TileRange& tr, int j, int n0, const int* __restrict__ src,
+                                                const int* __restrict__ dst, const int* __restrict__ rowptr) {
+  TileLanes t;
+  t.ev = j < tr.nedge;
+  t.anye = tr.nedge > 0;
+  // an edge-less tile still runs the (discarded) edge math on edge 0 / node n0, so the wave
+  // stays converged without indexing past the edge arrays
+  t.e = t.anye ? tr.edge0 + (t.ev ? j : 0) : 0;
+  t.sr = t.anye ? (size_t)src[t.e] : (size_t)n0;
+  t.dc = t.anye ? (size_t)dst[t.e] : (size_t)n0;
+  t.nv = j < tr.nnode;
+  t.ln = tr.node0 + (t.nv ? j : 0);
+  t.n = n0 + t.ln;
+  t.q0 = rowptr[t.ln] - tr.edge0;
+  t.q1 = t.nv ? rowptr[t.ln + 1] - tr.edge0 : t.q0;
+  return t;
+}
+
+// msg_e = active(e) * (out[col] - out[row]) * s_e  (or s_e * out[row])   (gnn.py:406-435)
+template <int NT>
+__device__ __forceinline__ void put_message(float* slab_row, const f32x4 (&os)[NT], const f32x4 (&od)[NT],
+                                            const f32x4 (&sv)[NT], bool ev, int grad, int upwind, int g) {
+#pragma clang fp contract(off)
+  float rs = 0.f, rd = 0.f;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.xd + (size_t)node * F + 16 * t + 4 * g, A[t]);
+  for (int t = 0; t < NT; ++t) {
+    rs += hsum(os[t]);
+    rd += hsum(od[t]);
+  }
+  const bool act = (row_sum(rs) != 0.f) || (row_sum(rd) != 0.f);  // gnn.py:408-411
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f32x4 gv;
+    if (grad) {
+      gv = od[t] - os[t];  // out[col] - out[row]
+      if (upwind) {
+        gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
+        gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
+      }
+    } else {
+      gv = os[t];          // s_ij * out[row]
     }
+    const f32x4 m = gv * sv[t];
+    st4(slab_row + 16 * t + 4 * g, (ev && act) ? m : zero4());
   }
 }
 
-// Plan-time per-row MLPs.  MODE 0: edge encoder chain (raw <= 16 features -> F -> ... -> F);
-// MODE 1: edge part of a SWEGNN layer's first layer, Pe = W1[:, 4F:] e + b1 (F -> h1t tiles).
+// Node phase: agg = sum of the node's messages (edge order), out' = base + W agg [+ skip].
+template <int NT>
+__device__ __forceinline__ void gather_messages(f32x4 (&agg)[NT], const float* slab, int q0, int q1, int g) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int t = 0; t < NT; ++t) agg[t] = zero4();
+  for (int q = q0; q < q1; ++q) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) agg[t] = agg[t] + ld4(slab + q * F + 16 * t + 4 * g);
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void apply_filter(f32x4 (&res)[NT], const f32x4 (&agg)[NT], int filt_a,
+                                             const float* W, int lane) {
+#pragma clang fp contract(off)
+  if (filt_a >= 0) {  // filter W_{k}; agg is already in B-operand layout
+    f32x4 acc[NT];
+    proj<NT, NT>(agg, acc, W + filt_a, lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + agg[t];
+  }
+}
+
+// ---------------------------------------------------------------------------- edge MLP + hop 1
+//  edges: s_ij = normalize(MLP(x_s[row], x_s[col], x_d[row], x_d[col], e_ij))
+//         (gnn.py:414-426; first layer pre-split: h1 = act(U[row] + V[col] + Pe[e]));
+//         computed ONCE per layer -- its inputs do not change across the K hops.
+//  nodes: out_1 = out_0 + W_1 agg [+ skip] -> store, or the epilogue when K = 1.
+template <int NT, int ACT>
+__global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  __shared__ __attribute__((aligned(16))) float msg[kWaves][kRowsPerWave][F];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int tile = blockIdx.x * kWaves + w;
+  const bool live = tile < a.ntiles;
+  MSW_MARK(a.c, 0);
+  const TileRange tr = a.tiles[live ? tile : 0];
+  Common c = a.c;
+  MSW_MARK(c, 1);
+  if constexpr (kStaged<NT>) {
+    stage_region(smem, 0, a.c.W, a.reg);
+    __syncthreads();
+    c.W = smem;
+  }
+  MSW_MARK(c, 2);
+  if (!live) return;
+  const TileLanes L = tile_lanes(tr, j, a.n0, a.src, a.dst, a.rowptr);
+  MSW_MARK(c, 3);
+  // everything the tile reads from HBM, issued together
+  const int hs = 16 * a.h1t;
+  f32x4 H[T2], os[NT], od[NT], res[NT], sk[NT];
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    if (t < a.h1t) {
+      const int off = 16 * t + 4 * g;
+      const f32x4 p = (a.Pe && L.anye) ? ld4(a.Pe + (size_t)L.e * hs + off) : ld4(c.W + a.b1_off + off);
+      H[t] = (ld4(a.U + L.sr * hs + off) + ld4(a.V + L.dc * hs + off)) + p;
+    } else {
+      H[t] = zero4();
+    }
+  }
+  load_row<NT>(os, a.in + L.sr * F, g);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    od[t] = a.own_zero ? zero4() : ld4(a.in + L.dc * F + 16 * t + 4 * g);
+    res[t] = a.own_zero ? zero4() : ld4(a.in + (size_t)L.n * F + 16 * t + 4 * g);
+    sk[t] = a.skip ? ld4(a.skip + (size_t)L.n * F + 16 * t + 4 * g) : zero4();
+  }
+  MSW_MARK(c, 4);
+  act_tiles<ACT, T2>(H, a.act1, a.slope1);
+  f32x4 sv[NT];
+  if (a.rest.n > 0) {
+    run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, c.W, lane, g);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sv[t] = H[t];
+  }
+  MSW_MARK(c, 5);
+  if (a.normalize) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+    const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 q = sv[t] / nrm;
+      q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+      q.y = (q.y == q.y) ? q.y : 0.f;
+      q.z = (q.z == q.z) ? q.z : 0.f;
+      q.w = (q.w == q.w) ? q.w : 0.f;
+      sv[t] = q;
+    }
+  }
+  if (L.ev && a.s) store_row<NT>(a.s + (size_t)L.e * F, sv, NT, g);
+  put_message<NT>(&msg[w][j][0], os, od, sv, L.ev, a.grad, a.upwind, g);
+  MSW_MARK(c, 6);
+  f32x4 agg[NT];
+  gather_messages<NT>(agg, &msg[w][0][0], L.q0, L.q1, g);
+  MSW_MARK(c, 7);
+  apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
+  MSW_MARK(c, 8);
+  if (a.skip) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + sk[t];
+  }
+  if (a.last) {
+    node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
+  } else if (L.nv && a.out) {
+    store_row<NT>(a.out + (size_t)L.n * F, res, NT, g);
+  }
+  MSW_MARK(c, 9);
+}
+
+// ---------------------------------------------------------------------------- hop
+// Hops 2..K (gnn.py:406-443) over the same tiles:
+//   active(e) = rowsum(out[src]) != 0 || rowsum(out[dst]) != 0          (gnn.py:408-411)
+//   agg[c]    = sum_e active(e) * (out[c] - out[src]) * s_e  (edge order; gnn.py:430-438)
+//   out'[c]   = out[c] + W_{k+1} agg[c]  (MFMA)  -> store, or the epilogue after hop K
+template <int NT, int ACT>
+__global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  __shared__ __attribute__((aligned(16))) float msg[kWaves][kRowsPerWave][F];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int tile = blockIdx.x * kWaves + w;
+  const bool live = tile < a.ntiles;
+  MSW_MARK(a.c, 0);
+  const TileRange tr = a.tiles[live ? tile : 0];
+  Common c = a.c;
+  MSW_MARK(c, 1);
+  if constexpr (kStaged<NT>) {
+    stage_region(smem, 0, a.c.W, a.reg);
+    __syncthreads();
+    c.W = smem;
+  }
+  MSW_MARK(c, 2);
+  if (!live) return;
+  const TileLanes L = tile_lanes(tr, j, a.n0, a.src, a.dst, a.rowptr);
+  MSW_MARK(c, 3);
+  f32x4 os[NT], od[NT], sv[NT], res[NT];
+  load_row<NT>(os, a.in + L.sr * F, g);
+  load_row<NT>(od, a.in + L.dc * F, g);
+  load_row<NT>(sv, a.s + (size_t)L.e * F, g);
+  load_row<NT>(res, a.in + (size_t)L.n * F, g);
+  MSW_MARK(c, 4);
+  put_message<NT>(&msg[w][j][0], os, od, sv, L.ev, a.grad, a.upwind, g);
+  MSW_MARK(c, 6);
+  f32x4 agg[NT];
+  gather_messages<NT>(agg, &msg[w][0][0], L.q0, L.q1, g);
+  MSW_MARK(c, 7);
+  apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
+  MSW_MARK(c, 8);
+  if (a.last) {
+    node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
+  } else if (L.nv) {
+    store_row<NT>(a.out + (size_t)L.n * F, res, NT, g);
+  }
+  MSW_MARK(c, 9);
+}
+
+// ---------------------------------------------------------------------------- pooling
+// scatter(x[fine], coarse, reduce='mean') (gnn.py:256): children summed in edge order,
+// divided by max(count, 1); then the projection of the next processor.  Tiles of coarse
+// nodes with <= 16 children in all: lane j loads child j, the coarse lanes sum.
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  __shared__ __attribute__((aligned(16))) float msg[kWaves][kRowsPerWave][F];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int tile = blockIdx.x * kWaves + w;
+  const bool live = tile < a.ntiles;
+  MSW_MARK(a.c, 0);
+  const TileRange tr = a.tiles[live ? tile : 0];
+  Common c = a.c;
+  MSW_MARK(c, 1);
+  if constexpr (kStaged<NT>) {
+    stage_region(smem, 0, a.c.W, a.reg);
+    __syncthreads();
+    c.W = smem;
+  }
+  MSW_MARK(c, 2);
+  if (!live) return;
+  const TileLanes L = tile_lanes(tr, j, a.n0, a.child, a.child, a.rowptr);
+  MSW_MARK(c, 3);
+  f32x4 x[NT], xs[NT];
+  load_row<NT>(x, a.in + L.sr * F, g);
+  load_row<NT>(xs, a.xs + (size_t)L.n * F, g);
+  MSW_MARK(c, 4);
+  store_row<NT>(&msg[w][j][0], x, NT, g);
+  f32x4 acc[NT];
+  gather_messages<NT>(acc, &msg[w][0][0], L.q0, L.q1, g);
+  MSW_MARK(c, 7);
+  const float cnt = (float)(L.q1 - L.q0 > 0 ? L.q1 - L.q0 : 1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = acc[t] / cnt;
+  np_project<NT>(xs, acc, a.np, c.W, L.n, L.nv, lane, g);
+  MSW_MARK(c, 9);
+}
+
+// ---------------------------------------------------------------------------- plan time
+// MODE 0: edge encoder chain (raw <= 16 features -> F -> ... -> F);
+// MODE 1: edge part of a SWEGNN layer's first layer, Pe = W1[:, 4F:] e + b1 (F -> 2F).
 template <int NT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_rowmlp(RowMlpArgs a) {
   const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -209,315 +667,69 @@ __global__ __launch_bounds__(kBlock) void k_rowmlp(RowMlpArgs a) {
     in[t] = v;
   }
   if (MODE == 0)
-    run_mlp<TI, NT, TO>(in, out, a.m, a.W, lane, g);
+    run_mlp<TI, NT, TO, -1>(in, out, a.m, a.W, lane, g);
   else
-    run_layer<TI, TO>(in, out, a.m.l[0], a.W, lane, g);
-  if (valid) {
-#pragma unroll
-    for (int t = 0; t < TO; ++t)
-      if (t < a.out_tiles) st4(a.out + (size_t)row * a.out_stride + 16 * t + 4 * g, out[t]);
-  }
-}
-
-// ---------------------------------------------------------------------------- node projection
-// U = W1[:, x_s(row) | x_d(row)] [x_s; x_in] (gnn.py:414-417, row = source node)
-// V = W1[:, x_s(col) | x_d(col)] [x_s; x_in] (col = receiving node)
-// O = filter_matrix[0] x_in                  (gnn.py:401-402)
-// blockIdx.y picks two consecutive output tiles of [U | V | O]: 5x the waves of a
-// one-wave-per-row-tile kernel, a 32-MFMA chain per wave (latency, not throughput, bounds
-// these small launches).
-template <int NT>
-__global__ __launch_bounds__(kBlock) void k_node_proj(NodeProjArgs a) {
-  constexpr int F = 16 * NT, TM = 2 * NT;
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int r0 = wave_row0();
-  if (r0 >= a.R) return;
-  const int q0 = 2 * blockIdx.y;  // first output tile of this block
-  const int nU = a.h1t;
-  const int li = r0 + (lane & 15);
-  const bool valid = li < a.R;
-  const size_t n = (size_t)a.r0 + (valid ? li : 0);
-  f32x4 in[TM];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    in[t] = ld4(a.xs + n * F + 16 * t + 4 * g);
-    in[NT + t] = a.xin ? ld4(a.xin + n * F + 16 * t + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int tn = a.xin ? TM : NT;  // x_in = 0: only the x_s tiles contribute
-#pragma unroll
-  for (int qq = 0; qq < 2; ++qq) {
-    const int q = q0 + qq;
-    int a_off, ti0, tin, tstride, to;
-    float* dst;
-    int stride;
-    if (q < nU) {
-      if (a.a_u < 0) continue;
-      a_off = a.a_u; ti0 = 0; tin = tn; tstride = TM; to = q; dst = a.U; stride = 16 * nU;
-    } else if (q < 2 * nU) {
-      if (a.a_v < 0) continue;
-      a_off = a.a_v; ti0 = 0; tin = tn; tstride = TM; to = q - nU; dst = a.V; stride = 16 * nU;
-    } else if (q < 2 * nU + NT) {
-      if (a.a_o < 0) continue;
-      a_off = a.a_o; ti0 = NT; tin = a.xin ? NT : 0; tstride = NT; to = q - 2 * nU; dst = a.O; stride = F;
-    } else {
-      continue;
-    }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ti = 0; ti < TM; ++ti) {
-      if (ti >= ti0 && ti < ti0 + tin) {
-        const f32x4 w = ld4(a.W + a_off + ((size_t)(to * tstride + (ti - ti0)) * 64 + lane) * 4);
-        acc = MSW_MFMA(w.x, in[ti].x, acc);
-        acc = MSW_MFMA(w.y, in[ti].y, acc);
-        acc = MSW_MFMA(w.z, in[ti].z, acc);
-        acc = MSW_MFMA(w.w, in[ti].w, acc);
-      }
-    }
-    if (valid) st4(dst + n * stride + 16 * to + 4 * g, acc);
-  }
-}
-
-// ---------------------------------------------------------------------------- edge MLP
-// s_ij = MLP(x_s[row], x_s[col], x_d[row], x_d[col], e_ij), normalised (gnn.py:414-426).
-// The first layer arrives pre-split: h1 = act(U[row] + V[col] + Pe[e]).  Computed ONCE per
-// SWEGNN layer: its inputs do not change across the K hops (gnn.py:414-420 reads x_s, x_d).
-template <int NT, int ACT>
-__global__ __launch_bounds__(kBlock) void k_edge_mlp(EdgeMlpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int F = 16 * NT, TM = 2 * NT;
-  for (int i = threadIdx.x * 4; i < a.w_count; i += kBlock * 4) st4(smem + i, ld4(a.W + i));
-  __syncthreads();
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int ntiles = (a.E + kRowsPerWave - 1) / kRowsPerWave;
-  const int hs = 16 * a.h1t;
-  for (int tile = blockIdx.x * kWaves + (threadIdx.x >> 6); tile < ntiles; tile += gridDim.x * kWaves) {
-    const int e = tile * kRowsPerWave + (lane & 15);
-    const bool valid = e < a.E;
-    const int ee = valid ? e : a.E - 1;
-    const size_t sr = (size_t)a.src[ee], dc = (size_t)a.dst[ee];
-    f32x4 H[TM];
-#pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      if (t < a.h1t) {
-        const int off = 16 * t + 4 * g;
-        const f32x4 u = ld4(a.U + sr * hs + off);
-        const f32x4 v = ld4(a.V + dc * hs + off);
-        const f32x4 p = a.Pe ? ld4(a.Pe + (size_t)ee * hs + off) : ld4(a.b1 + off);
-        H[t] = (u + v) + p;
-      } else {
-        H[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    act_tiles<ACT, TM>(H, a.act1, a.slope1);
-    if (a.rest.n > 0) {
-      f32x4 o[NT];
-      run_mlp<TM, TM, NT, ACT>(H, o, a.rest, smem, lane, g);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) H[t] = o[t];
-    }
-    if (a.normalize) {
-      float ss = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ss += hsum(H[t] * H[t]);
-      const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 q = H[t] / nrm;
-        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-        q.y = (q.y == q.y) ? q.y : 0.f;
-        q.z = (q.z == q.z) ? q.z : 0.f;
-        q.w = (q.w == q.w) ? q.w : 0.f;
-        H[t] = q;
-      }
-    }
-    if (valid) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) st4(a.s + (size_t)e * F + 16 * t + 4 * g, H[t]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------- hop
-// One SWEGNN hop (gnn.py:406-443), pull over CSR-by-destination, 16 destinations per wave:
-//   active(e) = rowsum(out[src]) != 0 || rowsum(out[dst]) != 0          (gnn.py:408-411)
-//   agg[c]    = sum_e active(e) * (out[c] - out[src]) * s_e  (edge order; gnn.py:430-438)
-//   out'[c]   = out[c] + W_{k+1} agg[c]    (MFMA; + skip, + post activation)
-template <int NT>
-__global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT;
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int r0 = wave_row0();
-  if (r0 >= a.R) return;
-  const int li = r0 + (lane & 15);
-  const bool valid = li < a.R;
-  const size_t c = (size_t)a.n0 + (valid ? li : 0);
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  f32x4 oc[NT], agg[NT];
-  float sc = 0.f;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    oc[t] = a.own_zero ? z : ld4(a.in + c * F + 16 * t + 4 * g);
-    sc += hsum(oc[t]);
-    agg[t] = z;
-  }
-  const bool fc = row_sum(sc) != 0.f;
-  const int e0 = valid ? a.rowptr[li] : 0, e1 = valid ? a.rowptr[li + 1] : 0;
-  for (int e = e0; e < e1; ++e) {
-    const size_t sidx = (size_t)a.src[e];
-    f32x4 os[NT], sv[NT];
-    float ss = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      os[t] = ld4(a.in + sidx * F + 16 * t + 4 * g);
-      sv[t] = ld4(a.s + (size_t)e * F + 16 * t + 4 * g);
-      ss += hsum(os[t]);
-    }
-    const bool act = fc || (row_sum(ss) != 0.f);
-    if (act) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 gv;
-        if (a.grad) {
-          gv = oc[t] - os[t];  // out[col] - out[row]
-          if (a.upwind) {
-            gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
-            gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
-          }
-        } else {
-          gv = os[t];          // s_ij * out[row]
-        }
-        agg[t] = agg[t] + gv * sv[t];
-      }
-    }
-  }
-  f32x4 res[NT];
-  if (a.A) {  // filter W_{k+1} on the MFMA, agg already in B-operand layout
-    f32x4 acc[NT];
-#pragma unroll
-    for (int to = 0; to < NT; ++to) acc[to] = z;
-#pragma unroll
-    for (int ti = 0; ti < NT; ++ti) {
-      f32x4 w[NT];
-#pragma unroll
-      for (int to = 0; to < NT; ++to) w[to] = ld4(a.A + ((size_t)(to * NT + ti) * 64 + lane) * 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int to = 0; to < NT; ++to) acc[to] = MSW_MFMA(w[to][r], agg[ti][r], acc[to]);
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = oc[t] + acc[t];
-  } else {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = oc[t] + agg[t];
-  }
-  if (a.skip) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = res[t] + ld4(a.skip + c * F + 16 * t + 4 * g);
-  }
-  if (a.post_act) act_tiles<-1, NT>(res, a.post_act, a.post_slope);  // GNN gnn_activation
-  if (valid) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) st4(a.out + c * F + 16 * t + 4 * g, res[t]);
-  }
-}
-
-// ---------------------------------------------------------------------------- pooling
-// scatter(x[fine], coarse, reduce='mean') (gnn.py:256): children summed in edge order,
-// divided by max(count, 1).
-template <int NT>
-__global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT;
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int r0 = wave_row0();
-  if (r0 >= a.R) return;
-  const int li = r0 + (lane & 15);
-  if (li >= a.R) return;
-  const size_t c = (size_t)a.n0 + li;
-  const int e0 = a.rowptr[li], e1 = a.rowptr[li + 1];
-  f32x4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int e = e0; e < e1; ++e) {
-    const size_t ch = (size_t)a.child[e];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = acc[t] + ld4(a.in + ch * F + 16 * t + 4 * g);
-  }
-  const float cnt = (float)(e1 - e0 > 0 ? e1 - e0 : 1);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) st4(a.out + c * F + 16 * t + 4 * g, acc[t] / cnt);
-}
-
-// ---------------------------------------------------------------------------- decoder
-// tanh(x_up) -> node_decoder -> + learned residual -> ReLU -> small-depth mask
-// (gnn.py:335-348, models.py:50-91); in rollout mode also use_prediction + BC of the next
-// step (dataset.py:486-529) and the rollout write (train.py:93-95).
-template <int NT, int ACT>
-__global__ __launch_bounds__(kBlock) void k_decode(DecodeArgs a) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT;
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  const int r0 = wave_row0();
-  if (r0 >= a.N) return;
-  const int n = r0 + (lane & 15);
-  const bool valid = n < a.N;
-  const size_t ni = valid ? n : 0;
-  f32x4 X0[NT], A[1];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) X0[t] = ld4(a.xup + ni * F + 16 * t + 4 * g);
-  act_tiles<-1, NT>(X0, a.pre_act, a.pre_slope);
-  run_mlp<NT, NT, 1, ACT>(X0, A, a.dec, a.W, lane, g);
-  if (!valid || g) return;  // lane group 0 holds output features 0 (h) and 1 (|q|)
-  const int ext = a.perm ? a.perm[n] : n;
-  float* xr = a.X + (size_t)(a.io ? n : ext) * a.nnf;
-  const int nstat = a.nnf - a.dyn;
-  float h = A[0].x, v = A[0].y;
-  if (a.resw) {
-    float rh = xr[nstat] * a.resw[0];
-    float rv = xr[nstat + 1] * a.resw[1];
-    for (int tau = 1; tau < a.p; ++tau) {
-      rh = rh + xr[nstat + 2 * tau] * a.resw[2 * tau];
-      rv = rv + xr[nstat + 2 * tau + 1] * a.resw[2 * tau + 1];
-    }
-    h = h + rh;
-    v = v + rv;
-  }
-  h = h > 0.f ? h : 0.f;  // torch.relu
-  v = v > 0.f ? v : 0.f;
-  const float hm = h * (fabsf(h) > 1e-4f ? 1.f : 0.f);  // _mask_small_WD(epsilon=1e-4)
-  const float vm = v * (h != 0.f ? 1.f : 0.f);
-  if (!a.io) {
-    a.y[(size_t)ext * 2 + 0] = hm;
-    a.y[(size_t)ext * 2 + 1] = vm;
-    return;
-  }
-  RolloutIO* io = a.io;
-  const int t = io->step;
-  io->out[((size_t)ext * 2 + 0) * io->T + t] = hm;
-  io->out[((size_t)ext * 2 + 1) * io->T + t] = vm;
-  for (int k = 0; k + 2 < a.dyn; ++k) xr[nstat + k] = xr[nstat + k + 2];
-  xr[a.nnf - 2] = hm;
-  xr[a.nnf - 1] = vm;
-  const int b = a.bc_slot ? a.bc_slot[n] : -1;
-  if (b >= 0 && t + 1 < io->bc_tstride) {
-    for (int tau = 0; tau < a.p; ++tau)
-      xr[nstat + (io->type_bc - 1) + 2 * tau] =
-          io->bc[((size_t)b * a.p + tau) * io->bc_tstride + t + 1];
-  }
+    mfma_layer<TI, TO, -1>(in, out, a.m.l[0], a.W, lane, g);
+  if (valid) store_row<TO>(a.out + (size_t)row * a.out_stride, out, a.out_tiles, g);
 }
 
 // ---------------------------------------------------------------------------- launchers
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 template <int NT>
+constexpr size_t lds_bytes(int floats) { return kStaged<NT> ? (size_t)floats * sizeof(float) : 0; }
+
+// Allow the dynamic weight regions past the 64 KB default (gfx950: 160 KB per CU).
+template <int NT>
+hipError_t prepare_kernels() {
+  const int mx = 160 * 1024 - kWaves * kRowsPerWave * 16 * NT * (int)sizeof(float);
+  const void* fns[] = {(const void*)k_encode<NT, 1>, (const void*)k_encode<NT, -1>,
+                       (const void*)k_edge_hop<NT, 1>, (const void*)k_edge_hop<NT, -1>,
+                       (const void*)k_hop<NT, 1>, (const void*)k_hop<NT, -1>, (const void*)k_pool<NT>};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <int NT>
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
-  if (a.N <= 0) return hipSuccess;
-  if (a.prelu_only)
-    hipLaunchKernelGGL((k_encode<NT, 1>), dim3(cdiv(a.N, kRowsPerBlock)), dim3(kBlock), 0, st, a);
+  if (a.Npad <= 0) return hipSuccess;
+  const dim3 grid(cdiv(a.Npad, kRowsPerBlock)), block(kBlock);
+  const size_t sh = lds_bytes<NT>(a.lds_floats);
+  if (a.c.prelu)
+    hipLaunchKernelGGL((k_encode<NT, 1>), grid, block, sh, st, a);
   else
-    hipLaunchKernelGGL((k_encode<NT, -1>), dim3(cdiv(a.N, kRowsPerBlock)), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((k_encode<NT, -1>), grid, block, sh, st, a);
+  return hipGetLastError();
+}
+template <int NT>
+hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
+  if (a.ntiles <= 0) return hipSuccess;
+  const dim3 grid(cdiv(a.ntiles, kWaves)), block(kBlock);
+  const size_t sh = lds_bytes<NT>(a.reg.len);
+  if (a.c.prelu)
+    hipLaunchKernelGGL((k_edge_hop<NT, 1>), grid, block, sh, st, a);
+  else
+    hipLaunchKernelGGL((k_edge_hop<NT, -1>), grid, block, sh, st, a);
+  return hipGetLastError();
+}
+template <int NT>
+hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
+  if (a.ntiles <= 0) return hipSuccess;
+  const dim3 grid(cdiv(a.ntiles, kWaves)), block(kBlock);
+  const size_t sh = lds_bytes<NT>(a.reg.len);
+  if (a.c.prelu)
+    hipLaunchKernelGGL((k_hop<NT, 1>), grid, block, sh, st, a);
+  else
+    hipLaunchKernelGGL((k_hop<NT, -1>), grid, block, sh, st, a);
+  return hipGetLastError();
+}
+template <int NT>
+hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
+  if (a.ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_pool<NT>), dim3(cdiv(a.ntiles, kWaves)), dim3(kBlock), lds_bytes<NT>(a.reg.len), st, a);
   return hipGetLastError();
 }
 template <int NT>
@@ -529,53 +741,13 @@ hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_rowmlp<NT, 0>), dim3(cdiv(a.R, kRowsPerBlock)), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
-template <int NT>
-hipError_t launch_node_proj(const NodeProjArgs& a, hipStream_t st) {
-  if (a.R <= 0) return hipSuccess;
-  const int tiles = 2 * a.h1t + NT;
-  hipLaunchKernelGGL(k_node_proj<NT>, dim3(cdiv(a.R, kRowsPerBlock), cdiv(tiles, 2)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-template <int NT>
-hipError_t launch_edge_mlp(const EdgeMlpArgs& a, hipStream_t st) {
-  if (a.E <= 0) return hipSuccess;
-  const int tiles = cdiv(a.E, kRowsPerWave);
-  const int grid = std::min(cdiv(tiles, kWaves), 256 * 8);
-  if (a.prelu_only)
-    hipLaunchKernelGGL((k_edge_mlp<NT, 1>), dim3(grid), dim3(kBlock), a.w_count * sizeof(float), st, a);
-  else
-    hipLaunchKernelGGL((k_edge_mlp<NT, -1>), dim3(grid), dim3(kBlock), a.w_count * sizeof(float), st, a);
-  return hipGetLastError();
-}
-template <int NT>
-hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
-  if (a.R <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hop<NT>, dim3(cdiv(a.R, kRowsPerBlock)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-template <int NT>
-hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
-  if (a.R <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pool<NT>, dim3(cdiv(a.R, kRowsPerBlock)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-template <int NT>
-hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
-  if (a.N <= 0) return hipSuccess;
-  if (a.prelu_only)
-    hipLaunchKernelGGL((k_decode<NT, 1>), dim3(cdiv(a.N, kRowsPerBlock)), dim3(kBlock), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_decode<NT, -1>), dim3(cdiv(a.N, kRowsPerBlock)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
 
 #define MSW_INSTANTIATE(NT)                                                       \
+  template hipError_t prepare_kernels<NT>();                                      \
   template hipError_t launch_encode<NT>(const EncodeArgs&, hipStream_t);          \
-  template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);          \
-  template hipError_t launch_node_proj<NT>(const NodeProjArgs&, hipStream_t);     \
-  template hipError_t launch_edge_mlp<NT>(const EdgeMlpArgs&, hipStream_t);       \
+  template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
-  template hipError_t launch_decode<NT>(const DecodeArgs&, hipStream_t);
+  template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);
 
 }  // namespace msw

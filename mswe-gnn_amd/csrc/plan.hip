@@ -1,6 +1,7 @@
-// Host side of the C ABI (include/mswegnn.h): graph plan (internal numbering, CSR by
-// destination, pooling / unpooling maps), weight packing for the gfx950 kernels, the
-// per-step schedule of MSGNN.forward / GNN.forward and the fused rollout.
+// Host side of the C ABI (include/mswegnn.h): graph plan (16-row-aligned internal
+// numbering, CSR by destination, edge tiles, pooling / unpooling maps), weight packing
+// for the gfx950 kernels, the per-step schedule of MSGNN.forward / GNN.forward and the
+// fused rollout (one hipGraph per step, replayed T times).
 //
 // Reference semantics followed (sdat2/mSWE-GNN):
 //   MSGNN.forward  models/gnn.py:267-350     GNN.forward  models/gnn.py:102-152
@@ -9,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -35,8 +37,8 @@ int fail(int code, const std::string& msg) {
       return fail(MSW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));     \
   } while (0)
 
-inline int tiles(int n) { return (n + 15) / 16; }
-
+inline int tiles16(int n) { return (n + 15) / 16; }
+inline int round64(int n) { return (n + kRowsPerBlock - 1) / kRowsPerBlock * kRowsPerBlock; }
 
 struct Blob {
   std::vector<float> h;
@@ -49,9 +51,9 @@ struct Blob {
 
 // Pack W (original [out_dim][in_dim]) as the A operand of v_mfma_f32_16x16x4_f32,
 // [tout][tin][lane][4]: lane l, k-step r of input tile ti for output tile to holds
-// W[16 to + (l & 15)][16 ti + 4 (l >> 4) + r] (see kernels_impl.h for the register layout).
-// in_map(k) / out_map(o) give the original column / row of packed input feature k /
-// output feature o, or -1 for a zero pad.
+// W[16 to + (l & 15)][16 ti + 4 (l >> 4) + r] (register layout: kernels_impl.h).
+// in_map(k) / out_map(o): original column / row of packed input feature k / output
+// feature o, or -1 for a zero pad.
 template <class InMap, class OutMap>
 int pack_operand(Blob& B, const float* W, int in_dim, int tout, int tin, InMap in_map,
                  OutMap out_map) {
@@ -70,17 +72,16 @@ int pack_operand(Blob& B, const float* W, int in_dim, int tout, int tin, InMap i
   return off;
 }
 
+// Every layer gets a bias vector (zeros for bias=False): the kernels add it unconditionally.
 int pack_bias(Blob& B, const float* b, int out_dim, int tout) {
-  if (!b) return -1;
   const int off = B.alloc((size_t)16 * tout);
-  for (int o = 0; o < out_dim; ++o) B.h[off + o] = b[o];
+  if (b)
+    for (int o = 0; o < out_dim; ++o) B.h[off + o] = b[o];
   return off;
 }
 
-int act_code(int a) { return (a >= 0 && a <= 7) ? a : -1; }
-
 // Pack a make_mlp stack (natural feature order in and out).
-int pack_mlp(Blob& B, const msw_mlp& m, MlpDev& d, int first_in_tiles_override = -1) {
+int pack_mlp(Blob& B, const msw_mlp& m, MlpDev& d) {
   if (m.n_layers < 1 || m.n_layers > kMaxLayers)
     return fail(MSW_ERR_UNSUPPORTED, "MLP depth must be 1.." + std::to_string(kMaxLayers));
   d.n = m.n_layers;
@@ -88,20 +89,24 @@ int pack_mlp(Blob& B, const msw_mlp& m, MlpDev& d, int first_in_tiles_override =
     const msw_linear& L = m.layer[i];
     if (!L.weight || L.in_features <= 0 || L.out_features <= 0)
       return fail(MSW_ERR_INVALID, "MLP layer without weight");
-    if (act_code(L.act) < 0) return fail(MSW_ERR_INVALID, "unknown activation code");
-    const int tin = (i == 0 && first_in_tiles_override > 0) ? first_in_tiles_override : tiles(L.in_features);
-    const int tout = tiles(L.out_features);
+    if (L.act < 0 || L.act > 7) return fail(MSW_ERR_INVALID, "unknown activation code");
+    const int tin = tiles16(L.in_features), tout = tiles16(L.out_features);
     const int din = L.in_features, dout = L.out_features;
     d.l[i].tin = tin;
     d.l[i].tout = tout;
-    d.l[i].a_off = pack_operand(B, L.weight, din, tout, tin,
-                                [&](int k) { return k < din ? k : -1; },
+    d.l[i].a_off = pack_operand(B, L.weight, din, tout, tin, [&](int k) { return k < din ? k : -1; },
                                 [&](int o) { return o < dout ? o : -1; });
     d.l[i].b_off = pack_bias(B, L.bias, dout, tout);
     d.l[i].act = L.act;
     d.l[i].slope = L.act_param;
   }
   return MSW_OK;
+}
+
+int all_prelu(const msw_mlp& m) {
+  for (int i = 0; i < m.n_layers; ++i)
+    if (m.layer[i].act != MSW_ACT_PRELU) return 0;
+  return 1;
 }
 
 template <class T>
@@ -120,8 +125,6 @@ int upload(T** p, const std::vector<T>& v, int64_t& counter) {
   return MSW_OK;
 }
 
-}  // namespace
-
 hipError_t rowmlp_dispatch(int NT, const RowMlpArgs& ra) {
   switch (NT) {
     case 1: return launch_rowmlp<1>(ra, nullptr);
@@ -130,73 +133,130 @@ hipError_t rowmlp_dispatch(int NT, const RowMlpArgs& ra) {
   }
 }
 
+// Edge tiles over a CSR by destination: consecutive destinations with <= 16 in-edges and
+// <= 16 destinations per tile (whole neighbourhoods, so hop 1 fuses into the edge MLP).
+int build_tiles(const std::vector<int>& rowptr, std::vector<TileRange>& out) {
+  out.clear();
+  const int ns = (int)rowptr.size() - 1;
+  int a = 0;
+  while (a < ns) {
+    int b = a, edges = 0;
+    while (b < ns && b - a < kRowsPerWave) {
+      const int d = rowptr[b + 1] - rowptr[b];
+      if (d > kRowsPerWave) return fail(MSW_ERR_UNSUPPORTED, "node with more than 16 in-edges");
+      if (edges + d > kRowsPerWave) break;
+      edges += d;
+      ++b;
+    }
+    out.push_back(TileRange{a, b - a, rowptr[a], edges});
+    a = b;
+  }
+  return MSW_OK;
+}
+
+}  // namespace
+
 // ============================================================================ plan
 struct ScaleCSR {
-  int n0 = 0, ns = 0;     // internal node range
-  int E = 0;              // edges of this scale
-  int* rowptr = nullptr;  // [ns+1]
-  int* src = nullptr;     // [E] internal ids, CSR order
-  int* dst = nullptr;     // [E]
-  std::vector<int> eorig; // CSR position -> original edge id
+  int n0 = 0, ns = 0;           // internal rows [n0, n0+ns) (n0 is a multiple of 16)
+  int E = 0;                    // edges of this scale
+  int* rowptr = nullptr;        // [ns+1] local
+  int* src = nullptr;           // [E] internal ids, CSR order
+  int* dst = nullptr;           // [E]
+  TileRange* tiles = nullptr;
+  int ntiles = 0;
+  std::vector<int> eorig;       // CSR position -> original edge id
 };
 
-struct LevelMaps {            // level l: coarse scale l+1, fine scale l
+struct LevelMaps {              // level l: coarse scale l+1, fine scale l
   int I = 0;
-  int* pool_rowptr = nullptr; // by coarse (local to scale l+1)
+  int* pool_rowptr = nullptr;   // by coarse (local to scale l+1)
   int* pool_child = nullptr;
-  int* un_rowptr = nullptr;   // by fine (local to scale l)
-  int* un_src = nullptr;      // coarse ids
-  int* un_dst = nullptr;      // fine ids
+  TileRange* pool_tiles = nullptr;  // coarse nodes with <= 16 children in all
+  int pool_ntiles = 0;
+  int* un_rowptr = nullptr;     // by fine (local to scale l)
+  int* un_src = nullptr;        // coarse ids
+  int* un_dst = nullptr;        // fine ids
+  TileRange* un_tiles = nullptr;
+  int un_ntiles = 0;
 };
 
-struct Proc {                 // one SWEGNN layer bound to a scale (or intra level)
+struct Proc {                   // one SWEGNN layer bound to a scale (or an intra level)
   int scale = 0;
   int K = 0, normalize = 1, with_filter = 1, with_gradient = 1, upwind = 0;
   int h1t = 1;
-  int a_u = -1, a_v = -1, a_o = -1;
-  float* Pe = nullptr;        // [E][32*h1t] (processors with edge features)
-  int b1_off = -1;            // bias of layer 1 (blob)
+  int a_u = -1, a_v = -1, a_o = -1;  // projection operands ([x_s | x_d] -> U, V, O)
+  int a_vu = -1;                // intra layers: V from x_s only (fine rows)
+  float* Pe = nullptr;          // [E][16*h1t] (layers with edge features)
+  int b1_off = -1;              // bias of the first edge-MLP layer
   int act1 = 0;
   float slope1 = 0.f;
-  MlpDev rest{};              // layers 2..L, offsets relative to rest_base
-  int rest_base = 0, rest_count = 0;
-  std::vector<int> wt_off;    // packed filters 1..K (blob offsets)
-  int prelu = 0;              // every edge-MLP activation is PReLU
+  MlpDev rest{};                // layers 2..L
+  std::vector<int> filt;        // packed filters 1..K
+  int prelu = 0;
+  int par = 0;                  // buffer set (execution index & 1)
+};
+
+// One kernel launch of a step, arguments fixed at plan time (forward mode patches the
+// input / output pointers per call).
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL };
+struct Launch {
+  int kind;
+  int scale;                    // destination scale (bench hook)
+  union {
+    EncodeArgs enc;
+    EdgeHopArgs eh;
+    HopArgs hop;
+    PoolArgs pool;
+  };
+  Launch() { memset((void*)this, 0, sizeof(*this)); }
+  Common& common() {
+    switch (kind) {
+      case L_ENCODE: return enc.c;
+      case L_EDGE_HOP: return eh.c;
+      case L_HOP: return hop.c;
+      default: return pool.c;
+    }
+  }
 };
 
 struct msw_plan {
   int device = 0;
   int model_type = 0, F = 32, NT = 2, S = 1, p = 3, nnf = 8, dyn = 6, nstat_raw = 2;
-  int with_wl = 1, skip = 1, ef = 1;
-  int N = 0;
+  int with_wl = 1, skip = 1;
+  int N = 0, Npad = 0;
   int64_t E = 0;
-  bool identity = true;
-  std::vector<int> perm, iperm;  // internal -> graph, graph -> internal
+  std::vector<int> perm, iperm;  // internal -> graph (-1 padding), graph -> internal
   std::vector<ScaleCSR> sc;
   std::vector<LevelMaps> lv;
   std::vector<Proc> procs, unpools;
   MlpDev stat{}, dynm{}, dec{}, edge_enc{};
   int gnn_act = 0;
   float gnn_slope = 0.f;
-  int enc_prelu = 0, dec_prelu = 0;
   int resw_off = -1;
+  int prelu = 0;
   Blob blob;
   float* dW = nullptr;
   int* perm_d = nullptr;
   int* bc_slot_d = nullptr;
-  std::vector<int> bc_rows_set;  // internal rows currently holding a BC slot
+  std::vector<int> bc_rows_set;
   RolloutIO* io_d = nullptr;
-  float *X = nullptr, *xs = nullptr, *xd0 = nullptr, *bufA = nullptr, *bufB = nullptr;
-  float *xin = nullptr, *xdown = nullptr, *xup = nullptr, *U = nullptr, *V = nullptr, *s = nullptr;
-  float* gnnbuf[2] = {nullptr, nullptr};
+  // O / U / V of consecutive SWEGNN layers alternate between two sets (Proc::par): the
+  // last hop of layer j reads O[j&1] (K = 1: also U/V[j&1]) while its epilogue writes the
+  // projection of layer j+1.  T[0] / T[1] carry the intermediate hops.
+  float *X = nullptr, *xs = nullptr, *xd0 = nullptr;
+  float *O[2] = {nullptr, nullptr}, *T[2] = {nullptr, nullptr};
+  float *xdown = nullptr, *xup = nullptr, *xgnn = nullptr;
+  float *U[2] = {nullptr, nullptr}, *V[2] = {nullptr, nullptr};
+  float *Uu = nullptr, *Vu = nullptr, *s = nullptr;
   int h1t_max = 1;
   int64_t dev_bytes = 0;
   int64_t forward_calls = 0, rollout_steps = 0;
   int kernels_per_step = 0;
+  std::vector<Launch> sched_fwd, sched_roll;  // one forward step: forward / rollout mode
   int use_graph = 1;
   hipStream_t cap_stream = nullptr;
   hipGraphExec_t step_exec = nullptr;
-  const float* last_x = nullptr;  // input the forward-mode kernels were built for
   std::vector<void*> owned;
   ~msw_plan() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
@@ -220,7 +280,7 @@ int pupload(msw_plan* P, T** p, const std::vector<T>& v) {
   return rc;
 }
 
-// Stable counting sort of (key, payload) pairs by key in [0, nkeys).
+// Stable counting sort by key in [0, nkeys): rowptr + order (original indices).
 void csr_build(int nkeys, const std::vector<int>& key, std::vector<int>& rowptr,
                std::vector<int>& order) {
   rowptr.assign(nkeys + 1, 0);
@@ -231,19 +291,18 @@ void csr_build(int nkeys, const std::vector<int>& key, std::vector<int>& rowptr,
   for (size_t e = 0; e < key.size(); ++e) order[pos[key[e]]++] = (int)e;
 }
 
-// SWEGNN layer -> packed Proc.  edge_in: width of the per-edge features it consumes.
+// SWEGNN layer -> packed Proc (gnn.py:352-445).
 int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr) {
-  const int F = P->F;
+  const int F = P->F, NT = P->NT;
   pr.scale = scale;
   pr.K = g.K;
   pr.normalize = g.normalize;
   pr.with_filter = g.with_filter_matrix;
   pr.with_gradient = g.with_gradient;
   pr.upwind = g.upwind_mode;
-  if (g.K < 1 && !intra) return fail(MSW_ERR_UNSUPPORTED, "SWEGNN with K < 1");
+  if (g.K < 1) return fail(MSW_ERR_UNSUPPORTED, "SWEGNN with K < 1");
   const msw_mlp& m = g.edge_mlp;
-  if (m.n_layers < 1 || m.n_layers > kMaxLayers)
-    return fail(MSW_ERR_UNSUPPORTED, "edge MLP depth must be 1..4");
+  if (m.n_layers < 1 || m.n_layers > kMaxLayers) return fail(MSW_ERR_UNSUPPORTED, "edge MLP depth must be 1..4");
   const msw_linear& L1 = m.layer[0];
   const int ef = g.edge_features;
   if (L1.in_features != 4 * F + ef) return fail(MSW_ERR_INVALID, "edge MLP input width != 4F + edge_features");
@@ -252,208 +311,358 @@ int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr
   for (int i = 1; i < m.n_layers; ++i)
     if (m.layer[i].in_features != 2 * F || m.layer[i].out_features != (i == m.n_layers - 1 ? F : 2 * F))
       return fail(MSW_ERR_UNSUPPORTED, "edge MLP layer widths must be 2F -> ... -> F");
-  pr.h1t = tiles(H1);
+  pr.h1t = tiles16(H1);
   P->h1t_max = std::max(P->h1t_max, pr.h1t);
   const int din = L1.in_features;
   const float* W1 = L1.weight;
   auto outm = [&](int o) { return o < H1 ? o : -1; };
-  // U: [x_s (tiles 0..T-1) | x_d (tiles T..2T-1)] of the ROW (source) node
-  auto in_u = [&](int k) {
-    if (k < F) return k;                                     // x_s[row]  cols [0, F)
-    return k < 2 * F ? 2 * F + (k - F) : -1;                 // x_d[row]  cols [2F, 3F)
-  };
-  auto in_v = [&](int k) {
-    if (k < F) return F + k;                                 // x_s[col]  cols [F, 2F)
-    return k < 2 * F ? 3 * F + (k - F) : -1;                 // x_d[col]  cols [3F, 4F)
-  };
-  pr.a_u = pack_operand(P->blob, W1, din, pr.h1t, 2 * P->NT, in_u, outm);
-  pr.a_v = pack_operand(P->blob, W1, din, pr.h1t, 2 * P->NT, in_v, outm);
+  // cat(x_s[row], x_s[col], x_d[row], x_d[col], e_ij) (gnn.py:414-420): U takes the row
+  // (source) blocks, V the col (receiving) blocks; packed input = [x_s (F) | x_d (F)]
+  auto in_u = [&](int k) { return k < F ? k : (k < 2 * F ? 2 * F + (k - F) : -1); };
+  auto in_v = [&](int k) { return k < F ? F + k : (k < 2 * F ? 3 * F + (k - F) : -1); };
+  pr.a_u = pack_operand(P->blob, W1, din, pr.h1t, 2 * NT, in_u, outm);
+  pr.a_v = pack_operand(P->blob, W1, din, pr.h1t, 2 * NT, in_v, outm);
+  if (intra)  // fine rows enter with x_d = 0: V from the x_s block alone
+    pr.a_vu = pack_operand(P->blob, W1, din, pr.h1t, NT, [&](int k) { return k < F ? F + k : -1; }, outm);
   pr.act1 = L1.act;
   pr.slope1 = L1.act_param;
-  if (L1.bias) {
-    pr.b1_off = P->blob.alloc(16 * pr.h1t);
+  pr.b1_off = P->blob.alloc(16 * pr.h1t);
+  if (L1.bias)
     for (int o = 0; o < H1; ++o) P->blob.h[pr.b1_off + o] = L1.bias[o];
-  } else {
-    pr.b1_off = P->blob.alloc(16 * pr.h1t);  // zeros
-  }
-  if (g.with_filter_matrix && !intra) {
+  auto idF = [&](int q) { return q < F ? q : -1; };
+  if (g.with_filter_matrix) {
+    if (intra) return fail(MSW_ERR_UNSUPPORTED, "intra-scale SWEGNN with filter matrix");
     if (!g.filter) return fail(MSW_ERR_INVALID, "with_filter_matrix but no filter weights");
-    // filter 0 as an MFMA operand over the x_in tiles: O = W0 . x_in
-    pr.a_o = pack_operand(P->blob, g.filter[0], F, P->NT, P->NT,
-                          [&](int k) { return k < F ? k : -1; },
-                          [&](int o) { return o < F ? o : -1; });
-    for (int k = 1; k <= g.K; ++k)  // filters 1..K as MFMA operands of the hop kernel
-      pr.wt_off.push_back(pack_operand(P->blob, g.filter[k], F, P->NT, P->NT,
-                                       [&](int q) { return q < F ? q : -1; },
-                                       [&](int o) { return o < F ? o : -1; }));
-  } else if (g.with_filter_matrix && intra) {
-    return fail(MSW_ERR_UNSUPPORTED, "intra-scale SWEGNN with filter matrix");
+    pr.a_o = pack_operand(P->blob, g.filter[0], F, NT, NT, idF, idF);
+    for (int k = 1; k <= g.K; ++k) pr.filt.push_back(pack_operand(P->blob, g.filter[k], F, NT, NT, idF, idF));
   } else if (!intra) {
     // out = x_d.clone() (gnn.py:404): identity operand, exact (1*x + 0*y sums)
     std::vector<float> I((size_t)F * F, 0.f);
     for (int i = 0; i < F; ++i) I[(size_t)i * F + i] = 1.f;
-    pr.a_o = pack_operand(P->blob, I.data(), F, P->NT, P->NT,
-                          [&](int k) { return k < F ? k : -1; },
-                          [&](int o) { return o < F ? o : -1; });
+    pr.a_o = pack_operand(P->blob, I.data(), F, NT, NT, idF, idF);
   }
-  // layers 2..L contiguous (staged to LDS by the edge kernel)
   pr.rest.n = m.n_layers - 1;
-  Blob rb;
   for (int i = 1; i < m.n_layers; ++i) {
     const msw_linear& L = m.layer[i];
-    const int tin = tiles(L.in_features), tout = tiles(L.out_features);
     const int di = L.in_features, dout = L.out_features;
-    pr.rest.l[i - 1].tin = tin;
-    pr.rest.l[i - 1].tout = tout;
-    pr.rest.l[i - 1].a_off = pack_operand(rb, L.weight, di, tout, tin,
-                                          [&](int k) { return k < di ? k : -1; },
-                                          [&](int o) { return o < dout ? o : -1; });
-    pr.rest.l[i - 1].b_off = pack_bias(rb, L.bias, dout, tout);
-    pr.rest.l[i - 1].act = L.act;
-    pr.rest.l[i - 1].slope = L.act_param;
+    LayerDev& d = pr.rest.l[i - 1];
+    d.tin = tiles16(di);
+    d.tout = tiles16(dout);
+    d.a_off = pack_operand(P->blob, L.weight, di, d.tout, d.tin, [&](int k) { return k < di ? k : -1; },
+                           [&](int o) { return o < dout ? o : -1; });
+    d.b_off = pack_bias(P->blob, L.bias, dout, d.tout);
+    d.act = L.act;
+    d.slope = L.act_param;
   }
-  if (m.layer[m.n_layers - 1].out_features != F) return fail(MSW_ERR_INVALID, "edge MLP output != F");
-  pr.prelu = 1;
-  for (int i = 0; i < m.n_layers; ++i) pr.prelu &= (m.layer[i].act == MSW_ACT_PRELU);
-  pr.rest_count = (int)((rb.h.size() + 3) / 4 * 4);
-  pr.rest_base = P->blob.alloc(pr.rest_count);
-  std::copy(rb.h.begin(), rb.h.end(), P->blob.h.begin() + pr.rest_base);
-  if ((size_t)pr.rest_count * 4 > 160 * 1024)
-    return fail(MSW_ERR_UNSUPPORTED, "edge MLP weights exceed LDS");
+  pr.prelu = all_prelu(m);
   return MSW_OK;
 }
 
-template <int NT>
-int run_proc(msw_plan* P, const Proc& pr, const float* xin, float* out, int post_act,
-             float post_slope, hipStream_t st, int& nk) {
+NpDesc np_of(msw_plan* P, const Proc& pr) {
+  NpDesc d{};
+  d.a_u = pr.a_u; d.a_v = pr.a_v; d.a_o = pr.a_o; d.h1t = pr.h1t;
+  d.U = P->U[pr.par]; d.V = P->V[pr.par]; d.O = P->O[pr.par];
+  return d;
+}
+NpDesc np_none() {
+  NpDesc d{};
+  d.a_u = d.a_v = d.a_o = -1;
+  d.h1t = 1;
+  return d;
+}
+
+Common common_of(msw_plan* P) {
+  Common c{};
+  c.W = P->dW; c.perm = P->perm_d; c.nnf = P->nnf; c.dyn = P->dyn; c.p = P->p;
+  c.nstat_raw = P->nstat_raw; c.with_wl = P->with_wl; c.prelu = P->prelu;
+  return c;
+}
+
+DecDesc dec_of(msw_plan* P, const float* x_src, bool rollout, float* y) {
+  DecDesc d{};
+  d.on = 1;
+  d.pre_act = P->model_type == 0 ? P->gnn_act : 0;
+  d.pre_slope = P->gnn_slope;
+  d.dec = P->dec;
+  d.resw_off = P->resw_off;
+  d.X = x_src;
+  d.x_internal = rollout ? 1 : 0;
+  d.y = y;
+  d.io = rollout ? P->io_d : nullptr;
+  d.bc_slot = P->bc_slot_d;
+  return d;
+}
+
+// One SWEGNN layer on its scale: fused edge-MLP + hop 1, then hops 2..K; the last hop
+// runs `epi` (and stores its output to `out` if non-null).  out_0 is in O[par].
+void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi) {
   const ScaleCSR& g = P->sc[pr.scale];
-  NodeProjArgs np{};
-  np.r0 = g.n0; np.R = g.ns; np.xs = P->xs; np.xin = xin;
-  np.a_u = pr.a_u; np.a_v = pr.a_v; np.a_o = pr.a_o; np.W = P->dW;
-  np.U = P->U; np.V = P->V; np.O = P->bufA; np.h1t = pr.h1t;
-  HIP_TRY(launch_node_proj<NT>(np, st)); ++nk;
-  EdgeMlpArgs em{};
-  em.E = g.E; em.src = g.src; em.dst = g.dst; em.U = P->U; em.V = P->V; em.Pe = pr.Pe;
-  em.b1 = P->dW + pr.b1_off; em.h1t = pr.h1t; em.act1 = pr.act1; em.slope1 = pr.slope1;
-  em.rest = pr.rest; em.W = P->dW + pr.rest_base; em.w_count = pr.rest_count;
-  em.normalize = pr.normalize; em.s = P->s; em.prelu_only = pr.prelu;
-  HIP_TRY(launch_edge_mlp<NT>(em, st)); ++nk;
-  const float* cur = P->bufA;
-  for (int k = 1; k <= pr.K; ++k) {
-    float* nxt = (k == pr.K) ? out : (cur == P->bufA ? P->bufB : P->bufA);
-    HopArgs h{};
-    h.n0 = g.n0; h.R = g.ns; h.rowptr = g.rowptr; h.src = g.src; h.s = P->s; h.in = cur;
-    h.out = nxt; h.A = pr.wt_off.empty() ? nullptr : P->dW + pr.wt_off[k - 1]; h.skip = nullptr; h.own_zero = 0;
+  const Common c = common_of(P);
+  Launch L1;
+  L1.kind = L_EDGE_HOP;
+  L1.scale = pr.scale;
+  EdgeHopArgs& eh = L1.eh;
+  eh.c = c; eh.n0 = g.n0; eh.tiles = g.tiles; eh.ntiles = g.ntiles; eh.rowptr = g.rowptr;
+  eh.src = g.src; eh.dst = g.dst; eh.xs = P->xs; eh.U = P->U[pr.par]; eh.V = P->V[pr.par]; eh.Pe = pr.Pe;
+  eh.b1_off = pr.b1_off; eh.h1t = pr.h1t; eh.act1 = pr.act1; eh.slope1 = pr.slope1;
+  eh.rest = pr.rest; eh.normalize = pr.normalize;
+  eh.c.prelu = P->prelu & pr.prelu;
+  eh.s = pr.K > 1 ? P->s : nullptr;
+  eh.in = P->O[pr.par]; eh.own_zero = 0; eh.grad = pr.with_gradient; eh.upwind = pr.upwind;
+  eh.filt_a = pr.filt.empty() ? -1 : pr.filt[0];
+  eh.skip = nullptr;
+  eh.last = pr.K == 1;
+  eh.out = pr.K == 1 ? out : P->T[0];
+  eh.epi = epi;
+  q.push_back(L1);
+  const float* cur = P->T[0];
+  for (int k = 2; k <= pr.K; ++k) {
+    float* nxt = (k == pr.K) ? out : (cur == P->T[0] ? P->T[1] : P->T[0]);
+    Launch L;
+    L.kind = L_HOP;
+    L.scale = pr.scale;
+    HopArgs& h = L.hop;
+    h.c = c;
+    h.n0 = g.n0; h.tiles = g.tiles; h.ntiles = g.ntiles; h.rowptr = g.rowptr; h.src = g.src; h.dst = g.dst;
+    h.s = P->s; h.xs = P->xs;
+    h.in = cur; h.out = nxt; h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
     h.grad = pr.with_gradient; h.upwind = pr.upwind;
-    h.post_act = (k == pr.K) ? post_act : 0; h.post_slope = post_slope;
-    HIP_TRY(launch_hop<NT>(h, st)); ++nk;
+    h.last = k == pr.K;
+    h.epi = epi;
+    q.push_back(L);
     cur = nxt;
   }
-  return MSW_OK;
 }
 
-// intra_scale_gnn[i] on level l: coarse rows (scale l+1) of `xo` -> fine rows of `dst`
-template <int NT>
-int run_unpool(msw_plan* P, const Proc& pr, int l, const float* xo, float* dst, hipStream_t st,
-               int& nk) {
-  const ScaleCSR& cs = P->sc[l + 1];
-  const ScaleCSR& fs = P->sc[l];
-  const LevelMaps& m = P->lv[l];
-  NodeProjArgs np{};
-  np.xs = P->xs; np.W = P->dW; np.U = P->U; np.V = P->V; np.O = nullptr; np.h1t = pr.h1t;
-  np.r0 = cs.n0; np.R = cs.ns; np.xin = xo; np.a_u = pr.a_u; np.a_v = -1; np.a_o = -1;
-  HIP_TRY(launch_node_proj<NT>(np, st)); ++nk;
-  np.r0 = fs.n0; np.R = fs.ns; np.xin = nullptr; np.a_u = -1; np.a_v = pr.a_v;
-  HIP_TRY(launch_node_proj<NT>(np, st)); ++nk;
-  EdgeMlpArgs em{};
-  em.E = m.I; em.src = m.un_src; em.dst = m.un_dst; em.U = P->U; em.V = P->V; em.Pe = nullptr;
-  em.b1 = P->dW + pr.b1_off; em.h1t = pr.h1t; em.act1 = pr.act1; em.slope1 = pr.slope1;
-  em.rest = pr.rest; em.W = P->dW + pr.rest_base; em.w_count = pr.rest_count;
-  em.normalize = pr.normalize; em.s = P->s; em.prelu_only = pr.prelu;
-  HIP_TRY(launch_edge_mlp<NT>(em, st)); ++nk;
-  HopArgs h{};
-  h.n0 = fs.n0; h.R = fs.ns; h.rowptr = m.un_rowptr; h.src = m.un_src; h.s = P->s; h.in = xo;
-  h.out = dst; h.A = nullptr; h.skip = P->skip ? P->xdown : nullptr; h.own_zero = 1;
-  h.grad = pr.with_gradient; h.upwind = pr.upwind; h.post_act = 0; h.post_slope = 0.f;
-  HIP_TRY(launch_hop<NT>(h, st)); ++nk;
-  return MSW_OK;
-}
-
-// One forward.  x_src/perm: input rows (forward mode: graph rows via perm; rollout: the
-// internal state X with perm = null).  y: forward-mode output (null in rollout mode).
-template <int NT>
-int enqueue_step(msw_plan* P, const float* x_src, const int* perm, float* y, bool rollout,
-                 hipStream_t st) {
-  int nk = 0;
-  EncodeArgs ea{};
-  ea.x = x_src; ea.perm = perm; ea.N = P->N; ea.nnf = P->nnf; ea.nstat_raw = P->nstat_raw;
-  ea.with_wl = P->with_wl; ea.dyn = P->dyn; ea.stat = P->stat; ea.dynm = P->dynm; ea.W = P->dW;
-  ea.xs = P->xs; ea.xd = P->xd0; ea.xd_rows = P->sc[0].n0 + P->sc[0].ns;
+// One forward.  Forward mode: the encoder reads graph rows of x (via perm) and the decoder
+// writes y (both patched per call); rollout mode: the internal state X is updated in place
+// by the decoder epilogue.
+void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
+  q.clear();
+  const int S = P->S;
+  const Common c = common_of(P);
+  Launch LE;
+  LE.kind = L_ENCODE;
+  EncodeArgs& ea = LE.enc;
+  ea.c = c;
+  ea.x = rollout ? P->X : nullptr; ea.x_internal = rollout ? 1 : 0; ea.Npad = P->Npad; ea.S = S;
+  for (int s = 0; s < S; ++s) {
+    ea.n0[s] = P->sc[s].n0;
+    ea.ns[s] = P->sc[s].ns;
+    ea.vu_a[s] = -1;
+  }
+  ea.n0[S] = P->Npad;
+  ea.stat = P->stat; ea.dynm = P->dynm; ea.xs = P->xs; ea.xd = P->xd0;
+  ea.np0 = np_of(P, P->procs[0]);
   ea.io = rollout ? P->io_d : nullptr;
-  ea.prelu_only = P->enc_prelu;
-  HIP_TRY(launch_encode<NT>(ea, st)); ++nk;
-  const float* dec_in = nullptr;
-  int pre_act = 0;
-  float pre_slope = 0.f;
-  int rc = MSW_OK;
+  ea.vu_h1t = 1;
+  if (P->model_type == 0 && S > 1) {
+    for (int l = 0; l < S - 1; ++l) ea.vu_a[l] = P->unpools[S - 2 - l].a_vu;  // level l <- intra_scale_gnn[S-2-l]
+    ea.vu_h1t = P->unpools[0].h1t;
+    ea.Vu = P->Vu;
+  }
+  q.push_back(LE);
+  const DecDesc dd = dec_of(P, rollout ? P->X : nullptr, rollout, nullptr);
   if (P->model_type == 0) {
-    const int S = P->S;
-    for (int i = 0; i < S - 1; ++i) {
-      rc = run_proc<NT>(P, P->procs[i], i == 0 ? P->xd0 : P->xin, P->xdown, 0, 0.f, st, nk);
-      if (rc) return rc;
-      PoolArgs pa{};
-      pa.n0 = P->sc[i + 1].n0; pa.R = P->sc[i + 1].ns; pa.rowptr = P->lv[i].pool_rowptr;
-      pa.child = P->lv[i].pool_child; pa.in = P->xdown; pa.out = P->xin;
-      HIP_TRY(launch_pool<NT>(pa, st)); ++nk;
+    Epilogue none{};
+    none.np = np_none(); none.uu_a = -1; none.dec.on = 0;
+    for (int i = 0; i < S - 1; ++i) {  // fine -> coarse
+      sched_proc(P, q, P->procs[i], P->xdown, none);
+      const LevelMaps& m = P->lv[i];
+      Launch L;
+      L.kind = L_POOL;
+      L.scale = i + 1;
+      PoolArgs& pa = L.pool;
+      pa.c = c; pa.n0 = P->sc[i + 1].n0; pa.tiles = m.pool_tiles; pa.ntiles = m.pool_ntiles;
+      pa.rowptr = m.pool_rowptr; pa.child = m.pool_child; pa.in = P->xdown; pa.xs = P->xs;
+      pa.np = np_of(P, P->procs[i + 1]);
+      q.push_back(L);
     }
-    for (int i = 0; i < S; ++i) {
-      const int j = S - 1 + i;
-      const float* in = (S == 1) ? P->xd0 : P->xin;
-      rc = run_proc<NT>(P, P->procs[j], in, P->xup, 0, 0.f, st, nk);
-      if (rc) return rc;
-      if (i < S - 1) {
-        const int l = S - 2 - i;
-        rc = run_unpool<NT>(P, P->unpools[i], l, P->xup, P->xin, st, nk);
-        if (rc) return rc;
+    for (int i = 0; i < S; ++i) {      // coarse -> fine
+      const int j = S - 1 + i, s = S - 1 - i;
+      Epilogue e{};
+      e.np = np_none();
+      e.uu_a = -1;
+      if (s > 0) {
+        const Proc& up = P->unpools[i];
+        e.uu_a = up.a_u; e.uu_h1t = up.h1t; e.Uu = P->Uu;
+      }
+      e.dec = dd;  // every scale's rows are decoded once final (gnn.py:335-348)
+      sched_proc(P, q, P->procs[j], P->xup, e);
+      if (s > 0) {                      // intra_scale_gnn[i] on level s-1 (+ skip) + projection
+        const Proc& up = P->unpools[i];
+        const ScaleCSR& fs = P->sc[s - 1];
+        const LevelMaps& m = P->lv[s - 1];
+        Launch L;
+        L.kind = L_EDGE_HOP;
+        L.scale = s - 1;
+        EdgeHopArgs& eh = L.eh;
+        eh.c = c; eh.c.prelu = P->prelu & up.prelu;
+        eh.n0 = fs.n0; eh.tiles = m.un_tiles; eh.ntiles = m.un_ntiles; eh.rowptr = m.un_rowptr;
+        eh.src = m.un_src; eh.dst = m.un_dst; eh.xs = P->xs; eh.U = P->Uu; eh.V = P->Vu;
+        eh.Pe = nullptr; eh.b1_off = up.b1_off; eh.h1t = up.h1t; eh.act1 = up.act1;
+        eh.slope1 = up.slope1; eh.rest = up.rest; eh.normalize = up.normalize; eh.s = nullptr;
+        eh.in = P->xup; eh.own_zero = 1; eh.grad = up.with_gradient; eh.upwind = up.upwind;
+        eh.filt_a = -1; eh.skip = P->skip ? P->xdown : nullptr; eh.out = nullptr; eh.last = 1;
+        eh.epi.np = np_of(P, P->procs[j + 1]); eh.epi.uu_a = -1; eh.epi.dec.on = 0;
+        q.push_back(L);
       }
     }
-    dec_in = P->xup;
-    pre_act = P->gnn_act;
-    pre_slope = P->gnn_slope;
   } else {
-    const float* cur = P->xd0;
-    for (size_t j = 0; j < P->procs.size(); ++j) {
-      float* out = P->gnnbuf[j & 1];
-      rc = run_proc<NT>(P, P->procs[j], cur, out, P->gnn_act, P->gnn_slope, st, nk);
-      if (rc) return rc;
-      cur = out;
+    const int L = (int)P->procs.size();
+    for (int j = 0; j < L; ++j) {
+      Epilogue e{};
+      e.post_act = P->gnn_act; e.post_slope = P->gnn_slope;
+      e.np = j + 1 < L ? np_of(P, P->procs[j + 1]) : np_none();
+      e.uu_a = -1;
+      if (j + 1 == L) e.dec = dd; else e.dec.on = 0;
+      sched_proc(P, q, P->procs[j], P->xgnn, e);
     }
-    dec_in = cur;
   }
-  DecodeArgs da{};
-  da.N = P->N; da.nnf = P->nnf; da.dyn = P->dyn; da.p = P->p; da.xup = dec_in;
-  da.pre_act = pre_act; da.pre_slope = pre_slope; da.dec = P->dec; da.W = P->dW;
-  da.resw = P->resw_off >= 0 ? P->dW + P->resw_off : nullptr;
-  da.X = const_cast<float*>(x_src);
-  da.perm = P->identity ? nullptr : P->perm_d;
-  da.y = y; da.io = rollout ? P->io_d : nullptr; da.bc_slot = P->bc_slot_d;
-  da.prelu_only = P->dec_prelu;
-  HIP_TRY(launch_decode<NT>(da, st)); ++nk;
-  P->kernels_per_step = nk;
+}
+
+// ---------------------------------------------------------------------------- weight regions
+// Copies the operands one launch reads into a contiguous blob region and rewrites the
+// launch's offsets to LDS offsets (kernels stage the region per workgroup).
+struct RegionBuilder {
+  Blob& B;
+  int base, shift;
+  std::map<int, int> memo;
+  RegionBuilder(Blob& b, int sh) : B(b), shift(sh) { base = B.alloc(0); }
+  int put(int off, int len) {
+    if (off < 0) return off;
+    auto it = memo.find(off);
+    if (it != memo.end()) return it->second;
+    len = (len + 3) & ~3;
+    std::vector<float> tmp(len, 0.f);
+    for (int i = 0; i < len && off + i < (int)B.h.size(); ++i) tmp[i] = B.h[off + i];
+    const int pos = (int)B.h.size();
+    B.h.insert(B.h.end(), tmp.begin(), tmp.end());
+    const int r = pos - base + shift;
+    memo[off] = r;
+    return r;
+  }
+  WReg done() const { return WReg{base, (int)B.h.size() - base}; }
+};
+
+struct Relocator {
+  int NT, p;
+  void layer(RegionBuilder& R, LayerDev& L) {
+    L.a_off = R.put(L.a_off, L.tout * L.tin * 256);
+    L.b_off = R.put(L.b_off, 16 * L.tout);
+  }
+  void mlp(RegionBuilder& R, MlpDev& m) {
+    for (int i = 0; i < m.n; ++i) layer(R, m.l[i]);
+  }
+  void np(RegionBuilder& R, NpDesc& d) {
+    d.a_u = R.put(d.a_u, d.h1t * 2 * NT * 256);
+    d.a_v = R.put(d.a_v, d.h1t * 2 * NT * 256);
+    d.a_o = R.put(d.a_o, NT * NT * 256);
+  }
+  void epi(RegionBuilder& R, Epilogue& e) {
+    np(R, e.np);
+    e.uu_a = R.put(e.uu_a, e.uu_h1t * 2 * NT * 256);
+    if (e.dec.on) {
+      mlp(R, e.dec.dec);
+      e.dec.resw_off = R.put(e.dec.resw_off, 2 * p);
+    }
+  }
+};
+
+constexpr int kMaxRegionFloats = (160 * 1024 - kWaves * kRowsPerWave * 32 * 4) / 4;
+
+int relocate(msw_plan* P, std::vector<Launch>& q) {
+  Relocator rl{P->NT, P->p};
+  for (Launch& L : q) {
+    WReg* reg = nullptr;
+    int tot = 0;
+    if (L.kind == L_ENCODE) {
+      EncodeArgs& a = L.enc;
+      RegionBuilder R0(P->blob, 0);
+      rl.mlp(R0, a.stat);
+      a.reg = R0.done();
+      a.lds_floats = a.reg.len;
+      for (int s = 0; s < a.S; ++s) {
+        RegionBuilder Rs(P->blob, a.reg.len);
+        if (s == 0) {
+          rl.mlp(Rs, a.dynm);
+          rl.np(Rs, a.np0);
+        }
+        a.vu_a[s] = Rs.put(a.vu_a[s], a.vu_h1t * P->NT * 256);
+        a.sreg[s] = Rs.done();
+        a.lds_floats = std::max(a.lds_floats, a.reg.len + a.sreg[s].len);
+      }
+      tot = a.lds_floats;
+    } else if (L.kind == L_EDGE_HOP) {
+      EdgeHopArgs& a = L.eh;
+      RegionBuilder R(P->blob, 0);
+      a.b1_off = R.put(a.b1_off, 16 * a.h1t);
+      rl.mlp(R, a.rest);
+      a.filt_a = R.put(a.filt_a, P->NT * P->NT * 256);
+      if (a.last) rl.epi(R, a.epi);
+      a.reg = R.done();
+      reg = &a.reg;
+    } else if (L.kind == L_HOP) {
+      HopArgs& a = L.hop;
+      RegionBuilder R(P->blob, 0);
+      a.filt_a = R.put(a.filt_a, P->NT * P->NT * 256);
+      if (a.last) rl.epi(R, a.epi);
+      a.reg = R.done();
+      reg = &a.reg;
+    } else {
+      PoolArgs& a = L.pool;
+      RegionBuilder R(P->blob, 0);
+      rl.np(R, a.np);
+      a.reg = R.done();
+      reg = &a.reg;
+    }
+    if (reg) tot = reg->len;
+    if (tot > kMaxRegionFloats)
+      return fail(MSW_ERR_UNSUPPORTED, "weights of one launch exceed the LDS budget (" + std::to_string(tot * 4) + " B)");
+  }
   return MSW_OK;
 }
 
-int step_dispatch(msw_plan* P, const float* x_src, const int* perm, float* y, bool rollout,
-                  hipStream_t st) {
+template <int NT>
+hipError_t launch_one(const Launch& L, hipStream_t st) {
+  switch (L.kind) {
+    case L_ENCODE: return launch_encode<NT>(L.enc, st);
+    case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
+    case L_HOP: return launch_hop<NT>(L.hop, st);
+    default: return launch_pool<NT>(L.pool, st);
+  }
+}
+
+template <int NT>
+int run_schedule(msw_plan* P, const std::vector<Launch>& q, hipStream_t st) {
+  for (const Launch& L : q) HIP_TRY(launch_one<NT>(L, st));
+  P->kernels_per_step = (int)q.size();
+  return MSW_OK;
+}
+
+int schedule_dispatch(msw_plan* P, const std::vector<Launch>& q, hipStream_t st) {
   switch (P->NT) {
-    case 1: return enqueue_step<1>(P, x_src, perm, y, rollout, st);
-    case 2: return enqueue_step<2>(P, x_src, perm, y, rollout, st);
-    default: return enqueue_step<4>(P, x_src, perm, y, rollout, st);
+    case 1: return run_schedule<1>(P, q, st);
+    case 2: return run_schedule<2>(P, q, st);
+    default: return run_schedule<4>(P, q, st);
+  }
+}
+
+// Forward mode: point the encoder at x (graph rows) and the decoder at x / y.
+void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
+  for (Launch& L : q) {
+    if (L.kind == L_ENCODE) L.enc.x = x;
+    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi : nullptr;
+    if (e && e->dec.on) {
+      e->dec.X = x;
+      e->dec.y = y;
+    }
   }
 }
 
 int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   const int S = P->S, G = g->num_graphs;
+  if (S > kMaxScales) return fail(MSW_ERR_UNSUPPORTED, "more than 8 scales");
   if (g->num_nodes <= 0 || g->num_nodes > (1LL << 30)) return fail(MSW_ERR_INVALID, "num_nodes out of range");
   if (g->num_edges < 0 || g->num_edges > (1LL << 31) - 64) return fail(MSW_ERR_INVALID, "num_edges out of range");
   if (G < 1 || !g->node_ptr) return fail(MSW_ERR_INVALID, "node_ptr missing");
@@ -461,7 +670,8 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   const int N = (int)g->num_nodes;
   P->N = N;
   P->E = g->num_edges;
-  // internal numbering: scale-major, graph-major inside a scale
+  // internal numbering: scale-major (graph-major inside a scale), scale starts padded to
+  // multiples of 16 rows so that every 16-row wave tile lies in one scale
   P->perm.clear();
   P->sc.assign(S, ScaleCSR{});
   for (int s = 0; s < S; ++s) {
@@ -472,19 +682,22 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       for (int64_t v = a; v < b; ++v) P->perm.push_back((int)v);
     }
     P->sc[s].ns = (int)P->perm.size() - P->sc[s].n0;
+    P->perm.resize(round64((int)P->perm.size()), -1);
   }
-  if ((int)P->perm.size() != N) return fail(MSW_ERR_INVALID, "node_ptr does not cover every node exactly once");
+  P->Npad = (int)P->perm.size();
   P->iperm.assign(N, -1);
-  for (int i = 0; i < N; ++i) {
+  int covered = 0;
+  for (int i = 0; i < P->Npad; ++i) {
+    if (P->perm[i] < 0) continue;
     if (P->iperm[P->perm[i]] != -1) return fail(MSW_ERR_INVALID, "node_ptr ranges overlap");
     P->iperm[P->perm[i]] = i;
+    ++covered;
   }
-  P->identity = true;
-  for (int i = 0; i < N; ++i)
-    if (P->perm[i] != i) { P->identity = false; break; }
-  // per-scale CSR by destination
+  if (covered != N) return fail(MSW_ERR_INVALID, "node_ptr does not cover every node exactly once");
+  // per-scale CSR by destination + edge tiles
   const int64_t E = g->num_edges;
   if (g->edge_ptr[0] != 0 || g->edge_ptr[S] != E) return fail(MSW_ERR_INVALID, "edge_ptr must span [0, E]");
+  int rc;
   for (int s = 0; s < S; ++s) {
     ScaleCSR& c = P->sc[s];
     const int64_t a = g->edge_ptr[s], b = g->edge_ptr[s + 1];
@@ -510,8 +723,11 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       dso[i] = dstv[order[i]];
       c.eorig[i] = (int)(a + order[i]);
     }
-    int rc;
-    if ((rc = pupload(P, &c.rowptr, rowptr)) || (rc = pupload(P, &c.src, so)) || (rc = pupload(P, &c.dst, dso)))
+    std::vector<TileRange> tl;
+    if ((rc = build_tiles(rowptr, tl))) return rc;
+    c.ntiles = (int)tl.size();
+    if ((rc = pupload(P, &c.rowptr, rowptr)) || (rc = pupload(P, &c.src, so)) ||
+        (rc = pupload(P, &c.dst, dso)) || (rc = pupload(P, &c.tiles, tl)))
       return rc;
   }
   // intra-scale levels
@@ -542,87 +758,58 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       csr_build(cs.ns, ck, rp, order);
       std::vector<int> child(m.I);
       for (int i = 0; i < m.I; ++i) child[i] = fv[order[i]];
-      int rc;
-      if ((rc = pupload(P, &m.pool_rowptr, rp)) || (rc = pupload(P, &m.pool_child, child))) return rc;
+      std::vector<TileRange> pt;
+      if ((rc = build_tiles(rp, pt))) return rc;
+      m.pool_ntiles = (int)pt.size();
+      if ((rc = pupload(P, &m.pool_rowptr, rp)) || (rc = pupload(P, &m.pool_child, child)) ||
+          (rc = pupload(P, &m.pool_tiles, pt)))
+        return rc;
       csr_build(fs.ns, fk, rp, order);
       std::vector<int> us(m.I), ud(m.I);
       for (int i = 0; i < m.I; ++i) {
         us[i] = cv[order[i]];
         ud[i] = fv[order[i]];
       }
+      std::vector<TileRange> tl;
+      if ((rc = build_tiles(rp, tl))) return rc;
+      m.un_ntiles = (int)tl.size();
       if ((rc = pupload(P, &m.un_rowptr, rp)) || (rc = pupload(P, &m.un_src, us)) ||
-          (rc = pupload(P, &m.un_dst, ud)))
+          (rc = pupload(P, &m.un_dst, ud)) || (rc = pupload(P, &m.un_tiles, tl)))
         return rc;
     }
   }
   return MSW_OK;
 }
 
-}  // namespace
-
-namespace {
-template <int NT>
+// Re-launch one kernel of the rollout schedule (first of its kind on `scale`), with its
+// rollout side effects removed: no epilogue (the output goes to a scratch buffer), no
+// rollout step advance.
 int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
   if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
-  const Proc* pr = nullptr;
-  for (auto& q : P->procs)
-    if (q.scale == scale) { pr = &q; break; }
-  const ScaleCSR& g = P->sc[scale];
-  int64_t rows = 0, edges = 0;
-  for (int it = 0; it < iters; ++it) {
-    if (kernel == 0 || kernel == 1 || kernel == 2) {
-      if (!pr) return fail(MSW_ERR_INVALID, "no processor on that scale");
-      if (kernel == 0) {
-        HopArgs h{};
-        h.n0 = g.n0; h.R = g.ns; h.rowptr = g.rowptr; h.src = g.src; h.s = P->s; h.in = P->bufA;
-        h.out = P->bufB; h.A = pr->wt_off.empty() ? nullptr : P->dW + pr->wt_off[0];
-        h.grad = pr->with_gradient; h.upwind = pr->upwind;
-        HIP_TRY(launch_hop<NT>(h, st));
-        rows = g.ns; edges = g.E;
-      } else if (kernel == 1) {
-        EdgeMlpArgs em{};
-        em.E = g.E; em.src = g.src; em.dst = g.dst; em.U = P->U; em.V = P->V; em.Pe = pr->Pe;
-        em.b1 = P->dW + pr->b1_off; em.h1t = pr->h1t; em.act1 = pr->act1; em.slope1 = pr->slope1;
-        em.rest = pr->rest; em.W = P->dW + pr->rest_base; em.w_count = pr->rest_count;
-        em.normalize = pr->normalize; em.s = P->s; em.prelu_only = pr->prelu;
-        HIP_TRY(launch_edge_mlp<NT>(em, st));
-        rows = 0; edges = g.E;
-      } else {
-        NodeProjArgs np{};
-        np.r0 = g.n0; np.R = g.ns; np.xs = P->xs; np.xin = P->xin;
-        np.a_u = pr->a_u; np.a_v = pr->a_v; np.a_o = pr->a_o; np.W = P->dW;
-        np.U = P->U; np.V = P->V; np.O = P->bufA; np.h1t = pr->h1t;
-        HIP_TRY(launch_node_proj<NT>(np, st));
-        rows = g.ns; edges = 0;
-      }
-    } else if (kernel == 3) {
-      if (scale < 1) return fail(MSW_ERR_INVALID, "pooling targets scale >= 1");
-      PoolArgs pa{};
-      pa.n0 = g.n0; pa.R = g.ns; pa.rowptr = P->lv[scale - 1].pool_rowptr;
-      pa.child = P->lv[scale - 1].pool_child; pa.in = P->xdown; pa.out = P->bufB;
-      HIP_TRY(launch_pool<NT>(pa, st));
-      rows = g.ns; edges = P->lv[scale - 1].I;
-    } else if (kernel == 4) {
-      EncodeArgs ea{};
-      ea.x = P->X; ea.perm = nullptr; ea.N = P->N; ea.nnf = P->nnf; ea.nstat_raw = P->nstat_raw;
-      ea.with_wl = P->with_wl; ea.dyn = P->dyn; ea.stat = P->stat; ea.dynm = P->dynm; ea.W = P->dW;
-      ea.xs = P->bufA; ea.xd = P->bufB; ea.xd_rows = P->sc[0].n0 + P->sc[0].ns; ea.io = nullptr;
-      ea.prelu_only = P->enc_prelu;
-      HIP_TRY(launch_encode<NT>(ea, st));
-      rows = P->N; edges = 0;
-    } else if (kernel == 5) {
-      DecodeArgs da{};
-      da.N = P->N; da.nnf = P->nnf; da.dyn = P->dyn; da.p = P->p; da.xup = P->xup;
-      da.pre_act = P->gnn_act; da.pre_slope = P->gnn_slope; da.dec = P->dec; da.W = P->dW;
-      da.resw = P->resw_off >= 0 ? P->dW + P->resw_off : nullptr;
-      da.X = P->X; da.perm = P->identity ? nullptr : P->perm_d; da.y = P->bufB; da.io = nullptr;
-      da.bc_slot = P->bc_slot_d; da.prelu_only = P->dec_prelu;
-      HIP_TRY(launch_decode<NT>(da, st));
-      rows = P->N; edges = 0;
-    } else {
-      return fail(MSW_ERR_INVALID, "unknown kernel id");
+  if (P->sched_roll.empty()) return fail(MSW_ERR_INVALID, "run a rollout before bench_kernel");
+  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE};
+  if (kernel < 0 || kernel > 3) return fail(MSW_ERR_INVALID, "unknown kernel id");
+  const Launch* src = nullptr;
+  for (const Launch& L : P->sched_roll)
+    if (L.kind == kind_of[kernel] && (L.kind == L_ENCODE || L.scale == scale)) {
+      if (!src) src = &L;
+      if (L.kind == L_HOP && !L.hop.last) { src = &L; break; }  // prefer a middle hop
+      if (L.kind != L_HOP) break;
     }
+  if (!src) return fail(MSW_ERR_INVALID, "no such kernel on that scale");
+  Launch L = *src;
+  const ScaleCSR& g = P->sc[scale];
+  int64_t rows = g.ns, edges = g.E;
+  if (L.kind == L_HOP && L.hop.last) { L.hop.last = 0; L.hop.out = P->T[1]; }
+  if (L.kind == L_EDGE_HOP && L.eh.last) { L.eh.last = 0; L.eh.out = P->T[1]; }
+  if (L.kind == L_POOL) edges = P->lv[scale - 1].I;
+  if (L.kind == L_ENCODE) { L.enc.io = nullptr; rows = P->N; edges = 0; }
+  std::vector<Launch> q(1, L);
+  for (int it = 0; it < iters; ++it) {
+    int rc = schedule_dispatch(P, q, st);
+    if (rc) return rc;
   }
+  P->kernels_per_step = (int)P->sched_roll.size();
   if (units) { units[0] = rows; units[1] = edges; }
   return MSW_OK;
 }
@@ -644,6 +831,7 @@ int64_t msw_struct_size(const char* name) {
   if (!strcmp(name, "msw_plan_stats")) return sizeof(msw_plan_stats);
   return -1;
 }
+
 int msw_abi_version(void) { return MSW_ABI_VERSION; }
 
 int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device,
@@ -680,21 +868,9 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
 
   int rc = build_graph_plan(P.get(), g);
   if (rc) return rc;
-  const int F = P->F, N = P->N;
+  const int F = P->F, Npad = P->Npad;
 
   // ---- weights
-  if ((rc = pack_mlp(P->blob, m->static_encoder, P->stat))) return rc;
-  if ((rc = pack_mlp(P->blob, m->dynamic_encoder, P->dynm))) return rc;
-  if ((rc = pack_mlp(P->blob, m->decoder, P->dec))) return rc;
-  {
-    auto all_prelu = [](const msw_mlp& mm) {
-      for (int i = 0; i < mm.n_layers; ++i)
-        if (mm.layer[i].act != MSW_ACT_PRELU) return 0;
-      return 1;
-    };
-    P->enc_prelu = all_prelu(m->static_encoder) & all_prelu(m->dynamic_encoder);
-    P->dec_prelu = all_prelu(m->decoder);
-  }
   auto chain_ok = [&](const msw_mlp& mm, int last_out) {
     for (int i = 0; i < mm.n_layers; ++i) {
       const int want = (i == mm.n_layers - 1) ? last_out : F;
@@ -706,10 +882,12 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   if (!chain_ok(m->static_encoder, F) || !chain_ok(m->dynamic_encoder, F) || !chain_ok(m->decoder, 2) ||
       (m->edge_mlp && !chain_ok(m->edge_encoder, F)) || m->decoder.layer[0].in_features != F)
     return fail(MSW_ERR_UNSUPPORTED, "encoder/decoder hidden widths must equal hid_features");
+  if ((rc = pack_mlp(P->blob, m->static_encoder, P->stat))) return rc;
+  if ((rc = pack_mlp(P->blob, m->dynamic_encoder, P->dynm))) return rc;
+  if ((rc = pack_mlp(P->blob, m->decoder, P->dec))) return rc;
   if (m->static_encoder.layer[0].in_features != P->nstat_raw + P->with_wl)
     return fail(MSW_ERR_INVALID, "static encoder input width");
   if (m->dynamic_encoder.layer[0].in_features != P->dyn) return fail(MSW_ERR_INVALID, "dynamic encoder input width");
-  if (m->decoder.layer[m->decoder.n_layers - 1].out_features != 2) return fail(MSW_ERR_INVALID, "decoder output != 2");
   if (m->residual_weights) {
     P->resw_off = P->blob.alloc(2 * P->p);
     for (int i = 0; i < 2 * P->p; ++i) P->blob.h[P->resw_off + i] = m->residual_weights[i];
@@ -729,44 +907,64 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     const int scale = P->model_type == 1 ? 0 : (j <= S - 1 ? j : 2 * S - 2 - j);
     if (m->processors[j].edge_features != ef) return fail(MSW_ERR_INVALID, "processor edge_features mismatch");
     if ((rc = build_proc(P.get(), m->processors[j], scale, false, P->procs[j]))) return rc;
+    P->procs[j].par = j & 1;
   }
   P->unpools.resize(P->model_type == 0 ? m->num_unpool : 0);
   for (size_t i = 0; i < P->unpools.size(); ++i) {
     if (m->unpool[i].edge_features != 0) return fail(MSW_ERR_INVALID, "intra-scale layer with edge features");
     if (m->unpool[i].K != 1) return fail(MSW_ERR_UNSUPPORTED, "intra-scale layer with K != 1");
+    if (m->unpool[i].with_gradient) return fail(MSW_ERR_UNSUPPORTED, "intra-scale layer with gradient");
     if ((rc = build_proc(P.get(), m->unpool[i], P->S - 2 - (int)i, true, P->unpools[i]))) return rc;
   }
+  P->prelu = all_prelu(m->static_encoder) & all_prelu(m->dynamic_encoder) & all_prelu(m->decoder);
 
   // ---- device buffers
-  if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
   if ((rc = pupload(P.get(), &P->perm_d, P->perm))) return rc;
-  std::vector<int> minus1(N, -1);
+  std::vector<int> minus1(Npad, -1);
   if ((rc = pupload(P.get(), &P->bc_slot_d, minus1))) return rc;
   if ((rc = palloc(P.get(), &P->io_d, 1))) return rc;
+  HIP_TRY(hipMemset(P->io_d, 0, sizeof(RolloutIO)));
   int Emax = 1;
   for (auto& c : P->sc) Emax = std::max(Emax, c.E);
-  for (auto& l : P->lv) Emax = std::max(Emax, l.I);
-  const size_t NF = (size_t)N * F;
-  const size_t NH = (size_t)N * 16 * P->h1t_max;
-  float** bufs[] = {&P->xs, &P->xd0, &P->bufA, &P->bufB, &P->xin, &P->xdown, &P->xup};
+  const size_t NF = (size_t)Npad * F;
+  const size_t NH = (size_t)Npad * 16 * P->h1t_max;
+  float** bufs[] = {&P->xs, &P->xd0, &P->O[0], &P->O[1], &P->T[0], &P->T[1], &P->xdown, &P->xup, &P->xgnn};
   for (float** b : bufs) {
     if ((rc = palloc(P.get(), b, NF))) return rc;
     HIP_TRY(hipMemset(*b, 0, NF * sizeof(float)));
   }
-  if (P->model_type == 1) {
-    P->gnnbuf[0] = P->xin;
-    P->gnnbuf[1] = P->xdown;
+  float** hbufs[] = {&P->U[0], &P->V[0], &P->U[1], &P->V[1], &P->Uu, &P->Vu};
+  for (float** b : hbufs) {
+    if ((rc = palloc(P.get(), b, NH))) return rc;
+    HIP_TRY(hipMemset(*b, 0, NH * sizeof(float)));
   }
-  if ((rc = palloc(P.get(), &P->U, NH)) || (rc = palloc(P.get(), &P->V, NH))) return rc;
   if ((rc = palloc(P.get(), &P->s, (size_t)Emax * F))) return rc;
-  if ((rc = palloc(P.get(), &P->X, (size_t)N * P->nnf))) return rc;
+  if ((rc = palloc(P.get(), &P->X, (size_t)Npad * P->nnf))) return rc;
+  HIP_TRY(hipMemset(P->X, 0, (size_t)Npad * P->nnf * sizeof(float)));
+  if (P->E > 0)
+    for (Proc& pr : P->procs)
+      if ((rc = palloc(P.get(), &pr.Pe, (size_t)std::max(P->sc[pr.scale].E, 1) * 16 * pr.h1t))) return rc;
+
+  // ---- launch schedules (forward / rollout), per-launch weight regions, weight upload
+  sched_step(P.get(), P->sched_fwd, false);
+  sched_step(P.get(), P->sched_roll, true);
+  if (P->NT <= 2) {
+    if ((rc = relocate(P.get(), P->sched_fwd)) || (rc = relocate(P.get(), P->sched_roll))) return rc;
+  }
+  if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
+  for (auto* q : {&P->sched_fwd, &P->sched_roll})
+    for (Launch& L : *q) L.common().W = P->dW;
+  switch (P->NT) {
+    case 1: HIP_TRY(prepare_kernels<1>()); break;
+    case 2: HIP_TRY(prepare_kernels<2>()); break;
+    default: HIP_TRY(prepare_kernels<4>()); break;
+  }
 
   // ---- static per-edge features: edge encoder + edge part of each processor's layer 1
   if (P->E > 0) {
     const int64_t E = P->E;
     std::vector<float> ea((size_t)E * ef_raw);
-    // CSR order, scale by scale (matching ScaleCSR::eorig)
-    std::vector<int64_t> sbase(P->S + 1, 0);
+    std::vector<int64_t> sbase(P->S + 1, 0);  // CSR order, scale by scale (ScaleCSR::eorig)
     for (int s = 0; s < P->S; ++s) sbase[s + 1] = sbase[s] + P->sc[s].E;
     for (int s = 0; s < P->S; ++s)
       for (int i = 0; i < P->sc[s].E; ++i)
@@ -791,25 +989,19 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
       Proc& pr = P->procs[j];
       const msw_linear& L1 = m->processors[j].edge_mlp.layer[0];
       const int H1 = L1.out_features;
-      // single-layer MLP: Pe = W1[:, 4F:4F+ef] . feat + b1 (no activation)
-      Blob tb;
+      Blob tb;  // Pe = W1[:, 4F:4F+ef] . feat + b1: one NT -> 2NT layer (zero padded)
       MlpDev md{};
       md.n = 1;
-      md.l[0].tin = P->NT;       // k_rowmlp<NT, 1>: one NT -> 2NT layer (zero padded)
+      md.l[0].tin = P->NT;
       md.l[0].tout = 2 * P->NT;
       md.l[0].a_off = pack_operand(tb, L1.weight, L1.in_features, 2 * P->NT, P->NT,
                                    [&](int k) { return k < feat_dim ? 4 * F + k : -1; },
                                    [&](int o) { return o < H1 ? o : -1; });
-      md.l[0].b_off = -1;
-      if (L1.bias) {
-        md.l[0].b_off = tb.alloc(16 * 2 * P->NT);
-        for (int o = 0; o < H1; ++o) tb.h[md.l[0].b_off + o] = L1.bias[o];
-      }
+      md.l[0].b_off = pack_bias(tb, L1.bias, H1, 2 * P->NT);
       md.l[0].act = 0;
       float* tw = nullptr;
       if ((rc = upload(&tw, tb.h, tmp_bytes))) return rc;
       const ScaleCSR& c = P->sc[pr.scale];
-      if ((rc = palloc(P.get(), &pr.Pe, (size_t)std::max(c.E, 1) * 16 * pr.h1t))) return rc;
       RowMlpArgs ra{};
       ra.mode = 1;
       ra.in = feat + (size_t)sbase[pr.scale] * feat_stride; ra.in_stride = feat_stride;
@@ -839,8 +1031,8 @@ int msw_plan_destroy(msw_plan* plan) {
 int msw_forward(msw_plan* P, const float* x, float* y, void* stream) {
   if (!P || !x || !y) return fail(MSW_ERR_INVALID, "null argument");
   HIP_TRY(hipSetDevice(P->device));
-  hipStream_t st = (hipStream_t)stream;
-  int rc = step_dispatch(P, x, P->identity ? nullptr : P->perm_d, y, false, st);
+  patch_forward(P->sched_fwd, x, y);
+  int rc = schedule_dispatch(P, P->sched_fwd, (hipStream_t)stream);
   if (rc) return rc;
   P->forward_calls++;
   return MSW_OK;
@@ -891,15 +1083,15 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
   io.bc = bc; io.out = out; io.bc_tstride = bc_tstride; io.type_bc = type_bc; io.T = T; io.step = -1;
   HIP_TRY(launch_set_io(P->io_d, io, st));
   InitArgs ia{};
-  ia.x0 = x0; ia.perm = P->identity ? nullptr : P->perm_d; ia.N = P->N; ia.nnf = P->nnf;
+  ia.x0 = x0; ia.perm = P->perm_d; ia.N = P->Npad; ia.nnf = P->nnf;
   ia.dyn = P->dyn; ia.p = P->p; ia.X = P->X; ia.io = P->io_d; ia.bc_slot = P->bc_slot_d;
   HIP_TRY(launch_init_state(ia, st));
-  if (P->use_graph && T > 0) {
+  if (P->use_graph) {
     if (!P->step_exec) {
       if (!P->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&P->cap_stream, hipStreamNonBlocking));
       hipGraph_t graph = nullptr;
       HIP_TRY(hipStreamBeginCapture(P->cap_stream, hipStreamCaptureModeThreadLocal));
-      int rc = step_dispatch(P, P->X, nullptr, nullptr, true, P->cap_stream);
+      int rc = schedule_dispatch(P, P->sched_roll, P->cap_stream);
       hipError_t ce = hipStreamEndCapture(P->cap_stream, &graph);
       if (rc) return rc;
       if (ce != hipSuccess) return fail(MSW_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
@@ -913,7 +1105,7 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
     for (int t = 0; t < T; ++t) HIP_TRY(hipGraphLaunch(P->step_exec, st));
   } else {
     for (int t = 0; t < T; ++t) {
-      int rc = step_dispatch(P, P->X, nullptr, nullptr, true, st);
+      int rc = schedule_dispatch(P, P->sched_roll, st);
       if (rc) return rc;
     }
   }
@@ -927,11 +1119,7 @@ int msw_bench_kernel(msw_plan* P, int32_t kernel, int32_t scale, int32_t iters, 
   if (!P || iters < 0) return fail(MSW_ERR_INVALID, "bad argument");
   HIP_TRY(hipSetDevice(P->device));
   hipStream_t st = (hipStream_t)stream;
-  switch (P->NT) {
-    case 1: return bench_kernel<1>(P, kernel, scale, iters, units, st);
-    case 2: return bench_kernel<2>(P, kernel, scale, iters, units, st);
-    default: return bench_kernel<4>(P, kernel, scale, iters, units, st);
-  }
+  return bench_kernel(P, kernel, scale, iters, units, st);
 }
 
 int msw_debug_buffer(msw_plan* P, const char* name, float* dst, void* stream) {
@@ -939,14 +1127,28 @@ int msw_debug_buffer(msw_plan* P, const char* name, float* dst, void* stream) {
   const float* src = nullptr;
   if (!strcmp(name, "x_s")) src = P->xs;
   else if (!strcmp(name, "x_d")) src = P->xd0;
-  else if (!strcmp(name, "x_down")) src = P->xdown;
-  else if (!strcmp(name, "x_in")) src = P->xin;
+  else if (!strcmp(name, "x_down")) src = P->model_type == 0 ? P->xdown : nullptr;
   else if (!strcmp(name, "x_up")) src = P->model_type == 0 ? P->xup : nullptr;
   if (!src) return fail(MSW_ERR_INVALID, std::string("unknown buffer ") + name);
-  if (!P->identity) return fail(MSW_ERR_UNSUPPORTED, "debug buffers only for identity numbering");
-  hipStream_t st = (hipStream_t)stream;
-  HIP_TRY(hipMemcpy2DAsync(dst, P->F * sizeof(float), src, P->F * sizeof(float), P->F * sizeof(float),
-                           P->N, hipMemcpyDeviceToDevice, st));
+  // debug only: synchronous host round trip into graph numbering
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  std::vector<float> h((size_t)P->Npad * P->F), o((size_t)P->N * P->F);
+  HIP_TRY(hipMemcpy(h.data(), src, h.size() * sizeof(float), hipMemcpyDeviceToHost));
+  for (int i = 0; i < P->Npad; ++i)
+    if (P->perm[i] >= 0)
+      std::copy(h.begin() + (size_t)i * P->F, h.begin() + (size_t)(i + 1) * P->F, o.begin() + (size_t)P->perm[i] * P->F);
+  HIP_TRY(hipMemcpy(dst, o.data(), o.size() * sizeof(float), hipMemcpyHostToDevice));
+  return MSW_OK;
+}
+
+int msw_set_trace(msw_plan* P, uint64_t* buf) {
+  if (!P) return fail(MSW_ERR_INVALID, "null plan");
+  for (auto* q : {&P->sched_fwd, &P->sched_roll})
+    for (Launch& L : *q) L.common().trace = reinterpret_cast<unsigned long long*>(buf);
+  if (P->step_exec) {  // the captured step holds the old arguments
+    (void)hipGraphExecDestroy(P->step_exec);
+    P->step_exec = nullptr;
+  }
   return MSW_OK;
 }
 

@@ -10,7 +10,10 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmswegnn.so")
+# MSW_LIB_VARIANT=trace selects the diagnostic build (tools/trace_kernels.py)
+_VARIANT = os.environ.get("MSW_LIB_VARIANT", "")
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib",
+                        f"libmswegnn_{_VARIANT}.so" if _VARIANT else "libmswegnn.so")
 
 MSW_OK = 0
 MAX_MLP_LAYERS = 4
@@ -85,6 +88,7 @@ SYMBOLS = [
     ("msw_struct_size", C.c_int64, [C.c_char_p]),
     ("msw_bench_kernel", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_int64_p,
                                    C.c_void_p]),
+    ("msw_set_trace", C.c_int, [C.c_void_p, C.c_void_p]),
 ]
 
 STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,

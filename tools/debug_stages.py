@@ -24,11 +24,3 @@ for i in range(4):
     ref = fx[f'mid__gnn_processor_{3+i}'][a:b]
     print(f'proc{3+i} scale{s}: rel {rel_err(xu[a:b], ref):.3e}  max|ref| {np.abs(ref).max():.3f}')
 print('y rel', rel_err(y.cpu(), fx['y']))
-xi = plan.debug_buffer('x_in', F).cpu()
-for i in range(3):
-    s = 2 - i; a, b = np_[s], np_[s+1]
-    ref = fx[f'mid__intra_scale_gnn_{i}'][a:b] + fx[f'mid__gnn_processor_{s}'][a:b]
-    print(f'unpool{i} -> scale{s}: rel {rel_err(xi[a:b], ref):.3e}  max|ref| {np.abs(ref).max():.3f}')
-    a2, b2 = np_[s+1], np_[s+2]
-    print('   hook coarse rows == proc out?', rel_err(fx[f'mid__intra_scale_gnn_{i}'][a2:b2], fx[f'mid__gnn_processor_{3+i}'][a2:b2]),
-          ' fine rows of proc input x_d zero?', np.abs(fx[f'mid__gnn_processor_{3+i}'][a:b]).max())

@@ -1,0 +1,63 @@
+"""Phase-by-phase latency chain of single launches (diagnostic build, GPU box).
+
+    python mswe-gnn_amd/build_engine.py --trace      # here (cross-compiles)
+    MSW_LIB_VARIANT=trace python tools/trace_kernels.py [workload]   # on the GPU box
+
+Wave 0 of workgroup 0 drains its memory counters at each phase mark and records
+{shader clock, 100 MHz clock} (kernels_impl.h MSW_MARK), so each line below is the time
+from the kernel's first instruction to that mark along ONE wave's dependency chain
+(the drains remove overlap: a lower bound on what a phase costs in the real kernel is the
+difference between consecutive marks).
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mswe-gnn_amd")]
+os.environ.setdefault("MSW_LIB_VARIANT", "trace")
+
+import ctypes as C  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from mswegnn import _lib as L  # noqa: E402
+from mswegnn.engine import plan_for  # noqa: E402
+
+PHASES = {0: "entry", 1: "tile/args", 2: "weights staged", 3: "indices", 4: "gathers",
+          5: "edge MLP", 6: "message", 7: "segmented sum", 8: "filter", 9: "end (epilogue)"}
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "zenodo4"
+    dev = torch.device("cuda:0")
+    g, m, w, desc = bench.build_workload(wl, seed=0, T=8)
+    g = g.to(dev)
+    m = m.to(dev)
+    m.engine = "hip"
+    plan = plan_for(m, g)
+    plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, 8)
+    buf = torch.zeros(20, dtype=torch.int64, device=dev)
+    L.check(L.lib().msw_set_trace(plan._h, C.c_void_p(buf.data_ptr())))
+    S = desc["num_scales"]
+    cases = [("encode", 0)] + [(k, s) for s in range(S) for k in ("edge_hop", "hop")] + \
+        [("pool", s) for s in range(1, S)]
+    for kern, scale in cases:
+        for rep in range(3):  # the last repetition is reported (warm caches)
+            buf.zero_()
+            plan.bench_kernel(kern, scale, 1)
+            torch.cuda.synchronize()
+        t = buf.cpu().tolist()
+        clk0, rt0 = t[0], t[1]
+        marks = [(k, t[2 * k] - clk0, (t[2 * k + 1] - rt0) * 10.0) for k in range(10) if t[2 * k] != 0]
+        last = marks[-1]
+        mhz = last[1] / (last[2] / 1e3) if last[2] > 0 else float("nan")
+        print(f"{kern:9s} scale {scale}: {last[2] / 1e3:6.2f} us on wave 0 (~{mhz:.0f} MHz)")
+        prev = 0.0
+        for k, cyc, ns in marks[1:]:
+            print(f"    {PHASES[k]:16s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
+            prev = ns
+    L.check(L.lib().msw_set_trace(plan._h, None))
+
+
+if __name__ == "__main__":
+    main()
