@@ -54,6 +54,8 @@ def build_workload(name, seed, T):
         "dk15": dict(mesh="dk15", S=4, F=32, K=4, weights="K4_F32"),
         # config 5: ~1M fine nodes, 3 scales, fully wet (every edge active)
         "hbm1m": dict(mesh="hbm1m", S=3, F=32, K=4, weights=None),
+        # plumbing size for the CPU (gloo) tests of the multi-rank path
+        "tiny": dict(mesh="tiny", S=4, F=32, K=4, weights="K4_F32"),
     }
     w = table[name]
     g = make_multiscale_mesh(**mesh_config(w["mesh"]), seed=seed, T=T)
@@ -74,6 +76,30 @@ def build_workload(name, seed, T):
                 fine_nodes=n0, all_nodes=int(g.x.shape[0]), edges=int(g.edge_index.shape[1]),
                 rollout_steps=T)
     return g, m, w, desc
+
+
+def make_gatherer(dist, world, n0, T, device):
+    """The end-of-rollout collective: ONE all-gather of every rank's fine-scale rollout
+    [n0_r, 2, T].  Sizes are exchanged once here (meshes may differ per rank); payloads are
+    padded to the largest n0.  Returns gather(out_fine) -> list of [n0_r, 2, T] per rank."""
+    if world == 1:
+        return lambda out_fine: [out_fine]
+    sz = torch.tensor([n0], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(sz) for _ in range(world)]
+    dist.all_gather(sizes, sz)
+    sizes = [int(x.item()) for x in sizes]
+    nmax = max(sizes)
+    slots = [torch.empty(nmax, 2, T, device=device) for _ in range(world)]
+    pad = torch.zeros(nmax, 2, T, device=device)
+
+    def gather(out_fine):
+        src = out_fine
+        if n0 != nmax:
+            pad[:n0].copy_(out_fine)
+            src = pad
+        dist.all_gather(slots, src.contiguous())
+        return [slots[r][:sizes[r]] for r in range(world)]
+    return gather
 
 
 def time_kernel(plan, kernel, scale, iters=200):
@@ -130,12 +156,12 @@ def main():
     from mswegnn.engine import plan_for
     plan = plan_for(model, g)
     out = torch.empty(g.num_nodes, 2, T, device=dev)
-    gathered = [torch.empty(n0, 2, T, device=dev) for _ in range(world)] if world > 1 else None
+    gather = make_gatherer(dist, world, n0, T, dev)
 
     def one_step():
         plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T, out=out)
         if world > 1:
-            dist.all_gather(gathered, out[:n0])
+            gather(out[:n0])
 
     for _ in range(args.warmup):
         one_step()

@@ -125,11 +125,27 @@ class _EngineMixin:
         return plan_for(self, graph)
 
     def rollout(self, graph, steps: Optional[int] = None):
-        """Fused autoregressive rollout on the GPU (rollout_test semantics,
-        training/train.py:67-95) -> [N, 2, T]."""
-        from mswegnn.engine import plan_for
+        """Autoregressive rollout (rollout_test semantics, training/train.py:67-95) -> [N, 2, T].
+
+        GPU graph (engine 'auto' / 'hip'): one fused msw_rollout call, every step replaying a
+        captured hipGraph.  CPU graph or engine='torch': the step-by-step torch path."""
         T = graph.y.shape[-1] if steps is None else steps
-        return plan_for(self, graph).rollout(graph.x, graph.BC, graph.node_BC, graph.type_BC, T)
+        with torch.no_grad():
+            if _engine_wanted(self, graph.x):
+                from mswegnn.engine import plan_for
+                return plan_for(self, graph).rollout(graph.x, graph.BC, graph.node_BC,
+                                                     graph.type_BC, T)
+            from utils.dataset import apply_boundary_condition, use_prediction
+            dyn = self.previous_t * self.NUM_WATER_VARS
+            temp = graph.clone()
+            preds = []
+            for t in range(T):
+                temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, t],
+                                                            temp.node_BC, type_BC=temp.type_BC)
+                pred = self(temp)
+                temp.x = use_prediction(temp.x, pred, self.previous_t)
+                preds.append(pred)
+            return torch.stack(preds, -1) if preds else graph.x.new_zeros(graph.x.shape[0], 2, 0)
 
 
 class GNN(_EngineMixin, BaseFloodModel):

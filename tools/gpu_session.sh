@@ -27,4 +27,15 @@ if [[ $MODE == all || $MODE == prof ]]; then
   rm -rf $OUT/prof
   step rocprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 fi
+if [[ $MODE == pmc ]]; then
+  export TMPDIR=/tmp
+  rm -rf $OUT/pmc_fetch $OUT/pmc_write
+  KRE='k_hop|k_edge_hop|k_pool|k_encode'
+  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_fetch.log 2>&1
+  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_write.log 2>&1
+  python3 tools/pmc_summary.py $OUT/pmc_summary.json $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_summary.log 2>&1
+fi
+if [[ $MODE == trace ]]; then
+  step trace 300 python tools/trace_kernels.py > $OUT/trace.log 2>&1
+fi
 echo done >> $OUT/steps.log

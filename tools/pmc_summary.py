@@ -1,0 +1,55 @@
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into profiles/<round>/pmc_summary.json.
+
+    python tools/pmc_summary.py OUT.json DIR_FETCH DIR_WRITE
+
+Per (kernel, grid) the counters are averaged over dispatches.  gfx950 correction
+(MI355X_MICROARCH.md §HBM): FETCH_SIZE (KB) reports half the bytes of 16-B/lane
+coalesced reads -> read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE (KB) is exact for
+16-B/lane stores.  Infinity-Cache hits are counted too (memory-side L2 requests), so at
+sizes that fit the 256 MB L3 this is L2-miss traffic, an upper bound on HBM bytes.
+"key" entries: the fine-scale middle hop (the bench roofline kernel) = the k_hop grid with
+the most dispatches (bench.py times it 200+ times).
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def load(d, counter):
+    files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+    acc = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0].replace("void msw::", "").replace("msw::", "")
+            grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)))
+            acc[(name, grid)].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main():
+    out, dfetch, dwrite = sys.argv[1:4]
+    fe, wr = load(dfetch, "FETCH_SIZE"), load(dwrite, "WRITE_SIZE")
+    table = {}
+    for key in sorted(set(fe) | set(wr)):
+        f, w = fe.get(key, []), wr.get(key, [])
+        rd = 2 * 1024 * sum(f) / len(f) if f else None
+        wb = 1024 * sum(w) / len(w) if w else None
+        table[f"{key[0]} grid={key[1]}"] = {
+            "dispatches": max(len(f), len(w)), "read_bytes_per_launch": rd,
+            "write_bytes_per_launch": wb,
+            "hbm_bytes_per_launch": (rd or 0) + (wb or 0) if (rd is not None or wb is not None) else None}
+    hops = [(k, v) for k, v in table.items() if k.startswith("k_hop")]
+    res = {"note": __doc__.strip().splitlines()[2], "kernels": table}
+    if hops:
+        k, v = max(hops, key=lambda kv: kv[1]["dispatches"])
+        res["k_hop"] = dict(v, kernel=k)
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res.get("k_hop"), indent=1))
+
+
+if __name__ == "__main__":
+    main()
