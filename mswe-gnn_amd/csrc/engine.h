@@ -101,9 +101,19 @@ struct EncodeArgs {
   RolloutIO* io;           // rollout mode: advance io->step
 };
 
-// Edge tile: whole destination neighbourhoods, <= 16 edges and <= 16 destinations.
+// Edge tile: whole destination neighbourhoods, <= 16 edges and <= 16 destinations (host).
 struct TileRange {
   int node0, nnode, edge0, nedge;  // local node index / local CSR edge index
+};
+// What lane j of a tile's wave needs, one 16-B load: as edge lane, edge slot j of the tile
+// (source row, local lane of its destination); as node lane, destination j (row, slot
+// range [q & 255, q >> 8) of its in-edges).  Per-edge arrays (Pe, s) are tile-padded:
+// edge slot j of tile t lives at row 16 t + j.
+struct LaneRec {
+  int src;  // internal source row, -1 = no edge in this slot
+  int dl;   // destination lane (0..15) of the edge
+  int n;    // internal destination row, -1 = no node in this lane
+  int q;    // q0 | q1 << 8
 };
 
 struct Epilogue {
@@ -119,19 +129,16 @@ struct EdgeHopArgs {
   Common c;
   WReg reg;
   int n0;                          // first internal row of the destination scale
-  const TileRange* tiles; int ntiles;
-  const int* rowptr;               // [ns+1] local CSR (by destination)
-  const int* src;                  // [E] internal ids (CSR order)
-  const int* dst;                  // [E] internal ids (CSR order)
+  const LaneRec* recs; int ntiles; // [ntiles][16]
   const float* xs;
   const float* U; const float* V;  // [Npad][16*h1t]
-  const float* Pe;                 // [E][16*h1t] or null (then bias b1_off)
+  const float* Pe;                 // [16 ntiles][16*h1t] or null (then bias b1_off)
   int b1_off;
   int h1t;
   int act1; float slope1;
   MlpDev rest;                     // layers 2..L
   int normalize;
-  float* s;                        // [E][F] (null: not needed later)
+  float* s;                        // [16 ntiles][F] (null: not needed later)
   const float* in;                 // out_0 rows [Npad][F]
   int own_zero;                    // destination rows read as zero (intra_scale_gnn)
   int grad, upwind;
@@ -147,11 +154,8 @@ struct HopArgs {
   Common c;
   WReg reg;
   int n0;                  // first internal row of the scale
-  const TileRange* tiles; int ntiles;
-  const int* rowptr;       // [ns+1] local CSR into src / dst / s
-  const int* src;
-  const int* dst;
-  const float* s;          // [E][F]
+  const LaneRec* recs; int ntiles;
+  const float* s;          // [16 ntiles][F]
   const float* xs;
   const float* in;         // [Npad][F]
   float* out;              // [Npad][F]
@@ -166,9 +170,7 @@ struct PoolArgs {
   Common c;
   WReg reg;
   int n0;                  // first internal row of the coarse scale
-  const TileRange* tiles; int ntiles;  // tiles of coarse nodes / their children
-  const int* rowptr;       // [ns+1] local, by coarse node
-  const int* child;
+  const LaneRec* recs; int ntiles;  // edge lanes = children, node lanes = coarse nodes
   const float* in;         // x_down
   const float* xs;
   NpDesc np;

@@ -34,11 +34,16 @@ __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4
 __device__ __forceinline__ float hsum(f32x4 v) { return (v.x + v.y) + (v.z + v.w); }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// sum over the 4 lane groups holding one row (lanes j, j+16, j+32, j+48)
+// sum over the 4 lane groups holding one row (lanes j, j+16, j+32, j+48): gfx950's
+// v_permlane16_swap / v_permlane32_swap exchange rows of 16 lanes in registers (no LDS
+// round trip as ds_bpermute would take); every lane gets (g0 + g1) + (g2 + g3).
 __device__ __forceinline__ float row_sum(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+  const unsigned u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const unsigned us = __float_as_uint(s);
+  const auto b = __builtin_amdgcn_permlane32_swap(us, us, false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
@@ -377,30 +382,33 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------- message passing
-// One wave = one tile of whole destination neighbourhoods (<= 16 edges, <= 16 nodes):
-// lane j is edge tr.edge0 + j in the edge phase and node tr.node0 + j in the node phase;
-// the messages cross lanes through the wave's LDS slab (no atomics, reference edge order).
-struct TileLanes {
-  bool ev, anye, nv;
-  int e, ln, n, q0, q1;
-  size_t sr, dc;
+// One wave = one edge tile (whole destination neighbourhoods, <= 16 edges, <= 16 nodes).
+// Lane j is edge slot j in the edge phase and destination j in the node phase; per-node
+// rows the edges need (V, out at the destination) are loaded ONCE by the node lanes and
+// handed to the edge lanes through the wave's LDS slab, the messages go back through the
+// same slab (no atomics; every destination sums its messages in the reference's edge
+// order).
+struct Lanes {
+  bool ev, nv;
+  int dl, q0, q1;
+  size_t sr, n;   // source row (edge lane) / destination row (node lane), safe rows if absent
+  size_t p;       // tile-padded edge slot
 };
-__device__ __forceinline__ TileLanes tile_lanes(const TileRange& tr, int j, int n0, const int* __restrict__ src,
-                                                const int* __restrict__ dst, const int* __restrict__ rowptr) {
-  TileLanes t;
-  t.ev = j < tr.nedge;
-  t.anye = tr.nedge > 0;
-  // an edge-less tile still runs the (discarded) edge math on edge 0 / node n0, so the wave
-  // stays converged without indexing past the edge arrays
-  t.e = t.anye ? tr.edge0 + (t.ev ? j : 0) : 0;
-  t.sr = t.anye ? (size_t)src[t.e] : (size_t)n0;
-  t.dc = t.anye ? (size_t)dst[t.e] : (size_t)n0;
-  t.nv = j < tr.nnode;
-  t.ln = tr.node0 + (t.nv ? j : 0);
-  t.n = n0 + t.ln;
-  t.q0 = rowptr[t.ln] - tr.edge0;
-  t.q1 = t.nv ? rowptr[t.ln + 1] - tr.edge0 : t.q0;
-  return t;
+__device__ __forceinline__ Lanes lanes_of(const LaneRec& r, int tile, int j, int n0) {
+  Lanes L;
+  L.ev = r.src >= 0;
+  L.nv = r.n >= 0;
+  L.dl = L.ev ? r.dl : 0;
+  L.sr = (size_t)(L.ev ? r.src : n0);
+  L.n = (size_t)(L.nv ? r.n : n0);
+  L.q0 = r.q & 255;
+  L.q1 = L.nv ? (r.q >> 8) : L.q0;
+  L.p = (size_t)tile * kRowsPerWave + j;
+  return L;
+}
+__device__ __forceinline__ LaneRec load_rec(const LaneRec* recs, int tile, int j) {
+  const int4 v = reinterpret_cast<const int4*>(recs)[(size_t)tile * kRowsPerWave + j];
+  return LaneRec{v.x, v.y, v.z, v.w};
 }
 
 // msg_e = active(e) * (out[col] - out[row]) * s_e  (or s_e * out[row])   (gnn.py:406-435)
@@ -432,26 +440,30 @@ __device__ __forceinline__ void put_message(float* slab_row, const f32x4 (&os)[N
   }
 }
 
-// Node phase: agg = sum of the node's messages (edge order), out' = base + W agg [+ skip].
-template <int NT>
-__device__ __forceinline__ void gather_messages(f32x4 (&agg)[NT], const float* slab, int q0, int q1, int g) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT;
+__device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
   __builtin_amdgcn_wave_barrier();
+}
+
+// Node phase: agg = sum of the node's messages (edge order).
+template <int NT, int STRIDE>
+__device__ __forceinline__ void gather_messages(f32x4 (&agg)[NT], const float* slab, int q0, int q1, int g) {
+#pragma clang fp contract(off)
+  wave_lds_sync();
 #pragma unroll
   for (int t = 0; t < NT; ++t) agg[t] = zero4();
   for (int q = q0; q < q1; ++q) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) agg[t] = agg[t] + ld4(slab + q * F + 16 * t + 4 * g);
+    for (int t = 0; t < NT; ++t) agg[t] = agg[t] + ld4(slab + q * STRIDE + 16 * t + 4 * g);
   }
 }
 
+// res += W agg (filter; agg is already in B-operand layout) or res += agg
 template <int NT>
 __device__ __forceinline__ void apply_filter(f32x4 (&res)[NT], const f32x4 (&agg)[NT], int filt_a,
                                              const float* W, int lane) {
 #pragma clang fp contract(off)
-  if (filt_a >= 0) {  // filter W_{k}; agg is already in B-operand layout
+  if (filt_a >= 0) {
     f32x4 acc[NT];
     proj<NT, NT>(agg, acc, W + filt_a, lane);
 #pragma unroll
@@ -470,16 +482,36 @@ __device__ __forceinline__ void apply_filter(f32x4 (&res)[NT], const f32x4 (&agg
 template <int NT, int ACT>
 __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
 #pragma clang fp contract(off)
-  constexpr int F = 16 * NT, T2 = 2 * NT;
-  __shared__ __attribute__((aligned(16))) float msg[kWaves][kRowsPerWave][F];
+  // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
+  constexpr int F = 16 * NT, T2 = 2 * NT, XS = 16 * T2 + F + 4;
+  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int tile = blockIdx.x * kWaves + w;
   const bool live = tile < a.ntiles;
-  MSW_MARK(a.c, 0);
-  const TileRange tr = a.tiles[live ? tile : 0];
   Common c = a.c;
+  MSW_MARK(c, 0);
+  const int tsafe = live ? tile : 0;  // idle waves of the last workgroup stay in bounds
+  const LaneRec rec = load_rec(a.recs, tsafe, j);
   MSW_MARK(c, 1);
+  const Lanes L = lanes_of(rec, tsafe, j, a.n0);
+  // every HBM row the tile needs, issued before the weight staging
+  const int hs = 16 * a.h1t;
+  f32x4 Us[T2], Ps[T2], Vn[T2], os[NT], inn[NT], sk[NT];
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    const bool on = t < a.h1t;
+    Us[t] = on ? ld4(a.U + L.sr * hs + off) : zero4();
+    Vn[t] = on ? ld4(a.V + L.n * hs + off) : zero4();
+    Ps[t] = (on && a.Pe) ? ld4(a.Pe + L.p * hs + off) : zero4();
+  }
+  load_row<NT>(os, a.in + L.sr * F, g);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    inn[t] = a.own_zero ? zero4() : ld4(a.in + L.n * F + 16 * t + 4 * g);
+    sk[t] = a.skip ? ld4(a.skip + L.n * F + 16 * t + 4 * g) : zero4();
+  }
   if constexpr (kStaged<NT>) {
     stage_region(smem, 0, a.c.W, a.reg);
     __syncthreads();
@@ -487,28 +519,20 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
   }
   MSW_MARK(c, 2);
   if (!live) return;
-  const TileLanes L = tile_lanes(tr, j, a.n0, a.src, a.dst, a.rowptr);
-  MSW_MARK(c, 3);
-  // everything the tile reads from HBM, issued together
-  const int hs = 16 * a.h1t;
-  f32x4 H[T2], os[NT], od[NT], res[NT], sk[NT];
+  // node rows -> edge lanes
+  float* my = &slab[w][j][0];
+  store_row<T2>(my, Vn, T2, g);
+  store_row<NT>(my + 16 * T2, inn, NT, g);
+  wave_lds_sync();
+  const float* dr = &slab[w][L.dl][0];
+  f32x4 H[T2], od[NT];
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
-    if (t < a.h1t) {
-      const int off = 16 * t + 4 * g;
-      const f32x4 p = (a.Pe && L.anye) ? ld4(a.Pe + (size_t)L.e * hs + off) : ld4(c.W + a.b1_off + off);
-      H[t] = (ld4(a.U + L.sr * hs + off) + ld4(a.V + L.dc * hs + off)) + p;
-    } else {
-      H[t] = zero4();
-    }
+    const int off = 16 * t + 4 * g;
+    const f32x4 p = a.Pe ? Ps[t] : ld4(c.W + a.b1_off + off);
+    H[t] = (t < a.h1t) ? (Us[t] + ld4(dr + off)) + p : zero4();
   }
-  load_row<NT>(os, a.in + L.sr * F, g);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    od[t] = a.own_zero ? zero4() : ld4(a.in + L.dc * F + 16 * t + 4 * g);
-    res[t] = a.own_zero ? zero4() : ld4(a.in + (size_t)L.n * F + 16 * t + 4 * g);
-    sk[t] = a.skip ? ld4(a.skip + (size_t)L.n * F + 16 * t + 4 * g) : zero4();
-  }
+  load_row<NT>(od, dr + 16 * T2, g);
   MSW_MARK(c, 4);
   act_tiles<ACT, T2>(H, a.act1, a.slope1);
   f32x4 sv[NT];
@@ -534,12 +558,14 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
       sv[t] = q;
     }
   }
-  if (L.ev && a.s) store_row<NT>(a.s + (size_t)L.e * F, sv, NT, g);
-  put_message<NT>(&msg[w][j][0], os, od, sv, L.ev, a.grad, a.upwind, g);
+  if (a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);  // padding slots too: never read
+  put_message<NT>(my, os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
   MSW_MARK(c, 6);
-  f32x4 agg[NT];
-  gather_messages<NT>(agg, &msg[w][0][0], L.q0, L.q1, g);
+  f32x4 agg[NT], res[NT];
+  gather_messages<NT, XS>(agg, &slab[w][0][0], L.q0, L.q1, g);
   MSW_MARK(c, 7);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) res[t] = inn[t];
   apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
   MSW_MARK(c, 8);
   if (a.skip) {
@@ -549,7 +575,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
   if (a.last) {
     node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
   } else if (L.nv && a.out) {
-    store_row<NT>(a.out + (size_t)L.n * F, res, NT, g);
+    store_row<NT>(a.out + L.n * F, res, NT, g);
   }
   MSW_MARK(c, 9);
 }
@@ -559,45 +585,81 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
 //   active(e) = rowsum(out[src]) != 0 || rowsum(out[dst]) != 0          (gnn.py:408-411)
 //   agg[c]    = sum_e active(e) * (out[c] - out[src]) * s_e  (edge order; gnn.py:430-438)
 //   out'[c]   = out[c] + W_{k+1} agg[c]  (MFMA)  -> store, or the epilogue after hop K
-template <int NT, int ACT>
+// LAST = false: no epilogue, the filter's A operand goes straight from the blob into
+// registers at kernel start (no LDS staging, no workgroup barrier).
+template <int NT, int ACT, bool LAST>
 __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
-  __shared__ __attribute__((aligned(16))) float msg[kWaves][kRowsPerWave][F];
+  constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
+  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int tile = blockIdx.x * kWaves + w;
   const bool live = tile < a.ntiles;
-  MSW_MARK(a.c, 0);
-  const TileRange tr = a.tiles[live ? tile : 0];
   Common c = a.c;
+  MSW_MARK(c, 0);
+  f32x4 wf[NT][NT];
+  if constexpr (!LAST) {
+    if (a.filt_a >= 0) {
+#pragma unroll
+      for (int to = 0; to < NT; ++to)
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti)
+          wf[to][ti] = ld4(c.W + a.filt_a + ((size_t)(to * NT + ti) * 64 + lane) * 4);
+    }
+  }
+  const int tsafe = live ? tile : 0;  // idle waves of the last workgroup stay in bounds
+  const LaneRec rec = load_rec(a.recs, tsafe, j);
   MSW_MARK(c, 1);
-  if constexpr (kStaged<NT>) {
+  const Lanes L = lanes_of(rec, tsafe, j, a.n0);
+  f32x4 os[NT], sv[NT], inn[NT];
+  load_row<NT>(os, a.in + L.sr * F, g);
+  load_row<NT>(sv, a.s + L.p * F, g);
+  load_row<NT>(inn, a.in + L.n * F, g);
+  if constexpr (LAST && kStaged<NT>) {
     stage_region(smem, 0, a.c.W, a.reg);
     __syncthreads();
     c.W = smem;
   }
   MSW_MARK(c, 2);
   if (!live) return;
-  const TileLanes L = tile_lanes(tr, j, a.n0, a.src, a.dst, a.rowptr);
-  MSW_MARK(c, 3);
-  f32x4 os[NT], od[NT], sv[NT], res[NT];
-  load_row<NT>(os, a.in + L.sr * F, g);
-  load_row<NT>(od, a.in + L.dc * F, g);
-  load_row<NT>(sv, a.s + (size_t)L.e * F, g);
-  load_row<NT>(res, a.in + (size_t)L.n * F, g);
+  float* my = &slab[w][j][0];
+  store_row<NT>(my, inn, NT, g);
+  wave_lds_sync();
+  f32x4 od[NT];
+  load_row<NT>(od, &slab[w][L.dl][0], g);
   MSW_MARK(c, 4);
-  put_message<NT>(&msg[w][j][0], os, od, sv, L.ev, a.grad, a.upwind, g);
+  put_message<NT>(my, os, od, sv, L.ev, a.grad, a.upwind, g);
   MSW_MARK(c, 6);
-  f32x4 agg[NT];
-  gather_messages<NT>(agg, &msg[w][0][0], L.q0, L.q1, g);
+  f32x4 agg[NT], res[NT];
+  gather_messages<NT, XS>(agg, &slab[w][0][0], L.q0, L.q1, g);
   MSW_MARK(c, 7);
-  apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) res[t] = inn[t];
+  if constexpr (LAST) {
+    apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
+  } else if (a.filt_a >= 0) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int to = 0; to < NT; ++to) acc[to] = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int to = 0; to < NT; ++to) acc[to] = MSW_MFMA(wf[to][ti][r], agg[ti][r], acc[to]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + agg[t];
+  }
   MSW_MARK(c, 8);
-  if (a.last) {
+  if constexpr (LAST) {
     node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
-  } else if (L.nv) {
-    store_row<NT>(a.out + (size_t)L.n * F, res, NT, g);
+  } else {
+    if (L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
   }
   MSW_MARK(c, 9);
 }
@@ -610,15 +672,21 @@ template <int NT>
 __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
-  __shared__ __attribute__((aligned(16))) float msg[kWaves][kRowsPerWave][F];
+  constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
+  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int tile = blockIdx.x * kWaves + w;
   const bool live = tile < a.ntiles;
-  MSW_MARK(a.c, 0);
-  const TileRange tr = a.tiles[live ? tile : 0];
   Common c = a.c;
+  MSW_MARK(c, 0);
+  const int tsafe = live ? tile : 0;  // idle waves of the last workgroup stay in bounds
+  const LaneRec rec = load_rec(a.recs, tsafe, j);
   MSW_MARK(c, 1);
+  const Lanes L = lanes_of(rec, tsafe, j, a.n0);
+  f32x4 x[NT], xs[NT];
+  load_row<NT>(x, a.in + L.sr * F, g);
+  load_row<NT>(xs, a.xs + L.n * F, g);
   if constexpr (kStaged<NT>) {
     stage_region(smem, 0, a.c.W, a.reg);
     __syncthreads();
@@ -626,15 +694,9 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
   }
   MSW_MARK(c, 2);
   if (!live) return;
-  const TileLanes L = tile_lanes(tr, j, a.n0, a.child, a.child, a.rowptr);
-  MSW_MARK(c, 3);
-  f32x4 x[NT], xs[NT];
-  load_row<NT>(x, a.in + L.sr * F, g);
-  load_row<NT>(xs, a.xs + (size_t)L.n * F, g);
-  MSW_MARK(c, 4);
-  store_row<NT>(&msg[w][j][0], x, NT, g);
+  store_row<NT>(&slab[w][j][0], x, NT, g);
   f32x4 acc[NT];
-  gather_messages<NT>(acc, &msg[w][0][0], L.q0, L.q1, g);
+  gather_messages<NT, XS>(acc, &slab[w][0][0], L.q0, L.q1, g);
   MSW_MARK(c, 7);
   const float cnt = (float)(L.q1 - L.q0 > 0 ? L.q1 - L.q0 : 1);
 #pragma unroll
@@ -682,10 +744,11 @@ constexpr size_t lds_bytes(int floats) { return kStaged<NT> ? (size_t)floats * s
 // Allow the dynamic weight regions past the 64 KB default (gfx950: 160 KB per CU).
 template <int NT>
 hipError_t prepare_kernels() {
-  const int mx = 160 * 1024 - kWaves * kRowsPerWave * 16 * NT * (int)sizeof(float);
+  const int mx = 160 * 1024 - kWaves * kRowsPerWave * (16 * 2 * NT + 16 * NT + 4) * (int)sizeof(float);
   const void* fns[] = {(const void*)k_encode<NT, 1>, (const void*)k_encode<NT, -1>,
                        (const void*)k_edge_hop<NT, 1>, (const void*)k_edge_hop<NT, -1>,
-                       (const void*)k_hop<NT, 1>, (const void*)k_hop<NT, -1>, (const void*)k_pool<NT>};
+                       (const void*)k_hop<NT, 1, true>, (const void*)k_hop<NT, -1, true>,
+                       (const void*)k_pool<NT>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     if (e != hipSuccess) return e;
@@ -719,11 +782,15 @@ template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const dim3 grid(cdiv(a.ntiles, kWaves)), block(kBlock);
-  const size_t sh = lds_bytes<NT>(a.reg.len);
-  if (a.c.prelu)
-    hipLaunchKernelGGL((k_hop<NT, 1>), grid, block, sh, st, a);
-  else
-    hipLaunchKernelGGL((k_hop<NT, -1>), grid, block, sh, st, a);
+  if (!a.last) {
+    hipLaunchKernelGGL((k_hop<NT, 1, false>), grid, block, 0, st, a);
+  } else {
+    const size_t sh = lds_bytes<NT>(a.reg.len);
+    if (a.c.prelu)
+      hipLaunchKernelGGL((k_hop<NT, 1, true>), grid, block, sh, st, a);
+    else
+      hipLaunchKernelGGL((k_hop<NT, -1, true>), grid, block, sh, st, a);
+  }
   return hipGetLastError();
 }
 template <int NT>

@@ -154,30 +154,47 @@ int build_tiles(const std::vector<int>& rowptr, std::vector<TileRange>& out) {
   return MSW_OK;
 }
 
+// Per-lane tile records (engine.h LaneRec) of a CSR by destination: `src` = source row of
+// CSR edge i (internal numbering), `n0` = first internal row of the destination scale.
+// porig (optional) receives, per tile-padded edge slot, the CSR position or -1.
+std::vector<LaneRec> make_recs(const std::vector<int>& rowptr, const std::vector<int>& src, int n0,
+                               const std::vector<TileRange>& tiles, std::vector<int>* porig) {
+  std::vector<LaneRec> r(tiles.size() * kRowsPerWave, LaneRec{-1, 0, -1, 0});
+  if (porig) porig->assign(tiles.size() * kRowsPerWave, -1);
+  for (size_t t = 0; t < tiles.size(); ++t) {
+    const TileRange& tr = tiles[t];
+    LaneRec* L = &r[t * kRowsPerWave];
+    for (int j = 0; j < tr.nnode; ++j) {
+      const int k = tr.node0 + j;
+      const int q0 = rowptr[k] - tr.edge0, q1 = rowptr[k + 1] - tr.edge0;
+      L[j].n = n0 + k;
+      L[j].q = q0 | (q1 << 8);
+      for (int q = q0; q < q1; ++q) {
+        L[q].src = src[tr.edge0 + q];
+        L[q].dl = j;
+        if (porig) (*porig)[t * kRowsPerWave + q] = tr.edge0 + q;
+      }
+    }
+  }
+  return r;
+}
+
 }  // namespace
 
 // ============================================================================ plan
 struct ScaleCSR {
   int n0 = 0, ns = 0;           // internal rows [n0, n0+ns) (n0 is a multiple of 16)
   int E = 0;                    // edges of this scale
-  int* rowptr = nullptr;        // [ns+1] local
-  int* src = nullptr;           // [E] internal ids, CSR order
-  int* dst = nullptr;           // [E]
-  TileRange* tiles = nullptr;
+  LaneRec* recs = nullptr;      // [ntiles][16]
   int ntiles = 0;
-  std::vector<int> eorig;       // CSR position -> original edge id
+  std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
 };
 
 struct LevelMaps {              // level l: coarse scale l+1, fine scale l
   int I = 0;
-  int* pool_rowptr = nullptr;   // by coarse (local to scale l+1)
-  int* pool_child = nullptr;
-  TileRange* pool_tiles = nullptr;  // coarse nodes with <= 16 children in all
+  LaneRec* pool_recs = nullptr; // coarse nodes (scale l+1) and their children (<= 16 per tile)
   int pool_ntiles = 0;
-  int* un_rowptr = nullptr;     // by fine (local to scale l)
-  int* un_src = nullptr;        // coarse ids
-  int* un_dst = nullptr;        // fine ids
-  TileRange* un_tiles = nullptr;
+  LaneRec* un_recs = nullptr;   // fine nodes (scale l) and their coarse parents
   int un_ntiles = 0;
 };
 
@@ -402,8 +419,7 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   L1.kind = L_EDGE_HOP;
   L1.scale = pr.scale;
   EdgeHopArgs& eh = L1.eh;
-  eh.c = c; eh.n0 = g.n0; eh.tiles = g.tiles; eh.ntiles = g.ntiles; eh.rowptr = g.rowptr;
-  eh.src = g.src; eh.dst = g.dst; eh.xs = P->xs; eh.U = P->U[pr.par]; eh.V = P->V[pr.par]; eh.Pe = pr.Pe;
+  eh.c = c; eh.n0 = g.n0; eh.recs = g.recs; eh.ntiles = g.ntiles; eh.xs = P->xs; eh.U = P->U[pr.par]; eh.V = P->V[pr.par]; eh.Pe = pr.Pe;
   eh.b1_off = pr.b1_off; eh.h1t = pr.h1t; eh.act1 = pr.act1; eh.slope1 = pr.slope1;
   eh.rest = pr.rest; eh.normalize = pr.normalize;
   eh.c.prelu = P->prelu & pr.prelu;
@@ -423,7 +439,7 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
     L.scale = pr.scale;
     HopArgs& h = L.hop;
     h.c = c;
-    h.n0 = g.n0; h.tiles = g.tiles; h.ntiles = g.ntiles; h.rowptr = g.rowptr; h.src = g.src; h.dst = g.dst;
+    h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
     h.s = P->s; h.xs = P->xs;
     h.in = cur; h.out = nxt; h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
     h.grad = pr.with_gradient; h.upwind = pr.upwind;
@@ -473,8 +489,8 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
       L.kind = L_POOL;
       L.scale = i + 1;
       PoolArgs& pa = L.pool;
-      pa.c = c; pa.n0 = P->sc[i + 1].n0; pa.tiles = m.pool_tiles; pa.ntiles = m.pool_ntiles;
-      pa.rowptr = m.pool_rowptr; pa.child = m.pool_child; pa.in = P->xdown; pa.xs = P->xs;
+      pa.c = c; pa.n0 = P->sc[i + 1].n0; pa.recs = m.pool_recs; pa.ntiles = m.pool_ntiles;
+      pa.in = P->xdown; pa.xs = P->xs;
       pa.np = np_of(P, P->procs[i + 1]);
       q.push_back(L);
     }
@@ -498,8 +514,8 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
         L.scale = s - 1;
         EdgeHopArgs& eh = L.eh;
         eh.c = c; eh.c.prelu = P->prelu & up.prelu;
-        eh.n0 = fs.n0; eh.tiles = m.un_tiles; eh.ntiles = m.un_ntiles; eh.rowptr = m.un_rowptr;
-        eh.src = m.un_src; eh.dst = m.un_dst; eh.xs = P->xs; eh.U = P->Uu; eh.V = P->Vu;
+        eh.n0 = fs.n0; eh.recs = m.un_recs; eh.ntiles = m.un_ntiles;
+        eh.xs = P->xs; eh.U = P->Uu; eh.V = P->Vu;
         eh.Pe = nullptr; eh.b1_off = up.b1_off; eh.h1t = up.h1t; eh.act1 = up.act1;
         eh.slope1 = up.slope1; eh.rest = up.rest; eh.normalize = up.normalize; eh.s = nullptr;
         eh.in = P->xup; eh.own_zero = 1; eh.grad = up.with_gradient; eh.upwind = up.upwind;
@@ -569,7 +585,7 @@ struct Relocator {
   }
 };
 
-constexpr int kMaxRegionFloats = (160 * 1024 - kWaves * kRowsPerWave * 32 * 4) / 4;
+constexpr int kMaxRegionFloats = (160 * 1024) / 4 - kWaves * kRowsPerWave * (3 * 32 + 4);  // minus the F=32 slab
 
 int relocate(msw_plan* P, std::vector<Launch>& q) {
   Relocator rl{P->NT, P->p};
@@ -604,9 +620,10 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       reg = &a.reg;
     } else if (L.kind == L_HOP) {
       HopArgs& a = L.hop;
+      if (!a.last) continue;  // middle hops load their filter from the blob (k_hop<.., false>)
       RegionBuilder R(P->blob, 0);
       a.filt_a = R.put(a.filt_a, P->NT * P->NT * 256);
-      if (a.last) rl.epi(R, a.epi);
+      rl.epi(R, a.epi);
       a.reg = R.done();
       reg = &a.reg;
     } else {
@@ -703,7 +720,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     const int64_t a = g->edge_ptr[s], b = g->edge_ptr[s + 1];
     if (b < a) return fail(MSW_ERR_INVALID, "edge_ptr not monotone");
     c.E = (int)(b - a);
-    std::vector<int> key(c.E), srcv(c.E), dstv(c.E);
+    std::vector<int> key(c.E), srcv(c.E);
     for (int64_t e = a; e < b; ++e) {
       const int64_t r = g->edge_index[e], cl = g->edge_index[E + e];
       if (r < 0 || r >= N || cl < 0 || cl >= N) return fail(MSW_ERR_INVALID, "edge_index out of range");
@@ -712,23 +729,20 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
         return fail(MSW_ERR_INVALID, "edge of scale " + std::to_string(s) + " leaves the scale");
       key[e - a] = ci - c.n0;
       srcv[e - a] = ri;
-      dstv[e - a] = ci;
     }
     std::vector<int> rowptr, order;
     csr_build(c.ns, key, rowptr, order);
-    std::vector<int> so(c.E), dso(c.E);
-    c.eorig.resize(c.E);
-    for (int i = 0; i < c.E; ++i) {
-      so[i] = srcv[order[i]];
-      dso[i] = dstv[order[i]];
-      c.eorig[i] = (int)(a + order[i]);
-    }
+    std::vector<int> so(c.E);
+    for (int i = 0; i < c.E; ++i) so[i] = srcv[order[i]];
     std::vector<TileRange> tl;
     if ((rc = build_tiles(rowptr, tl))) return rc;
     c.ntiles = (int)tl.size();
-    if ((rc = pupload(P, &c.rowptr, rowptr)) || (rc = pupload(P, &c.src, so)) ||
-        (rc = pupload(P, &c.dst, dso)) || (rc = pupload(P, &c.tiles, tl)))
-      return rc;
+    std::vector<int> pcsr;
+    const std::vector<LaneRec> recs = make_recs(rowptr, so, c.n0, tl, &pcsr);
+    c.porig.assign(pcsr.size(), -1);
+    for (size_t q = 0; q < pcsr.size(); ++q)
+      if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
+    if ((rc = pupload(P, &c.recs, recs))) return rc;
   }
   // intra-scale levels
   P->lv.assign(S > 1 ? S - 1 : 0, LevelMaps{});
@@ -761,21 +775,14 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       std::vector<TileRange> pt;
       if ((rc = build_tiles(rp, pt))) return rc;
       m.pool_ntiles = (int)pt.size();
-      if ((rc = pupload(P, &m.pool_rowptr, rp)) || (rc = pupload(P, &m.pool_child, child)) ||
-          (rc = pupload(P, &m.pool_tiles, pt)))
-        return rc;
+      if ((rc = pupload(P, &m.pool_recs, make_recs(rp, child, cs.n0, pt, nullptr)))) return rc;
       csr_build(fs.ns, fk, rp, order);
-      std::vector<int> us(m.I), ud(m.I);
-      for (int i = 0; i < m.I; ++i) {
-        us[i] = cv[order[i]];
-        ud[i] = fv[order[i]];
-      }
+      std::vector<int> us(m.I);
+      for (int i = 0; i < m.I; ++i) us[i] = cv[order[i]];
       std::vector<TileRange> tl;
       if ((rc = build_tiles(rp, tl))) return rc;
       m.un_ntiles = (int)tl.size();
-      if ((rc = pupload(P, &m.un_rowptr, rp)) || (rc = pupload(P, &m.un_src, us)) ||
-          (rc = pupload(P, &m.un_dst, ud)) || (rc = pupload(P, &m.un_tiles, tl)))
-        return rc;
+      if ((rc = pupload(P, &m.un_recs, make_recs(rp, us, fs.n0, tl, nullptr)))) return rc;
     }
   }
   return MSW_OK;
@@ -924,8 +931,8 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   if ((rc = pupload(P.get(), &P->bc_slot_d, minus1))) return rc;
   if ((rc = palloc(P.get(), &P->io_d, 1))) return rc;
   HIP_TRY(hipMemset(P->io_d, 0, sizeof(RolloutIO)));
-  int Emax = 1;
-  for (auto& c : P->sc) Emax = std::max(Emax, c.E);
+  int Emax = 1;  // tile-padded edge slots of the largest scale
+  for (auto& c : P->sc) Emax = std::max(Emax, c.ntiles * kRowsPerWave);
   const size_t NF = (size_t)Npad * F;
   const size_t NH = (size_t)Npad * 16 * P->h1t_max;
   float** bufs[] = {&P->xs, &P->xd0, &P->O[0], &P->O[1], &P->T[0], &P->T[1], &P->xdown, &P->xup, &P->xgnn};
@@ -943,7 +950,8 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   HIP_TRY(hipMemset(P->X, 0, (size_t)Npad * P->nnf * sizeof(float)));
   if (P->E > 0)
     for (Proc& pr : P->procs)
-      if ((rc = palloc(P.get(), &pr.Pe, (size_t)std::max(P->sc[pr.scale].E, 1) * 16 * pr.h1t))) return rc;
+      if ((rc = palloc(P.get(), &pr.Pe, (size_t)std::max(P->sc[pr.scale].ntiles * kRowsPerWave, 1) * 16 * pr.h1t)))
+        return rc;
 
   // ---- launch schedules (forward / rollout), per-launch weight regions, weight upload
   sched_step(P.get(), P->sched_fwd, false);
@@ -962,14 +970,16 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
 
   // ---- static per-edge features: edge encoder + edge part of each processor's layer 1
   if (P->E > 0) {
-    const int64_t E = P->E;
-    std::vector<float> ea((size_t)E * ef_raw);
-    std::vector<int64_t> sbase(P->S + 1, 0);  // CSR order, scale by scale (ScaleCSR::eorig)
-    for (int s = 0; s < P->S; ++s) sbase[s + 1] = sbase[s] + P->sc[s].E;
+    // tile-padded edge slots, scale by scale (ScaleCSR::porig); padding slots get zeros
+    std::vector<int64_t> sbase(P->S + 1, 0);
+    for (int s = 0; s < P->S; ++s) sbase[s + 1] = sbase[s] + (int64_t)P->sc[s].ntiles * kRowsPerWave;
+    const int64_t E = sbase[P->S];
+    std::vector<float> ea((size_t)std::max<int64_t>(E, 1) * ef_raw, 0.f);
     for (int s = 0; s < P->S; ++s)
-      for (int i = 0; i < P->sc[s].E; ++i)
-        for (int f = 0; f < ef_raw; ++f)
-          ea[(size_t)(sbase[s] + i) * ef_raw + f] = g->edge_attr[(size_t)P->sc[s].eorig[i] * ef_raw + f];
+      for (size_t q = 0; q < P->sc[s].porig.size(); ++q)
+        if (P->sc[s].porig[q] >= 0)
+          for (int f = 0; f < ef_raw; ++f)
+            ea[(size_t)(sbase[s] + q) * ef_raw + f] = g->edge_attr[(size_t)P->sc[s].porig[q] * ef_raw + f];
     float* ea_d = nullptr;
     float* enc_d = nullptr;
     int64_t tmp_bytes = 0;
@@ -1005,7 +1015,7 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
       RowMlpArgs ra{};
       ra.mode = 1;
       ra.in = feat + (size_t)sbase[pr.scale] * feat_stride; ra.in_stride = feat_stride;
-      ra.in_dim = feat_dim; ra.R = c.E; ra.m = md; ra.W = tw;
+      ra.in_dim = feat_dim; ra.R = c.ntiles * kRowsPerWave; ra.m = md; ra.W = tw;
       ra.out = pr.Pe; ra.out_stride = 16 * pr.h1t; ra.out_tiles = pr.h1t;
       HIP_TRY(rowmlp_dispatch(P->NT, ra));
       HIP_TRY(hipDeviceSynchronize());

@@ -17,6 +17,7 @@ step() {  # step NAME SECONDS CMD...  (exit codes 0/1 continue; anything else st
 MODE=${1:-all}
 if [[ $MODE == all || $MODE == tests ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+  if ! grep -q "smoke ok" $OUT/smoke.log; then echo "stopping: smoke failed" >> $OUT/steps.log; exit 3; fi
   step gputests 900 python -m pytest tests -m gpu -q > $OUT/gpu_tests.log 2>&1
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
