@@ -133,6 +133,8 @@ def main():
     ap.add_argument("--T", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--batch", type=int, default=1,
+                    help="simulations per GPU, run as one disjoint-union batch (SURVEY §8 f1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,21 +149,34 @@ def main():
     torch.cuda.set_device(dev)
 
     T = args.T
-    g_cpu, model_cpu, w, desc = build_workload(args.workload, seed=rank, T=T)
-    g = g_cpu.to(dev)
+    B = max(1, args.batch)
+    # rank r simulates seeds r*B .. r*B+B-1 (independent simulations, weak scaling)
+    sims = [build_workload(args.workload, seed=rank * B + i, T=T) for i in range(B)]
+    g_cpu, model_cpu, w, desc = sims[0]
+    n0 = desc["fine_nodes"]
+    if B == 1:
+        gb = g_cpu
+        fine_rows = None
+    else:  # the reference's batch layout (update_batch_multiscale, train.py:31-65)
+        from mswegnn.batch import collate
+        from training.train import adapt_batch_training
+        gb = adapt_batch_training(collate([s[0] for s in sims]))
+        npt = gb.node_ptr
+        fine_rows = torch.cat([torch.arange(int(npt[i, 0]), int(npt[i, 1])) for i in range(B)]).to(dev)
+        desc = dict(desc, batch=B, batch_nodes=int(gb.x.shape[0]))
+    g = gb.to(dev)
     model = model_cpu.to(dev)
     model.engine = "hip"
-    n0 = desc["fine_nodes"]
 
     from mswegnn.engine import plan_for
     plan = plan_for(model, g)
     out = torch.empty(g.num_nodes, 2, T, device=dev)
-    gather = make_gatherer(dist, world, n0, T, dev)
+    gather = make_gatherer(dist, world, n0 * B, T, dev)
 
     def one_step():
         plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T, out=out)
         if world > 1:
-            gather(out[:n0])
+            gather(out[:n0] if fine_rows is None else out.index_select(0, fine_rows))
 
     for _ in range(args.warmup):
         one_step()
@@ -180,7 +195,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / max(args.steps, 1) * 1e3
-    value = world * n0 * T * args.steps / dt
+    value = world * B * n0 * T * args.steps / dt
 
     result = None
     if rank == 0:
@@ -208,7 +223,7 @@ def main():
         # ---------------- parity vs the reference fixture (zenodo4 only; CPU reference run)
         parity = {}
         r_gpu = plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
-        if args.workload == "zenodo4" and rank == 0 and T == 48:
+        if args.workload == "zenodo4" and rank == 0 and T == 48 and B == 1:
             fx = np.load(os.path.join(ROOT, "tests", "golden", "fx_zenodo4_K4_F32_rollout48.npz"))
             ref = torch.from_numpy(fx["rollout_sel"])
             sel = r_gpu[..., fx["steps"]]
@@ -226,32 +241,41 @@ def main():
             torch.set_num_threads(threads)
             P = {k: v.detach().cpu() for k, v in model_cpu.state_dict().items()}
             cfg = orc.msgnn_config(num_scales=desc["num_scales"], hid_features=F, K=desc["K"])
+            # bounded sample: one step first, then as many rollout steps of simulation 0 as
+            # fit ~cpu_seconds (whole rollouts repeated for small meshes, up to 4)
+            c0 = time.perf_counter()
+            orc.rollout(P, cfg, g_cpu, 1)
+            t1 = time.perf_counter() - c0
+            Tc = int(min(T, max(1, args.cpu_seconds / max(t1, 1e-6))))
             reps, t_cpu, r_cpu = 0, 0.0, None
             while reps < 4 and (reps == 0 or t_cpu < args.cpu_seconds):
                 c0 = time.perf_counter()
-                r = orc.rollout(P, cfg, g_cpu, T)
+                r = orc.rollout(P, cfg, g_cpu, Tc)
                 t_cpu += time.perf_counter() - c0
                 reps += 1
                 r_cpu = r if r_cpu is None else r_cpu
-            cpu = {"value": n0 * T * reps / t_cpu, "unit": "fine-node-steps/s", "cores": threads,
+                if Tc < T:
+                    break
+            cpu = {"value": n0 * Tc * reps / t_cpu, "unit": "fine-node-steps/s", "cores": threads,
                    "kind": "port",
-                   "sample": f"{reps} x {T}-step rollout of the same workload (N0={n0}), "
-                             f"reference algorithm in oracle/msgnn_torch.py (same ATen CPU ops, "
-                             f"bit-identical to the reference), torch {torch.__version__}, "
+                   "sample": f"{reps} x {Tc}-step rollout of one simulation of the workload "
+                             f"(N0={n0}), reference algorithm in oracle/msgnn_torch.py (same ATen "
+                             f"CPU ops, bit-identical to the reference), torch {torch.__version__}, "
                              f"{threads} threads, {t_cpu:.1f} s"}
-            d = (r_gpu - r_cpu).abs()
+            r0 = r_gpu[:g_cpu.num_nodes, :, :Tc]  # simulation 0 = the batch's first graph
+            d = (r0 - r_cpu).abs()
             parity["vs_cpu_reference"] = {
-                "max_abs_err": float(d.max()),
+                "steps": Tc, "max_abs_err": float(d.max()),
                 "max_rel_err": float(max(d[..., t].max() / max(r_cpu[..., t].abs().max(), 1e-30)
-                                         for t in range(T)))}
+                                         for t in range(Tc)))}
         result = {
             "metric": "mesh-nodes x rollout-steps / sec (fine-scale nodes); fp32 max-abs err vs CPU ref",
             "value": value, "unit": "fine-node-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (own multi-scale triangular mesh generator; dry start + hydrograph BC)",
-            "config": dict(desc, parallelism=f"sim-sharded x{world} (1 sim/GPU, RCCL all-gather at end)"
-                           if world > 1 else "single GPU"),
+            "config": dict(desc, parallelism=f"sim-sharded x{world} ({B} sim/GPU, RCCL all-gather at end)"
+                           if world > 1 else ("single GPU" if B == 1 else f"single GPU, batch of {B} sims")),
             "all_node_steps_per_s": value * desc["all_nodes"] / n0,
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "engine": {"kernels_per_step": st["kernels_per_step"], "graph_captured": st["graph_captured"],

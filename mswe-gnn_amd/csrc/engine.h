@@ -82,6 +82,7 @@ struct Common {
 // Encoder.  Scale ranges start at multiples of 64 rows, so a workgroup has one scale.
 struct EncodeArgs {
   Common c;
+  int max_blocks;          // grid cap (resident workgroups), <= 0 = one per 64-row chunk
   WReg reg;                // static encoder (every scale)
   WReg sreg[kMaxScales];   // + per scale: dynamic encoder & projection 0 (s = 0), unpool V
   int lds_floats;          // max over s of reg.len + sreg[s].len
@@ -128,6 +129,7 @@ struct Epilogue {
 struct EdgeHopArgs {
   Common c;
   WReg reg;
+  int max_blocks;                  // grid cap (resident workgroups), <= 0 = one per 4 tiles
   int n0;                          // first internal row of the destination scale
   const LaneRec* recs; int ntiles; // [ntiles][16]
   const float* xs;
@@ -153,6 +155,7 @@ struct EdgeHopArgs {
 struct HopArgs {
   Common c;
   WReg reg;
+  int max_blocks;                  // grid cap (resident workgroups), <= 0 = one per 4 tiles
   int n0;                  // first internal row of the scale
   const LaneRec* recs; int ntiles;
   const float* s;          // [16 ntiles][F]
@@ -169,6 +172,7 @@ struct HopArgs {
 struct PoolArgs {
   Common c;
   WReg reg;
+  int max_blocks;                  // grid cap (resident workgroups), <= 0 = one per 4 tiles
   int n0;                  // first internal row of the coarse scale
   const LaneRec* recs; int ntiles;  // edge lanes = children, node lanes = coarse nodes
   const float* in;         // x_down
@@ -206,6 +210,8 @@ hipError_t launch_init_state(const InitArgs& a, hipStream_t st);
 
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
 template <int NT> hipError_t prepare_kernels();
+// kind 0 encode, 1 edge_hop, 2 hop, 3 pool
+template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes);
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);

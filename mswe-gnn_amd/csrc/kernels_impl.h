@@ -332,52 +332,62 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   MSW_MARK(a.c, 0);
   if (a.io && blockIdx.x == 0 && threadIdx.x == 0) a.io->step += 1;
-  const int rb = blockIdx.x * kRowsPerBlock;
-  int s = 0;
-  while (s + 1 < a.S && rb >= a.n0[s + 1]) ++s;
-  const int n = wave_row0() + j;
-  const bool valid = (n - a.n0[s]) < a.ns[s];
-  const int ext = a.c.perm ? a.c.perm[n] : n;
-  const int xrow = a.x_internal ? (valid ? n : a.n0[s]) : (valid ? ext : 0);
-  const float* xr = a.x + (size_t)xrow * a.c.nnf;
-  const int nstat = a.c.nstat_raw;
-  float raw[4], dyn[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int f = 4 * g + r;
-    raw[r] = f < nstat ? xr[f] : 0.f;
-    dyn[r] = f < a.c.dyn ? xr[nstat + f] : 0.f;
-  }
-  const float wlv = xr[nstat - 1] + xr[a.c.nnf - 2];  // water level = bed elevation + depth
   Common c = a.c;
-  MSW_MARK(c, 1);
-  if constexpr (kStaged<NT>) {
-    stage_region(smem, 0, a.c.W, a.reg);
-    stage_region(smem, a.reg.len, a.c.W, a.sreg[s]);
-    __syncthreads();
-    c.W = smem;
-  }
-  MSW_MARK(c, 2);
-  f32x4 xs[NT];
-  {
-    f32x4 v;
+  const int nchunks = a.Npad / kRowsPerBlock;
+  int staged = -1;  // scale whose region is in LDS
+  // grid-stride over 64-row chunks (scale ranges are 64-aligned: a chunk has one scale);
+  // the per-scale weight region is re-staged only when the scale changes
+  for (int chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int rb = chunk * kRowsPerBlock;
+    int s = 0;
+    while (s + 1 < a.S && rb >= a.n0[s + 1]) ++s;
+    const int n = rb + wave_id() * kRowsPerWave + j;
+    const bool valid = (n - a.n0[s]) < a.ns[s];
+    const int ext = a.c.perm ? a.c.perm[n] : n;
+    const int xrow = a.x_internal ? (valid ? n : a.n0[s]) : (valid ? ext : 0);
+    const float* xr = a.x + (size_t)xrow * a.c.nnf;
+    const int nstat = a.c.nstat_raw;
+    float raw[4], dyn[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = (c.with_wl && 4 * g + r == nstat) ? wlv : raw[r];
-    const f32x4 in[1] = {v};
-    run_mlp<1, NT, NT, ACT>(in, xs, a.stat, c.W, lane, g);
-    if (valid) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
+    for (int r = 0; r < 4; ++r) {
+      const int f = 4 * g + r;
+      raw[r] = f < nstat ? xr[f] : 0.f;
+      dyn[r] = f < a.c.dyn ? xr[nstat + f] : 0.f;
+    }
+    const float wlv = xr[nstat - 1] + xr[a.c.nnf - 2];  // water level = bed elevation + depth
+    MSW_MARK(c, 1);
+    if constexpr (kStaged<NT>) {
+      if (s != staged) {  // uniform across the workgroup: every wave walks the same chunks
+        if (staged >= 0) __syncthreads();  // everyone is done with the old region
+        else stage_region(smem, 0, a.c.W, a.reg);
+        stage_region(smem, a.reg.len, a.c.W, a.sreg[s]);
+        __syncthreads();
+        staged = s;
+        c.W = smem;
+      }
+    }
+    MSW_MARK(c, 2);
+    f32x4 xs[NT];
+    {
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (c.with_wl && 4 * g + r == nstat) ? wlv : raw[r];
+      const f32x4 in[1] = {v};
+      run_mlp<1, NT, NT, ACT>(in, xs, a.stat, c.W, lane, g);
+      if (valid) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
+    }
+    MSW_MARK(c, 5);
+    if (s == 0) {
+      f32x4 xd[NT];
+      const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
+      run_mlp<1, NT, NT, ACT>(in, xd, a.dynm, c.W, lane, g);
+      if (valid && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
+      MSW_MARK(c, 6);
+      np_project<NT>(xs, xd, a.np0, c.W, n, valid, lane, g);
+    }
+    MSW_MARK(c, 8);
+    if (a.vu_a[s] >= 0) side_proj<NT, NT>(xs, a.vu_h1t, c.W + a.vu_a[s], a.Vu, n, valid, lane, g);
   }
-  MSW_MARK(c, 5);
-  if (s == 0) {
-    f32x4 xd[NT];
-    const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
-    run_mlp<1, NT, NT, ACT>(in, xd, a.dynm, c.W, lane, g);
-    if (valid && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
-    MSW_MARK(c, 6);
-    np_project<NT>(xs, xd, a.np0, c.W, n, valid, lane, g);
-  }
-  MSW_MARK(c, 8);
-  if (a.vu_a[s] >= 0) side_proj<NT, NT>(xs, a.vu_h1t, c.W + a.vu_a[s], a.Vu, n, valid, lane, g);
   MSW_MARK(c, 9);
 }
 
@@ -474,63 +484,98 @@ __device__ __forceinline__ void apply_filter(f32x4 (&res)[NT], const f32x4 (&agg
   }
 }
 
+// Tile kernels: LOOP = false -> one tile per wave, the tile's HBM gathers issued before the
+// weight staging (latency-bound meshes); LOOP = true -> grid capped at the resident
+// workgroups, each stages its weight region ONCE and walks tiles grid-stride (large
+// meshes).  In the loop the lane id is made opaque per iteration so that the compiler does
+// not hoist every lane-derived weight address out of the loop (it pinned ~55 VGPRs).
+__device__ __forceinline__ int opaque_lane() {
+  int ln = (int)(threadIdx.x & 63);
+  asm volatile("" : "+v"(ln));
+  return ln;
+}
+
+// Filter A operand straight from the blob into registers (small: NT x NT tiles), issued at
+// kernel start; apply_filter_regs = apply_filter with the operand already in registers.
+template <int NT>
+__device__ __forceinline__ void load_filter(f32x4 (&wf)[NT][NT], const float* W, int filt_a, int lane) {
+  if (filt_a < 0) return;
+#pragma unroll
+  for (int to = 0; to < NT; ++to)
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) wf[to][ti] = ld4(W + filt_a + ((size_t)(to * NT + ti) * 64 + lane) * 4);
+}
+template <int NT>
+__device__ __forceinline__ void apply_filter_regs(f32x4 (&res)[NT], const f32x4 (&agg)[NT], int filt_a,
+                                                  const f32x4 (&wf)[NT][NT]) {
+#pragma clang fp contract(off)
+  if (filt_a >= 0) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int to = 0; to < NT; ++to) acc[to] = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int to = 0; to < NT; ++to) acc[to] = MSW_MFMA(wf[to][ti][r], agg[ti][r], acc[to]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + agg[t];
+  }
+}
+
 // ---------------------------------------------------------------------------- edge MLP + hop 1
 //  edges: s_ij = normalize(MLP(x_s[row], x_s[col], x_d[row], x_d[col], e_ij))
 //         (gnn.py:414-426; first layer pre-split: h1 = act(U[row] + V[col] + Pe[e]));
 //         computed ONCE per layer -- its inputs do not change across the K hops.
 //  nodes: out_1 = out_0 + W_1 agg [+ skip] -> store, or the epilogue when K = 1.
-template <int NT, int ACT>
-__global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
-#pragma clang fp contract(off)
-  // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
-  constexpr int F = 16 * NT, T2 = 2 * NT, XS = 16 * T2 + F + 4;
-  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int tile = blockIdx.x * kWaves + w;
-  const bool live = tile < a.ntiles;
-  Common c = a.c;
-  MSW_MARK(c, 0);
-  const int tsafe = live ? tile : 0;  // idle waves of the last workgroup stay in bounds
-  const LaneRec rec = load_rec(a.recs, tsafe, j);
-  MSW_MARK(c, 1);
-  const Lanes L = lanes_of(rec, tsafe, j, a.n0);
-  // every HBM row the tile needs, issued before the weight staging
+template <int NT>
+struct EdgeHopRows {  // everything one tile reads from HBM
+  Lanes L;
+  f32x4 Us[2 * NT], Ps[2 * NT], Vn[2 * NT], os[NT], inn[NT], sk[NT];
+};
+template <int NT>
+__device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  r.L = lanes_of(load_rec(a.recs, tile, j), tile, j, a.n0);
+  const Lanes& L = r.L;
   const int hs = 16 * a.h1t;
-  f32x4 Us[T2], Ps[T2], Vn[T2], os[NT], inn[NT], sk[NT];
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
     const int off = 16 * t + 4 * g;
     const bool on = t < a.h1t;
-    Us[t] = on ? ld4(a.U + L.sr * hs + off) : zero4();
-    Vn[t] = on ? ld4(a.V + L.n * hs + off) : zero4();
-    Ps[t] = (on && a.Pe) ? ld4(a.Pe + L.p * hs + off) : zero4();
+    r.Us[t] = on ? ld4(a.U + L.sr * hs + off) : zero4();
+    r.Vn[t] = on ? ld4(a.V + L.n * hs + off) : zero4();
+    r.Ps[t] = (on && a.Pe) ? ld4(a.Pe + L.p * hs + off) : zero4();
   }
-  load_row<NT>(os, a.in + L.sr * F, g);
+  load_row<NT>(r.os, a.in + L.sr * F, g);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    inn[t] = a.own_zero ? zero4() : ld4(a.in + L.n * F + 16 * t + 4 * g);
-    sk[t] = a.skip ? ld4(a.skip + L.n * F + 16 * t + 4 * g) : zero4();
+    r.inn[t] = a.own_zero ? zero4() : ld4(a.in + L.n * F + 16 * t + 4 * g);
+    r.sk[t] = a.skip ? ld4(a.skip + L.n * F + 16 * t + 4 * g) : zero4();
   }
-  if constexpr (kStaged<NT>) {
-    stage_region(smem, 0, a.c.W, a.reg);
-    __syncthreads();
-    c.W = smem;
-  }
-  MSW_MARK(c, 2);
-  if (!live) return;
+}
+template <int NT, int ACT, int XS>
+__device__ __forceinline__ void edge_hop_tile(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
+                                              const f32x4 (&wf)[NT][NT], float* slab, int j, int lane, int g) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  const Lanes& L = r.L;
   // node rows -> edge lanes
-  float* my = &slab[w][j][0];
-  store_row<T2>(my, Vn, T2, g);
-  store_row<NT>(my + 16 * T2, inn, NT, g);
+  float* my = slab + j * XS;
+  store_row<T2>(my, r.Vn, T2, g);
+  store_row<NT>(my + 16 * T2, r.inn, NT, g);
   wave_lds_sync();
-  const float* dr = &slab[w][L.dl][0];
+  const float* dr = slab + L.dl * XS;
   f32x4 H[T2], od[NT];
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
     const int off = 16 * t + 4 * g;
-    const f32x4 p = a.Pe ? Ps[t] : ld4(c.W + a.b1_off + off);
-    H[t] = (t < a.h1t) ? (Us[t] + ld4(dr + off)) + p : zero4();
+    const f32x4 p = a.Pe ? r.Ps[t] : ld4(c.W + a.b1_off + off);
+    H[t] = (t < a.h1t) ? (r.Us[t] + ld4(dr + off)) + p : zero4();
   }
   load_row<NT>(od, dr + 16 * T2, g);
   MSW_MARK(c, 4);
@@ -559,23 +604,61 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
     }
   }
   if (a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);  // padding slots too: never read
-  put_message<NT>(my, os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
+  put_message<NT>(my, r.os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
   MSW_MARK(c, 6);
   f32x4 agg[NT], res[NT];
-  gather_messages<NT, XS>(agg, &slab[w][0][0], L.q0, L.q1, g);
+  gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
   MSW_MARK(c, 7);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) res[t] = inn[t];
-  apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
+  for (int t = 0; t < NT; ++t) res[t] = r.inn[t];
+  apply_filter_regs<NT>(res, agg, a.filt_a, wf);
   MSW_MARK(c, 8);
   if (a.skip) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = res[t] + sk[t];
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + r.sk[t];
   }
   if (a.last) {
     node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
   } else if (L.nv && a.out) {
     store_row<NT>(a.out + L.n * F, res, NT, g);
+  }
+}
+template <int NT, int ACT, bool LOOP>
+__global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
+  // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
+  constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
+  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int stride = gridDim.x * kWaves;
+  int tile = blockIdx.x * kWaves + w;
+  Common c = a.c;
+  MSW_MARK(c, 0);
+  f32x4 wf[NT][NT];
+  load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
+  if constexpr (!LOOP) {
+    EdgeHopRows<NT> r;
+    edge_hop_load<NT>(r, a, tile < a.ntiles ? tile : 0, j, g);  // idle waves stay in bounds
+    MSW_MARK(c, 1);
+    if constexpr (kStaged<NT>) {
+      stage_region(smem, 0, a.c.W, a.reg);
+      __syncthreads();
+      c.W = smem;
+    }
+    MSW_MARK(c, 2);
+    if (tile < a.ntiles) edge_hop_tile<NT, ACT, XS>(r, a, c, wf, &slab[w][0][0], j, lane, g);
+  } else {
+    if constexpr (kStaged<NT>) {
+      stage_region(smem, 0, a.c.W, a.reg);
+      __syncthreads();
+      c.W = smem;
+    }
+    for (; tile < a.ntiles; tile += stride) {
+      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+      EdgeHopRows<NT> q;
+      edge_hop_load<NT>(q, a, tile, jj, gg);
+      edge_hop_tile<NT, ACT, XS>(q, a, c, wf, &slab[w][0][0], jj, ln, gg);
+    }
   }
   MSW_MARK(c, 9);
 }
@@ -587,79 +670,83 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
 //   out'[c]   = out[c] + W_{k+1} agg[c]  (MFMA)  -> store, or the epilogue after hop K
 // LAST = false: no epilogue, the filter's A operand goes straight from the blob into
 // registers at kernel start (no LDS staging, no workgroup barrier).
-template <int NT, int ACT, bool LAST>
+template <int NT>
+struct HopRows {
+  Lanes L;
+  f32x4 os[NT], sv[NT], inn[NT];
+};
+template <int NT>
+__device__ __forceinline__ void hop_load(HopRows<NT>& r, const HopArgs& a, int tile, int j, int g) {
+  constexpr int F = 16 * NT;
+  r.L = lanes_of(load_rec(a.recs, tile, j), tile, j, a.n0);
+  load_row<NT>(r.os, a.in + r.L.sr * F, g);
+  load_row<NT>(r.sv, a.s + r.L.p * F, g);
+  load_row<NT>(r.inn, a.in + r.L.n * F, g);
+}
+template <int NT, int ACT, bool LAST, bool LOOP>
 __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
-  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int tile = blockIdx.x * kWaves + w;
-  const bool live = tile < a.ntiles;
+  const int stride = gridDim.x * kWaves;
+  int tile = blockIdx.x * kWaves + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   f32x4 wf[NT][NT];
-  if constexpr (!LAST) {
-    if (a.filt_a >= 0) {
+  if constexpr (!LAST) load_filter<NT>(wf, c.W, a.filt_a, lane);
+  float* slab = &slab_all[w][0][0];
+  auto run = [&](const HopRows<NT>& r, int j, int lane, int g) {
+    float* my = slab + j * XS;
+    const Lanes& L = r.L;
+    store_row<NT>(my, r.inn, NT, g);
+    wave_lds_sync();
+    f32x4 od[NT];
+    load_row<NT>(od, slab + L.dl * XS, g);
+    MSW_MARK(c, 4);
+    put_message<NT>(my, r.os, od, r.sv, L.ev, a.grad, a.upwind, g);
+    MSW_MARK(c, 6);
+    f32x4 agg[NT], res[NT];
+    gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
+    MSW_MARK(c, 7);
 #pragma unroll
-      for (int to = 0; to < NT; ++to)
-#pragma unroll
-        for (int ti = 0; ti < NT; ++ti)
-          wf[to][ti] = ld4(c.W + a.filt_a + ((size_t)(to * NT + ti) * 64 + lane) * 4);
+    for (int t = 0; t < NT; ++t) res[t] = r.inn[t];
+    if constexpr (LAST)
+      apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
+    else
+      apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+    MSW_MARK(c, 8);
+    if constexpr (LAST) {
+      node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
+    } else {
+      if (L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
     }
-  }
-  const int tsafe = live ? tile : 0;  // idle waves of the last workgroup stay in bounds
-  const LaneRec rec = load_rec(a.recs, tsafe, j);
-  MSW_MARK(c, 1);
-  const Lanes L = lanes_of(rec, tsafe, j, a.n0);
-  f32x4 os[NT], sv[NT], inn[NT];
-  load_row<NT>(os, a.in + L.sr * F, g);
-  load_row<NT>(sv, a.s + L.p * F, g);
-  load_row<NT>(inn, a.in + L.n * F, g);
-  if constexpr (LAST && kStaged<NT>) {
-    stage_region(smem, 0, a.c.W, a.reg);
-    __syncthreads();
-    c.W = smem;
-  }
-  MSW_MARK(c, 2);
-  if (!live) return;
-  float* my = &slab[w][j][0];
-  store_row<NT>(my, inn, NT, g);
-  wave_lds_sync();
-  f32x4 od[NT];
-  load_row<NT>(od, &slab[w][L.dl][0], g);
-  MSW_MARK(c, 4);
-  put_message<NT>(my, os, od, sv, L.ev, a.grad, a.upwind, g);
-  MSW_MARK(c, 6);
-  f32x4 agg[NT], res[NT];
-  gather_messages<NT, XS>(agg, &slab[w][0][0], L.q0, L.q1, g);
-  MSW_MARK(c, 7);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) res[t] = inn[t];
-  if constexpr (LAST) {
-    apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
-  } else if (a.filt_a >= 0) {
-    f32x4 acc[NT];
-#pragma unroll
-    for (int to = 0; to < NT; ++to) acc[to] = zero4();
-#pragma unroll
-    for (int ti = 0; ti < NT; ++ti)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int to = 0; to < NT; ++to) acc[to] = MSW_MFMA(wf[to][ti][r], agg[ti][r], acc[to]);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = res[t] + acc[t];
+  };
+  if constexpr (!LOOP) {
+    HopRows<NT> r;
+    hop_load<NT>(r, a, tile < a.ntiles ? tile : 0, j, g);
+    MSW_MARK(c, 1);
+    if constexpr (LAST && kStaged<NT>) {
+      stage_region(smem, 0, a.c.W, a.reg);
+      __syncthreads();
+      c.W = smem;
+    }
+    MSW_MARK(c, 2);
+    if (tile < a.ntiles) run(r, j, lane, g);
   } else {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = res[t] + agg[t];
-  }
-  MSW_MARK(c, 8);
-  if constexpr (LAST) {
-    node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
-  } else {
-    if (L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
+    if constexpr (LAST && kStaged<NT>) {
+      stage_region(smem, 0, a.c.W, a.reg);
+      __syncthreads();
+      c.W = smem;
+    }
+    for (; tile < a.ntiles; tile += stride) {
+      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+      HopRows<NT> q;
+      hop_load<NT>(q, a, tile, jj, gg);
+      run(q, jj, ln, gg);
+    }
   }
   MSW_MARK(c, 9);
 }
@@ -668,40 +755,63 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
 // scatter(x[fine], coarse, reduce='mean') (gnn.py:256): children summed in edge order,
 // divided by max(count, 1); then the projection of the next processor.  Tiles of coarse
 // nodes with <= 16 children in all: lane j loads child j, the coarse lanes sum.
-template <int NT>
+template <int NT, bool LOOP>
 __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
-  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int tile = blockIdx.x * kWaves + w;
-  const bool live = tile < a.ntiles;
+  const int stride = gridDim.x * kWaves;
+  int tile = blockIdx.x * kWaves + w;
   Common c = a.c;
   MSW_MARK(c, 0);
-  const int tsafe = live ? tile : 0;  // idle waves of the last workgroup stay in bounds
-  const LaneRec rec = load_rec(a.recs, tsafe, j);
-  MSW_MARK(c, 1);
-  const Lanes L = lanes_of(rec, tsafe, j, a.n0);
-  f32x4 x[NT], xs[NT];
-  load_row<NT>(x, a.in + L.sr * F, g);
-  load_row<NT>(xs, a.xs + L.n * F, g);
-  if constexpr (kStaged<NT>) {
-    stage_region(smem, 0, a.c.W, a.reg);
-    __syncthreads();
-    c.W = smem;
-  }
-  MSW_MARK(c, 2);
-  if (!live) return;
-  store_row<NT>(&slab[w][j][0], x, NT, g);
-  f32x4 acc[NT];
-  gather_messages<NT, XS>(acc, &slab[w][0][0], L.q0, L.q1, g);
-  MSW_MARK(c, 7);
-  const float cnt = (float)(L.q1 - L.q0 > 0 ? L.q1 - L.q0 : 1);
+  struct Rows {
+    Lanes L;
+    f32x4 x[NT], xs[NT];
+  };
+  auto load = [&](Rows& r, int t, int j, int g) {
+    r.L = lanes_of(load_rec(a.recs, t, j), t, j, a.n0);
+    load_row<NT>(r.x, a.in + r.L.sr * F, g);
+    load_row<NT>(r.xs, a.xs + r.L.n * F, g);
+  };
+  float* slab = &slab_all[w][0][0];
+  auto run = [&](const Rows& r, int j, int lane, int g) {
+    const Lanes& L = r.L;
+    store_row<NT>(slab + j * XS, r.x, NT, g);
+    f32x4 acc[NT];
+    gather_messages<NT, XS>(acc, slab, L.q0, L.q1, g);
+    MSW_MARK(c, 7);
+    const float cnt = (float)(L.q1 - L.q0 > 0 ? L.q1 - L.q0 : 1);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = acc[t] / cnt;
-  np_project<NT>(xs, acc, a.np, c.W, L.n, L.nv, lane, g);
+    for (int t = 0; t < NT; ++t) acc[t] = acc[t] / cnt;
+    np_project<NT>(r.xs, acc, a.np, c.W, L.n, L.nv, lane, g);
+  };
+  if constexpr (!LOOP) {
+    Rows r0;
+    load(r0, tile < a.ntiles ? tile : 0, j, g);
+    MSW_MARK(c, 1);
+    if constexpr (kStaged<NT>) {
+      stage_region(smem, 0, a.c.W, a.reg);
+      __syncthreads();
+      c.W = smem;
+    }
+    MSW_MARK(c, 2);
+    if (tile < a.ntiles) run(r0, j, lane, g);
+  } else {
+    if constexpr (kStaged<NT>) {
+      stage_region(smem, 0, a.c.W, a.reg);
+      __syncthreads();
+      c.W = smem;
+    }
+    for (; tile < a.ntiles; tile += stride) {
+      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+      Rows q;
+      load(q, tile, jj, gg);
+      run(q, jj, ln, gg);
+    }
+  }
   MSW_MARK(c, 9);
 }
 
@@ -745,10 +855,13 @@ constexpr size_t lds_bytes(int floats) { return kStaged<NT> ? (size_t)floats * s
 template <int NT>
 hipError_t prepare_kernels() {
   const int mx = 160 * 1024 - kWaves * kRowsPerWave * (16 * 2 * NT + 16 * NT + 4) * (int)sizeof(float);
-  const void* fns[] = {(const void*)k_encode<NT, 1>, (const void*)k_encode<NT, -1>,
-                       (const void*)k_edge_hop<NT, 1>, (const void*)k_edge_hop<NT, -1>,
-                       (const void*)k_hop<NT, 1, true>, (const void*)k_hop<NT, -1, true>,
-                       (const void*)k_pool<NT>};
+  const void* fns[] = {
+      (const void*)k_encode<NT, 1>, (const void*)k_encode<NT, -1>,
+      (const void*)k_edge_hop<NT, 1, false>, (const void*)k_edge_hop<NT, -1, false>,
+      (const void*)k_edge_hop<NT, 1, true>, (const void*)k_edge_hop<NT, -1, true>,
+      (const void*)k_hop<NT, 1, true, false>, (const void*)k_hop<NT, -1, true, false>,
+      (const void*)k_hop<NT, 1, true, true>, (const void*)k_hop<NT, -1, true, true>,
+      (const void*)k_pool<NT, false>, (const void*)k_pool<NT, true>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     if (e != hipSuccess) return e;
@@ -759,7 +872,8 @@ hipError_t prepare_kernels() {
 template <int NT>
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   if (a.Npad <= 0) return hipSuccess;
-  const dim3 grid(cdiv(a.Npad, kRowsPerBlock)), block(kBlock);
+  const int n = a.Npad / kRowsPerBlock;
+  const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.lds_floats);
   if (a.c.prelu)
     hipLaunchKernelGGL((k_encode<NT, 1>), grid, block, sh, st, a);
@@ -767,36 +881,59 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_encode<NT, -1>), grid, block, sh, st, a);
   return hipGetLastError();
 }
+
+// one tile per wave while the grid fits the chip; grid-stride loop beyond that
+static inline bool tile_loop(int ntiles, int max_blocks) {
+  return max_blocks > 0 && cdiv(ntiles, kWaves) > max_blocks;
+}
+static inline int tile_grid(int ntiles, int max_blocks) {
+  return tile_loop(ntiles, max_blocks) ? max_blocks : cdiv(ntiles, kWaves);
+}
+
 template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(cdiv(a.ntiles, kWaves)), block(kBlock);
+  const dim3 grid(tile_grid(a.ntiles, a.max_blocks)), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.reg.len);
-  if (a.c.prelu)
-    hipLaunchKernelGGL((k_edge_hop<NT, 1>), grid, block, sh, st, a);
-  else
-    hipLaunchKernelGGL((k_edge_hop<NT, -1>), grid, block, sh, st, a);
+  const bool loop = tile_loop(a.ntiles, a.max_blocks);
+  if (a.c.prelu) {
+    if (loop) hipLaunchKernelGGL((k_edge_hop<NT, 1, true>), grid, block, sh, st, a);
+    else hipLaunchKernelGGL((k_edge_hop<NT, 1, false>), grid, block, sh, st, a);
+  } else {
+    if (loop) hipLaunchKernelGGL((k_edge_hop<NT, -1, true>), grid, block, sh, st, a);
+    else hipLaunchKernelGGL((k_edge_hop<NT, -1, false>), grid, block, sh, st, a);
+  }
   return hipGetLastError();
 }
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(cdiv(a.ntiles, kWaves)), block(kBlock);
+  const dim3 grid(tile_grid(a.ntiles, a.max_blocks)), block(kBlock);
+  const bool loop = tile_loop(a.ntiles, a.max_blocks);
   if (!a.last) {
-    hipLaunchKernelGGL((k_hop<NT, 1, false>), grid, block, 0, st, a);
+    if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_hop<NT, 1, false, false>), grid, block, 0, st, a);
   } else {
     const size_t sh = lds_bytes<NT>(a.reg.len);
-    if (a.c.prelu)
-      hipLaunchKernelGGL((k_hop<NT, 1, true>), grid, block, sh, st, a);
-    else
-      hipLaunchKernelGGL((k_hop<NT, -1, true>), grid, block, sh, st, a);
+    if (a.c.prelu) {
+      if (loop) hipLaunchKernelGGL((k_hop<NT, 1, true, true>), grid, block, sh, st, a);
+      else hipLaunchKernelGGL((k_hop<NT, 1, true, false>), grid, block, sh, st, a);
+    } else {
+      if (loop) hipLaunchKernelGGL((k_hop<NT, -1, true, true>), grid, block, sh, st, a);
+      else hipLaunchKernelGGL((k_hop<NT, -1, true, false>), grid, block, sh, st, a);
+    }
   }
   return hipGetLastError();
 }
 template <int NT>
 hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_pool<NT>), dim3(cdiv(a.ntiles, kWaves)), dim3(kBlock), lds_bytes<NT>(a.reg.len), st, a);
+  const dim3 grid(tile_grid(a.ntiles, a.max_blocks)), block(kBlock);
+  const size_t sh = lds_bytes<NT>(a.reg.len);
+  if (tile_loop(a.ntiles, a.max_blocks))
+    hipLaunchKernelGGL((k_pool<NT, true>), grid, block, sh, st, a);
+  else
+    hipLaunchKernelGGL((k_pool<NT, false>), grid, block, sh, st, a);
   return hipGetLastError();
 }
 template <int NT>
@@ -809,8 +946,30 @@ hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Workgroups of one launch resident on the whole chip (grid cap of the grid-stride kernels).
+template <int NT>
+int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes) {
+  const void* f = nullptr;
+  switch (kind) {
+    case 0: f = prelu ? (const void*)k_encode<NT, 1> : (const void*)k_encode<NT, -1>; break;
+    case 1: f = prelu ? (const void*)k_edge_hop<NT, 1, true> : (const void*)k_edge_hop<NT, -1, true>; break;
+    case 2:
+      f = !last ? (const void*)k_hop<NT, 1, false, true>
+                : (prelu ? (const void*)k_hop<NT, 1, true, true> : (const void*)k_hop<NT, -1, true, true>);
+      break;
+    default: f = (const void*)k_pool<NT, true>; break;
+  }
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, kStaged<NT> ? dyn_bytes : 0) != hipSuccess)
+    return 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return per_cu > 0 ? per_cu * cus : 0;
+}
+
 #define MSW_INSTANTIATE(NT)                                                       \
   template hipError_t prepare_kernels<NT>();                                      \
+  template int resident_blocks<NT>(int, int, int, size_t);                        \
   template hipError_t launch_encode<NT>(const EncodeArgs&, hipStream_t);          \
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \

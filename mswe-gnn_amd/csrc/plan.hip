@@ -613,8 +613,7 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       EdgeHopArgs& a = L.eh;
       RegionBuilder R(P->blob, 0);
       a.b1_off = R.put(a.b1_off, 16 * a.h1t);
-      rl.mlp(R, a.rest);
-      a.filt_a = R.put(a.filt_a, P->NT * P->NT * 256);
+      rl.mlp(R, a.rest);  // filt_a stays a blob offset: k_edge_hop loads it into registers
       if (a.last) rl.epi(R, a.epi);
       a.reg = R.done();
       reg = &a.reg;
@@ -638,6 +637,33 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       return fail(MSW_ERR_UNSUPPORTED, "weights of one launch exceed the LDS budget (" + std::to_string(tot * 4) + " B)");
   }
   return MSW_OK;
+}
+
+// Grid cap of a grid-stride launch: the workgroups the chip holds at once, so that each
+// stages its weight region once (large meshes) and none waits for a second wave of blocks.
+int resident_of(int NT, int kind, int prelu, int last, size_t bytes) {
+  switch (NT) {
+    case 1: return resident_blocks<1>(kind, prelu, last, bytes);
+    case 2: return resident_blocks<2>(kind, prelu, last, bytes);
+    default: return resident_blocks<4>(kind, prelu, last, bytes);
+  }
+}
+void set_grid_cap(msw_plan* P, Launch& L) {
+  const int NT = P->NT;
+  switch (L.kind) {
+    case L_ENCODE:
+      L.enc.max_blocks = resident_of(NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4);
+      break;
+    case L_EDGE_HOP:
+      L.eh.max_blocks = resident_of(NT, 1, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4);
+      break;
+    case L_HOP:
+      L.hop.max_blocks = resident_of(NT, 2, L.hop.c.prelu, L.hop.last, (size_t)L.hop.reg.len * 4);
+      break;
+    default:
+      L.pool.max_blocks = resident_of(NT, 3, 0, 0, (size_t)L.pool.reg.len * 4);
+      break;
+  }
 }
 
 template <int NT>
@@ -967,6 +993,8 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     case 2: HIP_TRY(prepare_kernels<2>()); break;
     default: HIP_TRY(prepare_kernels<4>()); break;
   }
+  for (auto* q : {&P->sched_fwd, &P->sched_roll})
+    for (Launch& L : *q) set_grid_cap(P.get(), L);
 
   // ---- static per-edge features: edge encoder + edge part of each processor's layer 1
   if (P->E > 0) {
