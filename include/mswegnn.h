@@ -177,10 +177,25 @@ int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
  * call after a forward or rollout: it reuses the plan's workspaces and overwrites scratch).
  *   kernel: 0 = middle hop (first processor on `scale`), 1 = fused edge MLP + hop 1
  *           (same processor), 2 = mean pooling + projection into `scale` (scale >= 1),
- *           3 = node encoders (+ projection of processor 0).
+ *           3 = node encoders (+ projection of processor 0), 4 = unpooling layer into
+ *           `scale` (scale < S-1) with its projection epilogue.
  * units_out (optional) receives {rows, edges} processed by ONE launch. */
 int msw_bench_kernel(msw_plan* plan, int32_t kernel, int32_t scale, int32_t iters,
                      int64_t* units_out, void* stream);
+
+/* On-device rollout evaluation (the reference's test-time metrics, finest scale only;
+ * utils/miscellaneous.py:123-199, training/loss.py:8-35).  pred, real: device [N][2][T]
+ * (graph numbering, as msw_rollout writes them); fine_ranges: host int64 [num_sims][2],
+ * the finest-scale row range of each simulation (node_ptr[g][0], node_ptr[g][1]);
+ * thresholds: host float [n_thr] (n_thr <= 4) water-depth thresholds.
+ * Outputs (device, ZEROED by the caller, accumulated with atomics):
+ *   sums   double [num_sims][T][9]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, the same four
+ *          over rows with dh != 0 or dv != 0 (mask_on_water), that row count;
+ *   counts uint64 [num_sims][T][n_thr][4]: TP, TN, FP, FN of h_pred > thr vs h_real > thr.
+ * Stream-ordered, no host synchronisation; needs no plan. */
+int msw_rollout_metrics(const float* pred, const float* real, int32_t T, const int64_t* fine_ranges,
+                        int32_t num_sims, const float* thresholds, int32_t n_thr, double* sums,
+                        uint64_t* counts, void* stream);
 
 /* Diagnostics: route per-phase timestamps of wave 0 of workgroup 0 of every launch to the
  * device buffer `buf` (uint64[20]: {shader clock, 100 MHz clock} for phase marks 0..9).

@@ -204,6 +204,9 @@ struct RowMlpArgs {
   float* out; int out_stride, out_tiles;
 };
 
+// Records `msg` as msw_last_error() (thread-local) and returns `code` (plan.hip).
+int set_error(int code, const char* msg);
+
 hipError_t launch_set_slots(const SlotArgs& a, hipStream_t st);
 hipError_t launch_set_io(RolloutIO* dst, const RolloutIO& v, hipStream_t st);
 hipError_t launch_init_state(const InitArgs& a, hipStream_t st);

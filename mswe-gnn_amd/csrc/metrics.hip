@@ -1,0 +1,120 @@
+// On-device rollout evaluation: the reference's test-time metrics over the
+// finest scale of each simulation, computed where the rollout already lives instead of
+// shipping [N, 2, T] to the host.
+//   get_rollout_loss (RMSE / MAE, all nodes or only_where_water)  utils/miscellaneous.py:177-199,
+//                                                                  training/loss.py:8-35
+//   confusion matrix -> CSI / F1 at water-depth thresholds        utils/miscellaneous.py:123-169
+// The kernel produces per-(simulation, step) partial sums in fp64 and exact integer counts;
+// the host side (mswegnn/metrics.py) forms the reference's ratios.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mswegnn.h"
+#include "engine.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTChunk = 32;    // time steps per workgroup (blockIdx.y)
+constexpr int kMaxThr = 4;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// One thread = one fine-scale row of simulation g, all steps of the block's time chunk.
+// sums[g][t][9]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, and the same four over the rows
+// where dh != 0 or dv != 0 (mask_on_water), then that row count.
+// counts[g][t][k][4]: TP, TN, FP, FN of (pred_h > thr_k) vs (real_h > thr_k).
+struct MetricArgs {
+  const float* pred;
+  const float* real;
+  int T;
+  int row0, nrows;  // fine-scale rows [row0, row0 + nrows) of this simulation
+  int nthr;
+  float thr[kMaxThr];
+  double* sums;                 // this simulation's [T][9]
+  unsigned long long* counts;   // this simulation's [T][nthr][4]
+};
+
+__global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  const bool valid = i < a.nrows;
+  const size_t n = (size_t)a.row0 + (valid ? i : 0);
+  const int lane = threadIdx.x & 63;
+  const int t0 = blockIdx.y * kTChunk;
+  for (int t = t0; t < t0 + kTChunk && t < a.T; ++t) {
+    float dh = 0.f, dv = 0.f, ph = 0.f, rh = 0.f;
+    if (valid) {
+      ph = a.pred[(n * 2 + 0) * a.T + t];
+      rh = a.real[(n * 2 + 0) * a.T + t];
+      dh = ph - rh;
+      dv = a.pred[(n * 2 + 1) * a.T + t] - a.real[(n * 2 + 1) * a.T + t];
+    }
+    const bool wet = valid && (dh != 0.f || dv != 0.f);
+    double v[9];
+    v[0] = fabs((double)dh);
+    v[1] = fabs((double)dv);
+    v[2] = (double)dh * dh;
+    v[3] = (double)dv * dv;
+    v[4] = wet ? v[0] : 0.0;
+    v[5] = wet ? v[1] : 0.0;
+    v[6] = wet ? v[2] : 0.0;
+    v[7] = wet ? v[3] : 0.0;
+    v[8] = wet ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) atomicAdd(a.sums + (size_t)t * 9 + k, v[k]);
+    }
+    for (int k = 0; k < a.nthr; ++k) {
+      const bool p = ph > a.thr[k], r = rh > a.thr[k];
+      const unsigned long long tp = __popcll(__ballot(valid && p && r));
+      const unsigned long long tn = __popcll(__ballot(valid && !p && !r));
+      const unsigned long long fp = __popcll(__ballot(valid && p && !r));
+      const unsigned long long fn = __popcll(__ballot(valid && !p && r));
+      if (lane == 0) {
+        unsigned long long* c = a.counts + ((size_t)t * a.nthr + k) * 4;
+        atomicAdd(c + 0, tp);
+        atomicAdd(c + 1, tn);
+        atomicAdd(c + 2, fp);
+        atomicAdd(c + 3, fn);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int msw_rollout_metrics(const float* pred, const float* real, int32_t T,
+                                   const int64_t* fine_ranges, int32_t num_sims,
+                                   const float* thresholds, int32_t n_thr, double* sums,
+                                   uint64_t* counts, void* stream) {
+  if (!pred || !real || !fine_ranges || !sums || (n_thr > 0 && (!thresholds || !counts)))
+    return msw::set_error(MSW_ERR_INVALID, "null argument");
+  if (T < 0 || num_sims < 0 || n_thr < 0 || n_thr > kMaxThr)
+    return msw::set_error(MSW_ERR_INVALID, "T, num_sims or n_thr out of range (n_thr <= 4)");
+  if (T == 0) return MSW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  for (int g = 0; g < num_sims; ++g) {
+    MetricArgs a{};
+    a.pred = pred;
+    a.real = real;
+    a.T = T;
+    a.row0 = (int)fine_ranges[2 * g];
+    a.nrows = (int)(fine_ranges[2 * g + 1] - fine_ranges[2 * g]);
+    if (a.nrows < 0) return msw::set_error(MSW_ERR_INVALID, "fine range end < start");
+    a.nthr = n_thr;
+    for (int k = 0; k < n_thr; ++k) a.thr[k] = thresholds[k];
+    a.sums = sums + (size_t)g * T * 9;
+    a.counts = reinterpret_cast<unsigned long long*>(counts) + (size_t)g * T * (n_thr > 0 ? n_thr : 1) * 4;
+    if (a.nrows == 0) continue;
+    const dim3 grid((a.nrows + kThreads - 1) / kThreads, (T + kTChunk - 1) / kTChunk);
+    hipLaunchKernelGGL(k_metrics, grid, dim3(kThreads), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
+  }
+  return MSW_OK;
+}

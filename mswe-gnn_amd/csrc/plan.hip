@@ -820,11 +820,13 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
 int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
   if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
   if (P->sched_roll.empty()) return fail(MSW_ERR_INVALID, "run a rollout before bench_kernel");
-  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE};
-  if (kernel < 0 || kernel > 3) return fail(MSW_ERR_INVALID, "unknown kernel id");
+  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP};
+  if (kernel < 0 || kernel > 4) return fail(MSW_ERR_INVALID, "unknown kernel id");
+  const bool unpool = kernel == 4;  // the intra-scale (unpooling) layer into `scale`
   const Launch* src = nullptr;
   for (const Launch& L : P->sched_roll)
-    if (L.kind == kind_of[kernel] && (L.kind == L_ENCODE || L.scale == scale)) {
+    if (L.kind == kind_of[kernel] && (L.kind == L_ENCODE || L.scale == scale) &&
+        (L.kind != L_EDGE_HOP || (L.eh.own_zero != 0) == unpool)) {
       if (!src) src = &L;
       if (L.kind == L_HOP && !L.hop.last) { src = &L; break; }  // prefer a middle hop
       if (L.kind != L_HOP) break;
@@ -834,7 +836,8 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
   const ScaleCSR& g = P->sc[scale];
   int64_t rows = g.ns, edges = g.E;
   if (L.kind == L_HOP && L.hop.last) { L.hop.last = 0; L.hop.out = P->T[1]; }
-  if (L.kind == L_EDGE_HOP && L.eh.last) { L.eh.last = 0; L.eh.out = P->T[1]; }
+  if (L.kind == L_EDGE_HOP && L.eh.last && !unpool) { L.eh.last = 0; L.eh.out = P->T[1]; }
+  if (unpool) edges = P->lv[scale].I;  // the unpool epilogue only writes the next layer's U/V/O
   if (L.kind == L_POOL) edges = P->lv[scale - 1].I;
   if (L.kind == L_ENCODE) { L.enc.io = nullptr; rows = P->N; edges = 0; }
   std::vector<Launch> q(1, L);
@@ -848,6 +851,8 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
 }
 
 }  // namespace
+
+int msw::set_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
 
 // ============================================================================ C ABI
 extern "C" {

@@ -89,6 +89,8 @@ SYMBOLS = [
     ("msw_bench_kernel", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, c_int64_p,
                                    C.c_void_p]),
     ("msw_set_trace", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("msw_rollout_metrics", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, c_int64_p, C.c_int32,
+                                      c_float_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
 ]
 
 STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,

@@ -201,3 +201,27 @@ def test_edge_cases(cuda):
     cfg = manifest()["weights_K4_F32_cfg"]
     ref = orc.rollout(weights("K4_F32"), cfg, g2.to("cpu"))
     assert per_step_rel(m.rollout(g2).cpu(), ref) <= REL_TOL
+
+
+def test_rollout_metrics_kernel_vs_reference(cuda):
+    """the on-device metrics kernel against the reference's own evaluation
+    functions (fx_metrics.npz): losses within fp32 rounding of the reference's fp32
+    means, confusion counts exact (CSI / F1 equal where defined)."""
+    from mswegnn.metrics import rollout_metrics
+    fx = golden("fx_metrics")
+    n0 = int(fx["n0"])
+    real = torch.from_numpy(golden("fx_small_K4_F32_rollout48")["rollout"])
+    pred = torch.from_numpy(golden("fx_small_K2_F16_rollout48")["rollout"])
+    m = rollout_metrics(pred.to(cuda), real.to(cuda), [(0, n0)], thresholds=(0.05, 0.3))
+    for key, ref in (("rmse", "loss_RMSE"), ("mae", "loss_MAE"), ("rmse_water", "loss_RMSE_water"),
+                     ("mae_water", "loss_MAE_water")):
+        assert rel_err(m[key][0].cpu(), fx[ref]) <= 1e-5, key
+    for thr in (0.05, 0.3):
+        for key in ("csi", "f1"):
+            np.testing.assert_allclose(m[key][thr][0].cpu().numpy(), fx[f"{key}_{thr}"], rtol=1e-6, equal_nan=True)
+    # two simulations in one [N, 2, T] pair (batch layout: consecutive row ranges)
+    p2 = torch.cat([pred[:n0], real[:n0].flip(-1)]).to(cuda)
+    r2 = torch.cat([real[:n0], pred[:n0]]).to(cuda)
+    m2 = rollout_metrics(p2, r2, [(0, n0), (n0, 2 * n0)], thresholds=(0.05,))
+    assert rel_err(m2["rmse"].cpu(), fx["loss_RMSE_stack"]) <= 1e-5
+    np.testing.assert_allclose(m2["csi"][0.05].cpu().numpy(), fx["csi_0.05_stack"], rtol=1e-6, equal_nan=True)

@@ -189,3 +189,22 @@ def test_two_rank_sharding_and_allgather_gloo():
         ref = m.rollout(g, T)[:desc["fine_nodes"]]
         assert np.array_equal(parts[r], ref.numpy()), f"rank {r} slot"
     assert not np.array_equal(parts[0], parts[1]), "ranks must simulate different seeds"
+
+
+def test_metrics_oracle_matches_reference_fixture():
+    """oracle/metrics_ref.py reproduces the reference's own evaluation functions
+    (fx_metrics.npz, made by oracle/gen_golden_metrics.py from utils/miscellaneous.py)."""
+    import metrics_ref as mr
+    fx = golden("fx_metrics")
+    n0 = int(fx["n0"])
+    real = torch.from_numpy(golden("fx_small_K4_F32_rollout48")["rollout"])[:n0]
+    pred = torch.from_numpy(golden("fx_small_K2_F16_rollout48")["rollout"])[:n0]
+    for tl in ("RMSE", "MAE"):
+        assert torch.equal(mr.rollout_loss(pred, real, tl), torch.from_numpy(fx[f"loss_{tl}"]))
+        assert torch.equal(mr.rollout_loss(pred, real, tl, True), torch.from_numpy(fx[f"loss_{tl}_water"]))
+    for thr in (0.05, 0.3):
+        np.testing.assert_array_equal(mr.csi(pred, real, thr).numpy(), fx[f"csi_{thr}"])
+        np.testing.assert_array_equal(mr.f1(pred, real, thr).numpy(), fx[f"f1_{thr}"])
+    p2, r2 = torch.stack([pred, real.flip(-1)]), torch.stack([real, pred])
+    assert torch.equal(mr.rollout_loss(p2, r2, "RMSE"), torch.from_numpy(fx["loss_RMSE_stack"]))
+    np.testing.assert_array_equal(mr.csi(p2, r2, 0.05).numpy(), fx["csi_0.05_stack"])

@@ -31,7 +31,7 @@ for a in starts:
         nx = rows[a + p + 1] if a + p + 1 < len(rows) else None
         if nx is not None:
             gap[p].append((int(nx["Start_Timestamp"]) - e) / 1e3)
-        name[p] = r["Kernel_Name"].split("(")[0].replace("void msw::", "")
+        name[p] = r["Kernel_Name"].split("(")[0].replace("void msw::", "").replace(", ", ",")
         grid[p] = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
 tot_d = tot_g = 0.0
 print(f"{steps} steps of {kps} launches")
@@ -40,5 +40,5 @@ for p in range(kps):
     g = sorted(gap[p])[len(gap[p]) // 2] if gap[p] else 0.0
     tot_d += d
     tot_g += g
-    print(f"{p:3d} {name[p]:22s} wg={grid[p]:5d} dur={d:7.2f}us gap={g:6.2f}us")
+    print(f"{p:3d} {name[p]:28s} wg={grid[p]:6d} dur={d:8.2f}us gap={g:6.2f}us")
 print(f"sum dur {tot_d:.1f} us, sum gap {tot_g:.1f} us, step {tot_d + tot_g:.1f} us")

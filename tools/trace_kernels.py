@@ -40,7 +40,7 @@ def main():
     L.check(L.lib().msw_set_trace(plan._h, C.c_void_p(buf.data_ptr())))
     S = desc["num_scales"]
     cases = [("encode", 0)] + [(k, s) for s in range(S) for k in ("edge_hop", "hop")] + \
-        [("pool", s) for s in range(1, S)]
+        [("pool", s) for s in range(1, S)] + [("unpool", s) for s in range(S - 1)]
     for kern, scale in cases:
         for rep in range(3):  # the last repetition is reported (warm caches)
             buf.zero_()
