@@ -32,6 +32,7 @@ struct MlpDev {
 // LDS offsets (plan.hip: relocate).  F = 64 launches read the blob in place (len = 0).
 struct WReg {
   int off, len;
+  int split;  // floats needed before the epilogue; [split, len) = epilogue operands (or len)
 };
 template <int NT> constexpr bool kStaged = NT <= 2;
 

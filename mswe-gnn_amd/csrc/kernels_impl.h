@@ -321,6 +321,20 @@ __device__ __forceinline__ void stage_region(float* smem, int dst, const float* 
   for (int i = 4 * (int)threadIdx.x; i < r.len; i += 4 * kBlock) st4(smem + dst + i, ld4(W + r.off + i));
 }
 
+// LDS-DMA staging (global_load_lds_dwordx4): one wave instruction copies 1 KB (256 floats)
+// of the region straight into LDS, no VGPR round trip.  Copies the 256-float chunks that
+// cover [first, last) floats of the region; a partial final chunk reads up to 255 floats
+// past the region (the blob and the LDS allocation are padded for it).
+constexpr int kChunk = 256;
+__device__ __forceinline__ void stage_glds(float* smem, const float* __restrict__ W, WReg r, int first, int last) {
+  const int lane = threadIdx.x & 63;
+  for (int ch = first / kChunk + wave_id(); ch * kChunk < last; ch += kWaves)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(W + r.off + ch * kChunk + lane * 4),
+        (__attribute__((address_space(3))) void*)(smem + ch * kChunk), 16, 0, 0);
+}
+__device__ __forceinline__ int chunk_ceil(int n) { return (n + kChunk - 1) / kChunk * kChunk; }
+
 // ---------------------------------------------------------------------------- encoder
 // Static / dynamic node encoders incl. the water-level feature (MSGNN.forward
 // gnn.py:284-294, GNN.forward :112-123) + projection of processor 0 + the x_s part of
@@ -559,8 +573,9 @@ __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopA
   }
 }
 template <int NT, int ACT, int XS>
-__device__ __forceinline__ void edge_hop_tile(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
-                                              const f32x4 (&wf)[NT][NT], float* slab, int j, int lane, int g) {
+__device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
+                                              const f32x4 (&wf)[NT][NT], float* slab, int j, int lane, int g,
+                                              f32x4 (&res_out)[NT]) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT, T2 = 2 * NT;
   const Lanes& L = r.L;
@@ -617,6 +632,13 @@ __device__ __forceinline__ void edge_hop_tile(const EdgeHopRows<NT>& r, const Ed
 #pragma unroll
     for (int t = 0; t < NT; ++t) res[t] = res[t] + r.sk[t];
   }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) res_out[t] = res[t];
+}
+template <int NT, int ACT>
+__device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const Lanes& L, const EdgeHopArgs& a,
+                                                const Common& c, int lane, int g) {
+  constexpr int F = 16 * NT;
   if (a.last) {
     node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
   } else if (L.nv && a.out) {
@@ -637,19 +659,27 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
   if constexpr (!LOOP) {
+    const bool live = tile < a.ntiles;
     EdgeHopRows<NT> r;
-    edge_hop_load<NT>(r, a, tile < a.ntiles ? tile : 0, j, g);  // idle waves stay in bounds
+    edge_hop_load<NT>(r, a, live ? tile : 0, j, g);  // idle waves stay in bounds
     MSW_MARK(c, 1);
+    // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
+    // stream into LDS behind the MLP and are waited for at the epilogue barrier
+    const bool split = kStaged<NT> && a.reg.split < a.reg.len;
     if constexpr (kStaged<NT>) {
-      stage_region(smem, 0, a.c.W, a.reg);
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.split);
       __syncthreads();
       c.W = smem;
+      if (split) stage_glds(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg.len);
     }
     MSW_MARK(c, 2);
-    if (tile < a.ntiles) edge_hop_tile<NT, ACT, XS>(r, a, c, wf, &slab[w][0][0], j, lane, g);
+    f32x4 res[NT];
+    if (live) edge_hop_core<NT, ACT, XS>(r, a, c, wf, &slab[w][0][0], j, lane, g, res);
+    if (split) __syncthreads();  // every wave: the epilogue operands have landed
+    if (live) edge_hop_finish<NT, ACT>(res, r.L, a, c, lane, g);
   } else {
     if constexpr (kStaged<NT>) {
-      stage_region(smem, 0, a.c.W, a.reg);
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -657,7 +687,9 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       EdgeHopRows<NT> q;
       edge_hop_load<NT>(q, a, tile, jj, gg);
-      edge_hop_tile<NT, ACT, XS>(q, a, c, wf, &slab[w][0][0], jj, ln, gg);
+      f32x4 res[NT];
+      edge_hop_core<NT, ACT, XS>(q, a, c, wf, &slab[w][0][0], jj, ln, gg, res);
+      edge_hop_finish<NT, ACT>(res, q.L, a, c, ln, gg);
     }
   }
   MSW_MARK(c, 9);
@@ -696,9 +728,9 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
   Common c = a.c;
   MSW_MARK(c, 0);
   f32x4 wf[NT][NT];
-  if constexpr (!LAST) load_filter<NT>(wf, c.W, a.filt_a, lane);
+  load_filter<NT>(wf, c.W, a.filt_a, lane);  // blob offset: not part of the LDS region
   float* slab = &slab_all[w][0][0];
-  auto run = [&](const HopRows<NT>& r, int j, int lane, int g) {
+  auto core = [&](const HopRows<NT>& r, int j, int lane, int g, f32x4 (&res)[NT]) {
     float* my = slab + j * XS;
     const Lanes& L = r.L;
     store_row<NT>(my, r.inn, NT, g);
@@ -708,16 +740,15 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
     MSW_MARK(c, 4);
     put_message<NT>(my, r.os, od, r.sv, L.ev, a.grad, a.upwind, g);
     MSW_MARK(c, 6);
-    f32x4 agg[NT], res[NT];
+    f32x4 agg[NT];
     gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
     MSW_MARK(c, 7);
 #pragma unroll
     for (int t = 0; t < NT; ++t) res[t] = r.inn[t];
-    if constexpr (LAST)
-      apply_filter<NT>(res, agg, a.filt_a, c.W, lane);
-    else
-      apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+    apply_filter_regs<NT>(res, agg, a.filt_a, wf);
     MSW_MARK(c, 8);
+  };
+  auto finish = [&](f32x4 (&res)[NT], const Lanes& L, int lane, int g) {
     if constexpr (LAST) {
       node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
     } else {
@@ -725,19 +756,23 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
     }
   };
   if constexpr (!LOOP) {
+    const bool live = tile < a.ntiles;
     HopRows<NT> r;
-    hop_load<NT>(r, a, tile < a.ntiles ? tile : 0, j, g);
+    hop_load<NT>(r, a, live ? tile : 0, j, g);
     MSW_MARK(c, 1);
+    // the epilogue's operands stream into LDS alongside the tile's gathers
+    if constexpr (LAST && kStaged<NT>) stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+    f32x4 res[NT];
+    if (live) core(r, j, lane, g, res);
     if constexpr (LAST && kStaged<NT>) {
-      stage_region(smem, 0, a.c.W, a.reg);
       __syncthreads();
       c.W = smem;
     }
     MSW_MARK(c, 2);
-    if (tile < a.ntiles) run(r, j, lane, g);
+    if (live) finish(res, r.L, lane, g);
   } else {
     if constexpr (LAST && kStaged<NT>) {
-      stage_region(smem, 0, a.c.W, a.reg);
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -745,7 +780,9 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       HopRows<NT> q;
       hop_load<NT>(q, a, tile, jj, gg);
-      run(q, jj, ln, gg);
+      f32x4 res[NT];
+      core(q, jj, ln, gg, res);
+      finish(res, q.L, ln, gg);
     }
   }
   MSW_MARK(c, 9);
@@ -793,7 +830,7 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
     load(r0, tile < a.ntiles ? tile : 0, j, g);
     MSW_MARK(c, 1);
     if constexpr (kStaged<NT>) {
-      stage_region(smem, 0, a.c.W, a.reg);
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -801,7 +838,7 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
     if (tile < a.ntiles) run(r0, j, lane, g);
   } else {
     if constexpr (kStaged<NT>) {
-      stage_region(smem, 0, a.c.W, a.reg);
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -848,8 +885,11 @@ __global__ __launch_bounds__(kBlock) void k_rowmlp(RowMlpArgs a) {
 // ---------------------------------------------------------------------------- launchers
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// dynamic LDS of a launch: its weight region rounded up to whole 1-KB LDS-DMA chunks
 template <int NT>
-constexpr size_t lds_bytes(int floats) { return kStaged<NT> ? (size_t)floats * sizeof(float) : 0; }
+constexpr size_t lds_bytes(int floats) {
+  return kStaged<NT> ? (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float) : 0;
+}
 
 // Allow the dynamic weight regions past the 64 KB default (gfx950: 160 KB per CU).
 template <int NT>

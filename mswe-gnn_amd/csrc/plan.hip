@@ -558,7 +558,11 @@ struct RegionBuilder {
     memo[off] = r;
     return r;
   }
-  WReg done() const { return WReg{base, (int)B.h.size() - base}; }
+  int pos() const { return (int)B.h.size() - base; }
+  WReg done(int split = -1) const {
+    const int len = (int)B.h.size() - base;
+    return WReg{base, len, split < 0 ? len : split};
+  }
 };
 
 struct Relocator {
@@ -614,14 +618,14 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       RegionBuilder R(P->blob, 0);
       a.b1_off = R.put(a.b1_off, 16 * a.h1t);
       rl.mlp(R, a.rest);  // filt_a stays a blob offset: k_edge_hop loads it into registers
+      const int split = R.pos();  // operands after this one stream in behind the MLP
       if (a.last) rl.epi(R, a.epi);
-      a.reg = R.done();
+      a.reg = R.done(split);
       reg = &a.reg;
     } else if (L.kind == L_HOP) {
       HopArgs& a = L.hop;
       if (!a.last) continue;  // middle hops load their filter from the blob (k_hop<.., false>)
-      RegionBuilder R(P->blob, 0);
-      a.filt_a = R.put(a.filt_a, P->NT * P->NT * 256);
+      RegionBuilder R(P->blob, 0);  // filt_a stays a blob offset (k_hop loads it into registers)
       rl.epi(R, a.epi);
       a.reg = R.done();
       reg = &a.reg;
@@ -632,7 +636,7 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       a.reg = R.done();
       reg = &a.reg;
     }
-    if (reg) tot = reg->len;
+    if (reg) tot = (reg->len + 255) / 256 * 256;  // LDS-DMA chunks
     if (tot > kMaxRegionFloats)
       return fail(MSW_ERR_UNSUPPORTED, "weights of one launch exceed the LDS budget (" + std::to_string(tot * 4) + " B)");
   }
@@ -990,6 +994,7 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
   if (P->NT <= 2) {
     if ((rc = relocate(P.get(), P->sched_fwd)) || (rc = relocate(P.get(), P->sched_roll))) return rc;
   }
+  P->blob.alloc(256);  // slack: LDS-DMA chunks may read up to 255 floats past a region
   if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
   for (auto* q : {&P->sched_fwd, &P->sched_roll})
     for (Launch& L : *q) L.common().W = P->dW;
