@@ -84,9 +84,10 @@ struct Common {
 struct EncodeArgs {
   Common c;
   int max_blocks;          // grid cap (resident workgroups), <= 0 = one per 64-row chunk
-  WReg reg;                // static encoder (every scale)
-  WReg sreg[kMaxScales];   // + per scale: dynamic encoder & projection 0 (s = 0), unpool V
-  int lds_floats;          // max over s of reg.len + sreg[s].len
+  WReg reg;                // unused (len 0)
+  WReg sreg[kMaxScales];   // per scale: static encoder, dynamic encoder & projection 0
+                           // (s = 0), unpool V -- the static encoder at the same offsets
+  int lds_floats;          // max over s of sreg[s].len
   const float* x;          // input rows (forward: graph rows via perm; rollout: X)
   int x_internal;
   int Npad;
@@ -130,7 +131,8 @@ struct Epilogue {
 struct EdgeHopArgs {
   Common c;
   WReg reg;
-  int max_blocks;                  // grid cap (resident workgroups), <= 0 = one per 4 tiles
+  int max_blocks;                  // grid cap of the grid-stride variant (resident workgroups)
+  int fit_blocks;                  // workgroups of the one-tile-per-wave variant the chip holds
   int n0;                          // first internal row of the destination scale
   const LaneRec* recs; int ntiles; // [ntiles][16]
   const float* xs;
@@ -156,7 +158,8 @@ struct EdgeHopArgs {
 struct HopArgs {
   Common c;
   WReg reg;
-  int max_blocks;                  // grid cap (resident workgroups), <= 0 = one per 4 tiles
+  int max_blocks;                  // grid cap of the grid-stride variant (resident workgroups)
+  int fit_blocks;                  // workgroups of the one-tile-per-wave variant the chip holds
   int n0;                  // first internal row of the scale
   const LaneRec* recs; int ntiles;
   const float* s;          // [16 ntiles][F]
@@ -173,7 +176,8 @@ struct HopArgs {
 struct PoolArgs {
   Common c;
   WReg reg;
-  int max_blocks;                  // grid cap (resident workgroups), <= 0 = one per 4 tiles
+  int max_blocks;                  // grid cap of the grid-stride variant (resident workgroups)
+  int fit_blocks;                  // workgroups of the one-tile-per-wave variant the chip holds
   int n0;                  // first internal row of the coarse scale
   const LaneRec* recs; int ntiles;  // edge lanes = children, node lanes = coarse nodes
   const float* in;         // x_down
@@ -215,7 +219,7 @@ hipError_t launch_init_state(const InitArgs& a, hipStream_t st);
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
 template <int NT> hipError_t prepare_kernels();
 // kind 0 encode, 1 edge_hop, 2 hop, 3 pool
-template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes);
+template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop);
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);

@@ -214,12 +214,37 @@ __device__ __forceinline__ void side_proj(const f32x4 (&in)[TIN], int h1t, const
     side_proj_t<TIN, NT, NT>(in, A, dst, n, valid, lane, g);
 }
 
+// Everything an epilogue reads from HBM that does not depend on the tile's result, loaded
+// with the tile's gathers at kernel start instead of after the hop (one latency less on the
+// chain): x_s rows for the projections, the decoder's dynamic state columns, the step.
+constexpr int kMaxDyn = 16;
+template <int NT>
+struct EpiPre {
+  f32x4 xs[NT];
+  float xd[kMaxDyn];  // X[row, nstat : nnf] (lane group 0 uses it)
+  int ext, step;
+};
+template <int NT>
+__device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, const Common& c,
+                                             const float* xs_rows, size_t n, int g) {
+  constexpr int F = 16 * NT;
+  if (e.np.a_u >= 0 || e.np.a_v >= 0 || e.np.a_o >= 0 || e.uu_a >= 0) load_row<NT>(p.xs, xs_rows + n * F, g);
+  if (e.dec.on) {
+    p.ext = c.perm ? c.perm[n] : (int)n;
+    p.step = e.dec.io ? e.dec.io->step : 0;
+    const size_t row = e.dec.x_internal ? n : (size_t)(p.ext > 0 ? p.ext : 0);
+    const float* xr = e.dec.X + row * c.nnf + (c.nnf - c.dyn);
+#pragma unroll
+    for (int k = 0; k < kMaxDyn; ++k) p.xd[k] = k < c.dyn ? xr[k] : 0.f;
+  }
+}
+
 // tanh(x_up) -> node_decoder -> + learned residual -> ReLU -> small-depth mask
 // (gnn.py:335-348, models.py:50-91); rollout mode: use_prediction + BC of the next step
 // (dataset.py:486-529) and the rollout write (train.py:88-95).
 template <int NT, int ACT>
-__device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDesc& d,
-                                            const Common& c, int n, bool valid, int lane, int g) {
+__device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDesc& d, const Common& c,
+                                            const EpiPre<NT>& pre, int n, bool valid, int lane, int g) {
 #pragma clang fp contract(off)
   f32x4 x0[NT], o[1];
 #pragma unroll
@@ -227,18 +252,20 @@ __device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDes
   act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
   run_mlp<NT, NT, 1, ACT>(x0, o, d.dec, c.W, lane, g);
   if (!valid || g) return;  // lane group 0 holds output features 0 (h) and 1 (|q|)
-  const int ext = c.perm ? c.perm[n] : n;
+  const int ext = pre.ext;
   if (ext < 0) return;
-  const float* xr = d.X + (size_t)(d.x_internal ? n : ext) * c.nnf;
-  const int nstat = c.nnf - c.dyn;
+  float* xw = const_cast<float*>(d.X) + (size_t)(d.x_internal ? n : ext) * c.nnf + (c.nnf - c.dyn);
   float h = o[0].x, v = o[0].y;
   if (d.resw_off >= 0) {
     const float* rw = c.W + d.resw_off;
-    float rh = xr[nstat] * rw[0];
-    float rv = xr[nstat + 1] * rw[1];
-    for (int tau = 1; tau < c.p; ++tau) {
-      rh = rh + xr[nstat + 2 * tau] * rw[2 * tau];
-      rv = rv + xr[nstat + 2 * tau + 1] * rw[2 * tau + 1];
+    float rh = pre.xd[0] * rw[0];
+    float rv = pre.xd[1] * rw[1];
+#pragma unroll
+    for (int tau = 1; tau < kMaxDyn / 2; ++tau) {
+      if (tau < c.p) {
+        rh = rh + pre.xd[2 * tau] * rw[2 * tau];
+        rv = rv + pre.xd[2 * tau + 1] * rw[2 * tau + 1];
+      }
     }
     h = h + rh;
     v = v + rv;
@@ -253,32 +280,33 @@ __device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDes
     return;
   }
   RolloutIO* io = d.io;
-  const int t = io->step;
+  const int t = pre.step;
   io->out[((size_t)ext * 2 + 0) * io->T + t] = hm;
   io->out[((size_t)ext * 2 + 1) * io->T + t] = vm;
-  float* xw = const_cast<float*>(xr);
-  for (int k = 0; k + 2 < c.dyn; ++k) xw[nstat + k] = xw[nstat + k + 2];
-  xw[c.nnf - 2] = hm;
-  xw[c.nnf - 1] = vm;
+  // use_prediction: shift the window by one step, the prediction becomes the newest pair
+#pragma unroll
+  for (int k = 0; k + 2 < kMaxDyn; ++k)
+    if (k + 2 < c.dyn) xw[k] = pre.xd[k + 2];
+  xw[c.dyn - 2] = hm;
+  xw[c.dyn - 1] = vm;
   const int b = d.bc_slot ? d.bc_slot[n] : -1;
   if (b >= 0 && t + 1 < io->bc_tstride) {
     for (int tau = 0; tau < c.p; ++tau)
-      xw[nstat + (io->type_bc - 1) + 2 * tau] = io->bc[((size_t)b * c.p + tau) * io->bc_tstride + t + 1];
+      xw[(io->type_bc - 1) + 2 * tau] = io->bc[((size_t)b * c.p + tau) * io->bc_tstride + t + 1];
   }
 }
 
 // What follows the last hop of a SWEGNN layer, on the layer's destination rows.
 template <int NT, int ACT>
 __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& e, const Common& c,
-                                              const float* xs_rows, float* out, int n,
+                                              const EpiPre<NT>& pre, float* out, int n,
                                               bool valid, int lane, int g) {
   constexpr int F = 16 * NT, T2 = 2 * NT;
   if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
   if (out && valid) store_row<NT>(out + (size_t)n * F, res, NT, g);
   const bool np = e.np.a_u >= 0 || e.np.a_v >= 0 || e.np.a_o >= 0;
   if (np || e.uu_a >= 0) {
-    f32x4 xs[NT];
-    load_row<NT>(xs, xs_rows + (size_t)n * F, g);
+    const f32x4(&xs)[NT] = pre.xs;
     if (np) np_project<NT>(xs, res, e.np, c.W, n, valid, lane, g);
     if (e.uu_a >= 0) {
       f32x4 in[T2];
@@ -290,7 +318,7 @@ __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& 
       side_proj<T2, NT>(in, e.uu_h1t, c.W + e.uu_a, e.Uu, n, valid, lane, g);
     }
   }
-  if (e.dec.on) decode_rows<NT, ACT>(res, e.dec, c, n, valid, lane, g);
+  if (e.dec.on) decode_rows<NT, ACT>(res, e.dec, c, pre, n, valid, lane, g);
 }
 
 // ---------------------------------------------------------------------------- tracing
@@ -314,13 +342,6 @@ __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& 
 #endif
 
 // ---------------------------------------------------------------------------- staging
-// Copy a launch's weight region into LDS (all threads; one batch of independent 16-B loads,
-// so the whole MLP chain then waits on one memory latency instead of one per layer).
-__device__ __forceinline__ void stage_region(float* smem, int dst, const float* __restrict__ W, WReg r) {
-#pragma unroll 4
-  for (int i = 4 * (int)threadIdx.x; i < r.len; i += 4 * kBlock) st4(smem + dst + i, ld4(W + r.off + i));
-}
-
 // LDS-DMA staging (global_load_lds_dwordx4): one wave instruction copies 1 KB (256 floats)
 // of the region straight into LDS, no VGPR round trip.  Copies the 256-float chunks that
 // cover [first, last) floats of the region; a partial final chunk reads up to 255 floats
@@ -373,8 +394,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     if constexpr (kStaged<NT>) {
       if (s != staged) {  // uniform across the workgroup: every wave walks the same chunks
         if (staged >= 0) __syncthreads();  // everyone is done with the old region
-        else stage_region(smem, 0, a.c.W, a.reg);
-        stage_region(smem, a.reg.len, a.c.W, a.sreg[s]);
+        stage_glds(smem, a.c.W, a.sreg[s], 0, a.sreg[s].len);
         __syncthreads();
         staged = s;
         c.W = smem;
@@ -550,6 +570,7 @@ template <int NT>
 struct EdgeHopRows {  // everything one tile reads from HBM
   Lanes L;
   f32x4 Us[2 * NT], Ps[2 * NT], Vn[2 * NT], os[NT], inn[NT], sk[NT];
+  EpiPre<NT> pre;  // a.last only
 };
 template <int NT>
 __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
@@ -571,6 +592,7 @@ __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopA
     r.inn[t] = a.own_zero ? zero4() : ld4(a.in + L.n * F + 16 * t + 4 * g);
     r.sk[t] = a.skip ? ld4(a.skip + L.n * F + 16 * t + 4 * g) : zero4();
   }
+  if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
 }
 template <int NT, int ACT, int XS>
 __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
@@ -636,11 +658,12 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
   for (int t = 0; t < NT; ++t) res_out[t] = res[t];
 }
 template <int NT, int ACT>
-__device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const Lanes& L, const EdgeHopArgs& a,
+__device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const EdgeHopRows<NT>& r, const EdgeHopArgs& a,
                                                 const Common& c, int lane, int g) {
   constexpr int F = 16 * NT;
+  const Lanes& L = r.L;
   if (a.last) {
-    node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
+    node_epilogue<NT, ACT>(res, a.epi, c, r.pre, a.out, L.n, L.nv, lane, g);
   } else if (L.nv && a.out) {
     store_row<NT>(a.out + L.n * F, res, NT, g);
   }
@@ -676,7 +699,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
     f32x4 res[NT];
     if (live) edge_hop_core<NT, ACT, XS>(r, a, c, wf, &slab[w][0][0], j, lane, g, res);
     if (split) __syncthreads();  // every wave: the epilogue operands have landed
-    if (live) edge_hop_finish<NT, ACT>(res, r.L, a, c, lane, g);
+    if (live) edge_hop_finish<NT, ACT>(res, r, a, c, lane, g);
   } else {
     if constexpr (kStaged<NT>) {
       stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
@@ -689,7 +712,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
       edge_hop_load<NT>(q, a, tile, jj, gg);
       f32x4 res[NT];
       edge_hop_core<NT, ACT, XS>(q, a, c, wf, &slab[w][0][0], jj, ln, gg, res);
-      edge_hop_finish<NT, ACT>(res, q.L, a, c, ln, gg);
+      edge_hop_finish<NT, ACT>(res, q, a, c, ln, gg);
     }
   }
   MSW_MARK(c, 9);
@@ -706,14 +729,16 @@ template <int NT>
 struct HopRows {
   Lanes L;
   f32x4 os[NT], sv[NT], inn[NT];
+  EpiPre<NT> pre;  // LAST only
 };
-template <int NT>
+template <int NT, bool LAST>
 __device__ __forceinline__ void hop_load(HopRows<NT>& r, const HopArgs& a, int tile, int j, int g) {
   constexpr int F = 16 * NT;
   r.L = lanes_of(load_rec(a.recs, tile, j), tile, j, a.n0);
   load_row<NT>(r.os, a.in + r.L.sr * F, g);
   load_row<NT>(r.sv, a.s + r.L.p * F, g);
   load_row<NT>(r.inn, a.in + r.L.n * F, g);
+  if constexpr (LAST) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, r.L.n, g);
 }
 template <int NT, int ACT, bool LAST, bool LOOP>
 __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
@@ -748,9 +773,10 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
     apply_filter_regs<NT>(res, agg, a.filt_a, wf);
     MSW_MARK(c, 8);
   };
-  auto finish = [&](f32x4 (&res)[NT], const Lanes& L, int lane, int g) {
+  auto finish = [&](f32x4 (&res)[NT], const HopRows<NT>& r, int lane, int g) {
+    const Lanes& L = r.L;
     if constexpr (LAST) {
-      node_epilogue<NT, ACT>(res, a.epi, c, a.xs, a.out, L.n, L.nv, lane, g);
+      node_epilogue<NT, ACT>(res, a.epi, c, r.pre, a.out, L.n, L.nv, lane, g);
     } else {
       if (L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
     }
@@ -758,7 +784,7 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
   if constexpr (!LOOP) {
     const bool live = tile < a.ntiles;
     HopRows<NT> r;
-    hop_load<NT>(r, a, live ? tile : 0, j, g);
+    hop_load<NT, LAST>(r, a, live ? tile : 0, j, g);
     MSW_MARK(c, 1);
     // the epilogue's operands stream into LDS alongside the tile's gathers
     if constexpr (LAST && kStaged<NT>) stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
@@ -769,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
       c.W = smem;
     }
     MSW_MARK(c, 2);
-    if (live) finish(res, r.L, lane, g);
+    if (live) finish(res, r, lane, g);
   } else {
     if constexpr (LAST && kStaged<NT>) {
       stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
@@ -779,10 +805,10 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
     for (; tile < a.ntiles; tile += stride) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       HopRows<NT> q;
-      hop_load<NT>(q, a, tile, jj, gg);
+      hop_load<NT, LAST>(q, a, tile, jj, gg);
       f32x4 res[NT];
       core(q, jj, ln, gg, res);
-      finish(res, q.L, ln, gg);
+      finish(res, q, ln, gg);
     }
   }
   MSW_MARK(c, 9);
@@ -922,20 +948,22 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// one tile per wave while the grid fits the chip; grid-stride loop beyond that
-static inline bool tile_loop(int ntiles, int max_blocks) {
-  return max_blocks > 0 && cdiv(ntiles, kWaves) > max_blocks;
+// one tile per wave while that grid is resident at once; grid-stride loop beyond that
+template <class A>
+static inline bool tile_loop(const A& a) {
+  return a.fit_blocks > 0 && a.max_blocks > 0 && cdiv(a.ntiles, kWaves) > a.fit_blocks;
 }
-static inline int tile_grid(int ntiles, int max_blocks) {
-  return tile_loop(ntiles, max_blocks) ? max_blocks : cdiv(ntiles, kWaves);
+template <class A>
+static inline int tile_grid(const A& a) {
+  return tile_loop(a) ? a.max_blocks : cdiv(a.ntiles, kWaves);
 }
 
 template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(tile_grid(a.ntiles, a.max_blocks)), block(kBlock);
+  const dim3 grid(tile_grid(a)), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.reg.len);
-  const bool loop = tile_loop(a.ntiles, a.max_blocks);
+  const bool loop = tile_loop(a);
   if (a.c.prelu) {
     if (loop) hipLaunchKernelGGL((k_edge_hop<NT, 1, true>), grid, block, sh, st, a);
     else hipLaunchKernelGGL((k_edge_hop<NT, 1, false>), grid, block, sh, st, a);
@@ -948,8 +976,8 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(tile_grid(a.ntiles, a.max_blocks)), block(kBlock);
-  const bool loop = tile_loop(a.ntiles, a.max_blocks);
+  const dim3 grid(tile_grid(a)), block(kBlock);
+  const bool loop = tile_loop(a);
   if (!a.last) {
     if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_hop<NT, 1, false, false>), grid, block, 0, st, a);
@@ -968,9 +996,9 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
 template <int NT>
 hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(tile_grid(a.ntiles, a.max_blocks)), block(kBlock);
+  const dim3 grid(tile_grid(a)), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.reg.len);
-  if (tile_loop(a.ntiles, a.max_blocks))
+  if (tile_loop(a))
     hipLaunchKernelGGL((k_pool<NT, true>), grid, block, sh, st, a);
   else
     hipLaunchKernelGGL((k_pool<NT, false>), grid, block, sh, st, a);
@@ -987,20 +1015,22 @@ hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
 }
 
 // Workgroups of one launch resident on the whole chip (grid cap of the grid-stride kernels).
-template <int NT>
-int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes) {
-  const void* f = nullptr;
+template <int NT, bool LOOP>
+static const void* kernel_of(int kind, int prelu, int last) {
   switch (kind) {
-    case 0: f = prelu ? (const void*)k_encode<NT, 1> : (const void*)k_encode<NT, -1>; break;
-    case 1: f = prelu ? (const void*)k_edge_hop<NT, 1, true> : (const void*)k_edge_hop<NT, -1, true>; break;
+    case 0: return prelu ? (const void*)k_encode<NT, 1> : (const void*)k_encode<NT, -1>;
+    case 1: return prelu ? (const void*)k_edge_hop<NT, 1, LOOP> : (const void*)k_edge_hop<NT, -1, LOOP>;
     case 2:
-      f = !last ? (const void*)k_hop<NT, 1, false, true>
-                : (prelu ? (const void*)k_hop<NT, 1, true, true> : (const void*)k_hop<NT, -1, true, true>);
-      break;
-    default: f = (const void*)k_pool<NT, true>; break;
+      return !last ? (const void*)k_hop<NT, 1, false, LOOP>
+                   : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
+    default: return (const void*)k_pool<NT, LOOP>;
   }
+}
+template <int NT>
+int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
+  const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, kStaged<NT> ? dyn_bytes : 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, lds_bytes<NT>((int)(dyn_bytes / 4))) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
@@ -1009,7 +1039,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes) {
 
 #define MSW_INSTANTIATE(NT)                                                       \
   template hipError_t prepare_kernels<NT>();                                      \
-  template int resident_blocks<NT>(int, int, int, size_t);                        \
+  template int resident_blocks<NT>(int, int, int, size_t, int);                   \
   template hipError_t launch_encode<NT>(const EncodeArgs&, hipStream_t);          \
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \

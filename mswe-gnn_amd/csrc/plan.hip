@@ -597,22 +597,27 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
     WReg* reg = nullptr;
     int tot = 0;
     if (L.kind == L_ENCODE) {
+      // one contiguous region per scale (one LDS-DMA copy per workgroup): the static
+      // encoder first -- identical relative offsets in every scale's region -- then the
+      // dynamic encoder + projection 0 (scale 0) and that scale's unpool V operand
       EncodeArgs& a = L.enc;
-      RegionBuilder R0(P->blob, 0);
-      rl.mlp(R0, a.stat);
-      a.reg = R0.done();
-      a.lds_floats = a.reg.len;
+      const MlpDev stat0 = a.stat;
+      a.reg = WReg{0, 0, 0};
+      a.lds_floats = 0;
       for (int s = 0; s < a.S; ++s) {
-        RegionBuilder Rs(P->blob, a.reg.len);
+        RegionBuilder Rs(P->blob, 0);
+        MlpDev st = stat0;
+        rl.mlp(Rs, st);
+        a.stat = st;
         if (s == 0) {
           rl.mlp(Rs, a.dynm);
           rl.np(Rs, a.np0);
         }
         a.vu_a[s] = Rs.put(a.vu_a[s], a.vu_h1t * P->NT * 256);
         a.sreg[s] = Rs.done();
-        a.lds_floats = std::max(a.lds_floats, a.reg.len + a.sreg[s].len);
+        a.lds_floats = std::max(a.lds_floats, a.sreg[s].len);
       }
-      tot = a.lds_floats;
+      tot = (a.lds_floats + 255) / 256 * 256;
     } else if (L.kind == L_EDGE_HOP) {
       EdgeHopArgs& a = L.eh;
       RegionBuilder R(P->blob, 0);
@@ -645,28 +650,26 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
 
 // Grid cap of a grid-stride launch: the workgroups the chip holds at once, so that each
 // stages its weight region once (large meshes) and none waits for a second wave of blocks.
-int resident_of(int NT, int kind, int prelu, int last, size_t bytes) {
+int resident_of(int NT, int kind, int prelu, int last, size_t bytes, int loop) {
   switch (NT) {
-    case 1: return resident_blocks<1>(kind, prelu, last, bytes);
-    case 2: return resident_blocks<2>(kind, prelu, last, bytes);
-    default: return resident_blocks<4>(kind, prelu, last, bytes);
+    case 1: return resident_blocks<1>(kind, prelu, last, bytes, loop);
+    case 2: return resident_blocks<2>(kind, prelu, last, bytes, loop);
+    default: return resident_blocks<4>(kind, prelu, last, bytes, loop);
   }
 }
+template <class A>
+void caps(msw_plan* P, A& a, int kind, int prelu, int last, int floats) {
+  a.max_blocks = resident_of(P->NT, kind, prelu, last, (size_t)floats * 4, 1);
+  a.fit_blocks = resident_of(P->NT, kind, prelu, last, (size_t)floats * 4, 0);
+}
 void set_grid_cap(msw_plan* P, Launch& L) {
-  const int NT = P->NT;
   switch (L.kind) {
     case L_ENCODE:
-      L.enc.max_blocks = resident_of(NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4);
+      L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
       break;
-    case L_EDGE_HOP:
-      L.eh.max_blocks = resident_of(NT, 1, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4);
-      break;
-    case L_HOP:
-      L.hop.max_blocks = resident_of(NT, 2, L.hop.c.prelu, L.hop.last, (size_t)L.hop.reg.len * 4);
-      break;
-    default:
-      L.pool.max_blocks = resident_of(NT, 3, 0, 0, (size_t)L.pool.reg.len * 4);
-      break;
+    case L_EDGE_HOP: caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len); break;
+    case L_HOP: caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len); break;
+    default: caps(P, L.pool, 3, 0, 0, L.pool.reg.len); break;
   }
 }
 
