@@ -133,6 +133,8 @@ def main():
     ap.add_argument("--T", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-roofline-large", action="store_true",
+                    help="skip the hop-kernel roofline on the ~1M-node mesh (config 5)")
     ap.add_argument("--batch", type=int, default=1,
                     help="simulations per GPU, run as one disjoint-union batch (SURVEY §8 f1)")
     args = ap.parse_args()
@@ -220,6 +222,23 @@ def main():
                         "peak_tflops": FP32_MFMA_PEAK_TFS},
                     "k_pool<32> (mean pool + projection), scale 1": {
                         "avg_launch_us": t_pool * 1e6, "rows": r_pool}}}
+        # ---------------- the same hop kernel where HBM, not latency, bounds it: the ~1M-node
+        # mesh of config 5 (fully wet; one rollout step to populate the buffers)
+        if world == 1 and not args.no_roofline_large and args.workload != "hbm1m":
+            gl, ml, _, dl = build_workload("hbm1m", seed=0, T=1)
+            gl = gl.to(dev)
+            ml = ml.to(dev)
+            ml.engine = "hip"
+            pl = plan_for(ml, gl)
+            pl.rollout(gl.x, gl.BC, gl.node_BC, gl.type_BC, 1)
+            tl, (rl, el) = time_kernel(pl, "hop", 0, iters=50)
+            bl = el * (4 * F + 4) + rl * (12 * F + 4)
+            roof["large_mesh"] = {
+                "workload": "hbm1m", "fine_nodes": dl["fine_nodes"], "rows": rl, "edges": el,
+                "algorithmic_bytes_per_launch": bl, "avg_launch_us": tl * 1e6,
+                "achieved": bl / tl / 1e9, "frac": bl / tl / 1e9 / HBM_PEAK_GBS}
+            del pl, ml, gl
+            torch.cuda.empty_cache()
         # ---------------- parity vs the reference fixture (zenodo4 only; CPU reference run)
         parity = {}
         r_gpu = plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()

@@ -172,6 +172,38 @@ struct HopArgs {
   Epilogue epi;
 };
 
+// Two consecutive middle hops (k, k+1 < K) in one launch.  Workgroup b owns the nodes A of
+// its kWaves edge tiles.  Level 1: out_k -> out_{k+1} on B = A + every in-neighbour of A
+// (recomputed redundantly by each workgroup that needs it; same arithmetic, same order as
+// k_hop), kept in LDS.  Level 2: out_{k+1} -> out_{k+2} on A, reading B from LDS.  Saves
+// one launch (its dispatch + drain) per pair at the price of the halo recomputation.
+struct PairRec {  // level-1 lane record (32 B)
+  int src;        // internal source row (out_k from HBM), -1 = no edge in this slot
+  int p;          // tile-padded s slot of the edge
+  int dl;         // destination lane
+  int n;          // internal destination row, -1 = no node in this lane
+  int bl;         // destination's row in the workgroup's LDS set B
+  int q;          // q0 | q1 << 8
+  int pad0, pad1;
+};
+struct Hop2Args {
+  Common c;
+  int max_blocks, fit_blocks;
+  int n0;
+  const LaneRec* recs; int ntiles;  // level 2 = the layer's edge tiles
+  const int2* l2;                   // [ntiles][16] {source, destination} rows in B
+  int nblocks;                      // ceil(ntiles / kWaves)
+  const int* l1_off;                // [nblocks + 1] level-1 tiles of each workgroup
+  const PairRec* l1;                // [level-1 tiles][16]
+  const int* a0;                    // [nblocks] local index of the workgroup's first A node
+  int bmax;                         // rows of the LDS set B (largest workgroup)
+  const float* s;
+  const float* in;                  // out_k
+  float* out;                       // out_{k+2}
+  int filt1, filt2;                 // blob offsets of the filters of hops k and k+1 (-1: none)
+  int grad, upwind;
+};
+
 // Mean pooling into the coarse rows + projection of the next processor.
 struct PoolArgs {
   Common c;
@@ -218,12 +250,13 @@ hipError_t launch_init_state(const InitArgs& a, hipStream_t st);
 
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
 template <int NT> hipError_t prepare_kernels();
-// kind 0 encode, 1 edge_hop, 2 hop, 3 pool
+// kind 0 encode, 1 edge_hop, 2 hop, 3 pool, 4 hop pair
 template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop);
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_hop2(const Hop2Args& a, hipStream_t st);
 template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);
 
 }  // namespace msw

@@ -814,6 +814,77 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- hop pair
+// Hops k and k+1 (both before the layer's last hop) in one launch (engine.h Hop2Args).
+// Grid-stride over workgroup blocks; every wave of a workgroup walks the same blocks, so
+// the barriers are uniform.  Filters come straight from the blob into registers.
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_hop2(Hop2Args a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
+  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
+  extern __shared__ __attribute__((aligned(16))) float outB[];  // [bmax][XS] = out_{k+1} on B
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const Common& c = a.c;
+  f32x4 wf1[NT][NT], wf2[NT][NT];
+  load_filter<NT>(wf1, c.W, a.filt1, lane);
+  load_filter<NT>(wf2, c.W, a.filt2, lane);
+  float* slab = &slab_all[w][0][0];
+  float* my = slab + j * XS;
+  for (int blk = blockIdx.x; blk < a.nblocks; blk += gridDim.x) {
+    // level-2 tile of this wave: records and s rows first (they do not depend on level 1)
+    const int tile2 = blk * kWaves + w;
+    const bool live2 = tile2 < a.ntiles;
+    const int ts = live2 ? tile2 : 0;
+    const Lanes L2 = lanes_of(load_rec(a.recs, ts, j), ts, j, a.n0);
+    const int2 sd = a.l2[(size_t)ts * kRowsPerWave + j];
+    const int a0 = a.a0[blk];
+    f32x4 sv2[NT];
+    load_row<NT>(sv2, a.s + L2.p * F, g);
+    // ---- level 1: out_{k+1} on B (whole in-neighbourhoods, k_hop arithmetic)
+    const int t_end = a.l1_off[blk + 1];
+    for (int t1 = a.l1_off[blk] + w; t1 < t_end; t1 += kWaves) {
+      const int4* rp = reinterpret_cast<const int4*>(a.l1 + (size_t)t1 * kRowsPerWave + j);
+      const int4 r0 = rp[0], r1 = rp[1];  // {src, p, dl, n}, {bl, q, -, -}
+      const bool ev = r0.x >= 0, nv = r0.w >= 0;
+      const size_t sr = (size_t)(ev ? r0.x : a.n0), nn = (size_t)(nv ? r0.w : a.n0);
+      f32x4 os[NT], sv[NT], inn[NT], od[NT];
+      load_row<NT>(os, a.in + sr * F, g);
+      load_row<NT>(sv, a.s + (size_t)(ev ? r0.y : 0) * F, g);
+      load_row<NT>(inn, a.in + nn * F, g);
+      store_row<NT>(my, inn, NT, g);
+      wave_lds_sync();
+      load_row<NT>(od, slab + (ev ? r0.z : 0) * XS, g);
+      put_message<NT>(my, os, od, sv, ev, a.grad, a.upwind, g);
+      f32x4 agg[NT], res[NT];
+      const int q0 = r1.y & 255, q1 = nv ? (r1.y >> 8) : q0;
+      gather_messages<NT, XS>(agg, slab, q0, q1, g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) res[t] = inn[t];
+      apply_filter_regs<NT>(res, agg, a.filt1, wf1);
+      if (nv) store_row<NT>(outB + (size_t)r1.x * XS, res, NT, g);
+    }
+    __syncthreads();
+    // ---- level 2: out_{k+2} on A from B in LDS
+    if (live2) {
+      const int nl = L2.nv ? (int)(L2.n - a.n0) - a0 : 0;
+      f32x4 os[NT], od[NT], inn[NT];
+      load_row<NT>(os, outB + (size_t)(L2.ev ? sd.x : 0) * XS, g);
+      load_row<NT>(od, outB + (size_t)(L2.ev ? sd.y : 0) * XS, g);
+      load_row<NT>(inn, outB + (size_t)nl * XS, g);
+      put_message<NT>(my, os, od, sv2, L2.ev, a.grad, a.upwind, g);
+      f32x4 agg[NT], res[NT];
+      gather_messages<NT, XS>(agg, slab, L2.q0, L2.q1, g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) res[t] = inn[t];
+      apply_filter_regs<NT>(res, agg, a.filt2, wf2);
+      if (L2.nv) store_row<NT>(a.out + L2.n * F, res, NT, g);
+    }
+    __syncthreads();  // outB is reused by the next block
+  }
+}
+
 // ---------------------------------------------------------------------------- pooling
 // scatter(x[fine], coarse, reduce='mean') (gnn.py:256): children summed in edge order,
 // divided by max(count, 1); then the projection of the next processor.  Tiles of coarse
@@ -927,7 +998,7 @@ hipError_t prepare_kernels() {
       (const void*)k_edge_hop<NT, 1, true>, (const void*)k_edge_hop<NT, -1, true>,
       (const void*)k_hop<NT, 1, true, false>, (const void*)k_hop<NT, -1, true, false>,
       (const void*)k_hop<NT, 1, true, true>, (const void*)k_hop<NT, -1, true, true>,
-      (const void*)k_pool<NT, false>, (const void*)k_pool<NT, true>};
+      (const void*)k_pool<NT, false>, (const void*)k_pool<NT, true>, (const void*)k_hop2<NT>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     if (e != hipSuccess) return e;
@@ -1005,6 +1076,14 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 template <int NT>
+hipError_t launch_hop2(const Hop2Args& a, hipStream_t st) {
+  if (a.nblocks <= 0) return hipSuccess;
+  const int grid = a.max_blocks > 0 && a.nblocks > a.max_blocks ? a.max_blocks : a.nblocks;
+  const size_t sh = (size_t)a.bmax * (16 * NT + 4) * sizeof(float);
+  hipLaunchKernelGGL((k_hop2<NT>), dim3(grid), dim3(kBlock), sh, st, a);
+  return hipGetLastError();
+}
+template <int NT>
 hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
   if (a.R <= 0) return hipSuccess;
   if (a.mode == 1)
@@ -1023,14 +1102,16 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 2:
       return !last ? (const void*)k_hop<NT, 1, false, LOOP>
                    : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
-    default: return (const void*)k_pool<NT, LOOP>;
+    case 3: return (const void*)k_pool<NT, LOOP>;
+    default: return (const void*)k_hop2<NT>;
   }
 }
 template <int NT>
 int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, lds_bytes<NT>((int)(dyn_bytes / 4))) != hipSuccess)
+  const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, dyn) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
@@ -1044,6 +1125,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
+  template hipError_t launch_hop2<NT>(const Hop2Args&, hipStream_t);              \
   template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);
 
 }  // namespace msw

@@ -9,6 +9,7 @@
 //   update_batch_multiscale training/train.py:31-65 (batched node_ptr layout)
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -188,6 +189,13 @@ struct ScaleCSR {
   LaneRec* recs = nullptr;      // [ntiles][16]
   int ntiles = 0;
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
+  // hop pairs (engine.h Hop2Args); pair_ok = false -> hops stay one launch each
+  bool pair_ok = false;
+  int pair_blocks = 0, pair_bmax = 0;
+  int* pair_l1_off = nullptr;
+  PairRec* pair_l1 = nullptr;
+  int* pair_a0 = nullptr;
+  int2* pair_l2 = nullptr;
 };
 
 struct LevelMaps {              // level l: coarse scale l+1, fine scale l
@@ -216,7 +224,7 @@ struct Proc {                   // one SWEGNN layer bound to a scale (or an intr
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOP2 };
 struct Launch {
   int kind;
   int scale;                    // destination scale (bench hook)
@@ -225,6 +233,7 @@ struct Launch {
     EdgeHopArgs eh;
     HopArgs hop;
     PoolArgs pool;
+    Hop2Args hop2;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
   Common& common() {
@@ -232,6 +241,7 @@ struct Launch {
       case L_ENCODE: return enc.c;
       case L_EDGE_HOP: return eh.c;
       case L_HOP: return hop.c;
+      case L_HOP2: return hop2.c;
       default: return pool.c;
     }
   }
@@ -272,6 +282,7 @@ struct msw_plan {
   int kernels_per_step = 0;
   std::vector<Launch> sched_fwd, sched_roll;  // one forward step: forward / rollout mode
   int use_graph = 1;
+  int hop_pairs = 1;  // fuse hop pairs (MSW_NO_HOP_PAIRS=1 disables, for A/B measurements)
   hipStream_t cap_stream = nullptr;
   hipGraphExec_t step_exec = nullptr;
   std::vector<void*> owned;
@@ -433,6 +444,24 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   q.push_back(L1);
   const float* cur = P->T[0];
   for (int k = 2; k <= pr.K; ++k) {
+    if (g.pair_ok && k + 1 < pr.K) {  // hops k, k+1 in one launch (neither is the last)
+      float* nxt = cur == P->T[0] ? P->T[1] : P->T[0];
+      Launch L;
+      L.kind = L_HOP2;
+      L.scale = pr.scale;
+      Hop2Args& h = L.hop2;
+      h.c = c;
+      h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles; h.l2 = g.pair_l2; h.nblocks = g.pair_blocks;
+      h.l1_off = g.pair_l1_off; h.l1 = g.pair_l1; h.a0 = g.pair_a0; h.bmax = g.pair_bmax;
+      h.s = P->s; h.in = cur; h.out = nxt;
+      h.filt1 = pr.filt.empty() ? -1 : pr.filt[k - 1];
+      h.filt2 = pr.filt.empty() ? -1 : pr.filt[k];
+      h.grad = pr.with_gradient; h.upwind = pr.upwind;
+      q.push_back(L);
+      cur = nxt;
+      ++k;
+      continue;
+    }
     float* nxt = (k == pr.K) ? out : (cur == P->T[0] ? P->T[1] : P->T[0]);
     Launch L;
     L.kind = L_HOP;
@@ -627,6 +656,8 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       if (a.last) rl.epi(R, a.epi);
       a.reg = R.done(split);
       reg = &a.reg;
+    } else if (L.kind == L_HOP2) {
+      continue;  // filters from the blob, no LDS weight region
     } else if (L.kind == L_HOP) {
       HopArgs& a = L.hop;
       if (!a.last) continue;  // middle hops load their filter from the blob (k_hop<.., false>)
@@ -669,6 +700,9 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     case L_EDGE_HOP: caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len); break;
     case L_HOP: caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len); break;
+    case L_HOP2:
+      L.hop2.max_blocks = resident_of(P->NT, 4, 0, 0, (size_t)L.hop2.bmax * (16 * P->NT + 4) * 4, 0);
+      break;
     default: caps(P, L.pool, 3, 0, 0, L.pool.reg.len); break;
   }
 }
@@ -679,6 +713,7 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_ENCODE: return launch_encode<NT>(L.enc, st);
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
+    case L_HOP2: return launch_hop2<NT>(L.hop2, st);
     default: return launch_pool<NT>(L.pool, st);
   }
 }
@@ -708,6 +743,85 @@ void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
       e->dec.y = y;
     }
   }
+}
+
+constexpr int kPairMaxTiles = 1024;
+
+// Level-1 / level-2 structures of the hop-pair kernel for one scale (engine.h Hop2Args).
+// rowptr / so: the scale's CSR by destination (local rows / internal source rows);
+// pcsr: tile-padded slot -> CSR position.  Leaves pair_ok = false when a workgroup's B set
+// would not fit the LDS budget (the schedule then keeps one launch per hop).
+int build_pairs(msw_plan* P, ScaleCSR& c, const std::vector<int>& rowptr, const std::vector<int>& so,
+                const std::vector<TileRange>& tl, const std::vector<int>& pcsr) {
+  const int ns = c.ns, n0 = c.n0, nt = (int)tl.size();
+  // only where a launch is latency-bound: on larger scales the halo recomputation costs
+  // more than the saved launch (measured: zenodo4 +1 %, batch of 8 / dk15 -2..-4 % when
+  // every scale pairs; the finest zenodo4 scale has ~2k tiles)
+  if (nt == 0 || nt > kPairMaxTiles) return MSW_OK;
+  std::vector<int> slot_of_csr(rowptr[ns], -1);
+  for (size_t q = 0; q < pcsr.size(); ++q)
+    if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
+  const int nb = (nt + kWaves - 1) / kWaves;
+  std::vector<int> stamp(ns, -1), bidx(ns, -1), B, l1_off(nb + 1, 0), a0(nb);
+  std::vector<PairRec> l1;
+  std::vector<int2> l2((size_t)nt * kRowsPerWave, int2{0, 0});
+  int bmax = 0;
+  for (int b = 0; b < nb; ++b) {
+    const int t0 = b * kWaves, t1 = std::min(t0 + kWaves, nt);
+    const int abeg = tl[t0].node0, aend = tl[t1 - 1].node0 + tl[t1 - 1].nnode;
+    B.clear();
+    for (int v = abeg; v < aend; ++v) { stamp[v] = b; bidx[v] = (int)B.size(); B.push_back(v); }
+    for (int v = abeg; v < aend; ++v)
+      for (int i = rowptr[v]; i < rowptr[v + 1]; ++i) {
+        const int u = so[i] - n0;
+        if (stamp[u] != b) { stamp[u] = b; bidx[u] = (int)B.size(); B.push_back(u); }
+      }
+    bmax = std::max(bmax, (int)B.size());
+    a0[b] = abeg;
+    // level-1 tiles over B: whole in-neighbourhoods, <= 16 edges and <= 16 nodes each
+    l1_off[b] = (int)(l1.size() / kRowsPerWave);
+    size_t tbase = l1.size();
+    int nn = 0, ne = 0;
+    auto open_tile = [&]() {
+      tbase = l1.size();
+      l1.resize(tbase + kRowsPerWave, PairRec{-1, 0, 0, -1, 0, 0, 0, 0});
+      nn = ne = 0;
+    };
+    open_tile();
+    for (int v : B) {
+      const int d = rowptr[v + 1] - rowptr[v];
+      if (d > kRowsPerWave) return fail(MSW_ERR_UNSUPPORTED, "node with more than 16 in-edges");
+      if (nn == kRowsPerWave || ne + d > kRowsPerWave) open_tile();
+      PairRec* T = &l1[tbase];
+      T[nn].n = n0 + v;
+      T[nn].bl = bidx[v];
+      T[nn].q = ne | ((ne + d) << 8);
+      for (int i = rowptr[v]; i < rowptr[v + 1]; ++i, ++ne) {
+        T[ne].src = so[i];
+        T[ne].p = slot_of_csr[i];
+        T[ne].dl = nn;
+      }
+      ++nn;
+    }
+    // level 2: B rows of each edge slot of the workgroup's own tiles
+    for (int t = t0; t < t1; ++t)
+      for (int jn = 0; jn < tl[t].nnode; ++jn) {
+        const int v = tl[t].node0 + jn;
+        for (int i = rowptr[v]; i < rowptr[v + 1]; ++i)
+          l2[(size_t)t * kRowsPerWave + (i - tl[t].edge0)] = int2{bidx[so[i] - n0], bidx[v]};
+      }
+  }
+  l1_off[nb] = (int)(l1.size() / kRowsPerWave);
+  const size_t lds = (size_t)bmax * (16 * P->NT + 4) * sizeof(float);
+  if (lds > 64 * 1024) return MSW_OK;  // B too large for LDS: no pairs on this scale
+  int rc;
+  if ((rc = pupload(P, &c.pair_l1_off, l1_off)) || (rc = pupload(P, &c.pair_l1, l1)) ||
+      (rc = pupload(P, &c.pair_a0, a0)) || (rc = pupload(P, &c.pair_l2, l2)))
+    return rc;
+  c.pair_blocks = nb;
+  c.pair_bmax = bmax;
+  c.pair_ok = true;
+  return MSW_OK;
 }
 
 int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
@@ -776,6 +890,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     for (size_t q = 0; q < pcsr.size(); ++q)
       if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
     if ((rc = pupload(P, &c.recs, recs))) return rc;
+    if (P->hop_pairs && (rc = build_pairs(P, c, rowptr, so, tl, pcsr))) return rc;
   }
   // intra-scale levels
   P->lv.assign(S > 1 ? S - 1 : 0, LevelMaps{});
@@ -827,8 +942,8 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
 int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
   if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
   if (P->sched_roll.empty()) return fail(MSW_ERR_INVALID, "run a rollout before bench_kernel");
-  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP};
-  if (kernel < 0 || kernel > 4) return fail(MSW_ERR_INVALID, "unknown kernel id");
+  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP, L_HOP2};
+  if (kernel < 0 || kernel > 5) return fail(MSW_ERR_INVALID, "unknown kernel id");
   const bool unpool = kernel == 4;  // the intra-scale (unpooling) layer into `scale`
   const Launch* src = nullptr;
   for (const Launch& L : P->sched_roll)
@@ -911,6 +1026,7 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     return fail(MSW_ERR_INVALID, "MSGNN needs S-1 intra-scale layers");
   if (m->model_type == 1 && m->num_processors < 1) return fail(MSW_ERR_INVALID, "GNN needs >= 1 layer");
 
+  P->hop_pairs = getenv("MSW_NO_HOP_PAIRS") ? 0 : 1;
   int rc = build_graph_plan(P.get(), g);
   if (rc) return rc;
   const int F = P->F, Npad = P->Npad;
