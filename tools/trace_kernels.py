@@ -40,15 +40,23 @@ def main():
     L.check(L.lib().msw_set_trace(plan._h, C.c_void_p(buf.data_ptr())))
     S = desc["num_scales"]
     cases = [("encode", 0)] + [(k, s) for s in range(S) for k in ("edge_hop", "hop")] + \
-        [("pool", s) for s in range(1, S)] + [("unpool", s) for s in range(S - 1)]
+        [("pool", s) for s in range(1, S)] + [("unpool", s) for s in range(S - 1)] + \
+        [("hop2", s) for s in range(1, S)]
     for kern, scale in cases:
-        for rep in range(3):  # the last repetition is reported (warm caches)
-            buf.zero_()
-            plan.bench_kernel(kern, scale, 1)
-            torch.cuda.synchronize()
+        try:
+            for rep in range(3):  # the last repetition is reported (warm caches)
+                buf.zero_()
+                plan.bench_kernel(kern, scale, 1)
+                torch.cuda.synchronize()
+        except RuntimeError as e:  # e.g. no hop pair on that scale
+            print(f"{kern:9s} scale {scale}: n/a ({e})")
+            continue
         t = buf.cpu().tolist()
         clk0, rt0 = t[0], t[1]
         marks = [(k, t[2 * k] - clk0, (t[2 * k + 1] - rt0) * 10.0) for k in range(10) if t[2 * k] != 0]
+        if len(marks) < 2:
+            print(f"{kern:9s} scale {scale}: no phase marks in this kernel")
+            continue
         last = marks[-1]
         mhz = last[1] / (last[2] / 1e3) if last[2] > 0 else float("nan")
         print(f"{kern:9s} scale {scale}: {last[2] / 1e3:6.2f} us on wave 0 (~{mhz:.0f} MHz)")
