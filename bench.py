@@ -236,7 +236,8 @@ def main():
             roof["large_mesh"] = {
                 "workload": "hbm1m", "fine_nodes": dl["fine_nodes"], "rows": rl, "edges": el,
                 "algorithmic_bytes_per_launch": bl, "avg_launch_us": tl * 1e6,
-                "achieved": bl / tl / 1e9, "frac": bl / tl / 1e9 / HBM_PEAK_GBS}
+                "achieved": bl / tl / 1e9, "frac": bl / tl / 1e9 / HBM_PEAK_GBS,
+                "traffic": read_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_hop_large")}
             del pl, ml, gl
             torch.cuda.empty_cache()
         # ---------------- parity vs the reference fixture (zenodo4 only; CPU reference run)

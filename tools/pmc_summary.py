@@ -47,6 +47,10 @@ def main():
     if hops:
         k, v = max(hops, key=lambda kv: kv[1]["dispatches"])
         res["k_hop"] = dict(v, kernel=k)
+        # bench.py's large-mesh roofline (config 5): the middle hop with the largest grid
+        mids = [(kk, vv) for kk, vv in hops if "false," in kk or kk.count("false") >= 1]
+        kl, vl = max(mids or hops, key=lambda kv: int(kv[0].split("grid=")[1]))
+        res["k_hop_large"] = dict(vl, kernel=kl)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res.get("k_hop"), indent=1))
 
