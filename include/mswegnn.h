@@ -144,11 +144,51 @@ typedef struct {
   int32_t graph_captured;    /* a hipGraph of one rollout step is instantiated */
 } msw_plan_stats;
 
+/* Halo exchange of one rank of a single mesh split over several ranks (SURVEY §8 f2,
+ * mswegnn/partition.py).  The graph given to msw_plan_create_part is the rank's LOCAL graph
+ * (owned nodes + halo nodes, in-edges of owned nodes only).  An entry = one (scale, peer)
+ * pair: the rows this rank receives from `peer` (its halo rows of that scale, local graph
+ * numbering) and the rows it sends to `peer` (its owned rows the peer holds as halo, in the
+ * peer's receive order).  Exchanged before every launch that gathers from other nodes:
+ * U and out_0 before a layer's first hop, out_k before each further hop. */
+typedef struct msw_exchange_desc {
+  int32_t num_entries;
+  const int32_t* peer;       /* [num_entries] peer rank */
+  const int32_t* scale;      /* [num_entries] scale of the entry */
+  const int64_t* recv_ptr;   /* [num_entries + 1] offsets into recv_rows */
+  const int32_t* recv_rows;
+  const int64_t* send_ptr;   /* [num_entries + 1] offsets into send_rows */
+  const int32_t* send_rows;
+} msw_exchange_desc;
+
 /* Build CSR-by-destination per scale, pooling/unpooling maps, pack the weights for
  * the gfx950 kernels, allocate workspaces.  Host-synchronous; call once per graph. */
 int msw_plan_create(const msw_graph_desc* graph, const msw_model_desc* model, int device,
                     msw_plan** out_plan);
 int msw_plan_destroy(msw_plan* plan);
+
+/* msw_plan_create for one rank of a partitioned mesh: `xch` describes its halo exchange
+ * (hop pairs are not used: their halo is two rings deep).  The exchange itself runs either
+ * over RCCL (msw_plan_set_comm, one process per GPU, inside msw_rollout; eager launches
+ * unless MSW_PART_GRAPH=1 asks for graph capture) or between plans of one process
+ * (msw_group_rollout, validation on one GPU). */
+int msw_plan_create_part(const msw_graph_desc* graph, const msw_model_desc* model, int device,
+                         const msw_exchange_desc* xch, int32_t rank, msw_plan** out_plan);
+
+/* RCCL transport.  msw_comm_unique_id writes an ncclUniqueId (128 bytes) on the rank that
+ * creates it; every rank then calls msw_plan_set_comm with the same bytes.  RCCL is bound
+ * at run time from the process (the copy PyTorch loaded) or librccl.so.1. */
+int msw_comm_unique_id(char* uid128);
+int msw_plan_set_comm(msw_plan* plan, const char* uid128, int32_t nranks, int32_t rank);
+
+/* All ranks' plans of one partitioned mesh in ONE process, stepped in lockstep with the
+ * halo exchange done by device copies between the plans (no RCCL): validates the
+ * decomposition on a single GPU.  Per-plan arrays: x0, bc, bc_tstride, node_bc, n_bc, out
+ * as msw_rollout takes them. */
+int msw_group_rollout(msw_plan* const* plans, int32_t num_plans, const float* const* x0,
+                      const float* const* bc, const int32_t* bc_tstride,
+                      const int32_t* const* node_bc, const int32_t* n_bc, int32_t type_bc,
+                      int32_t T, float* const* out, void* stream);
 
 /* One forward (MSGNN.forward / GNN.forward): x [N][num_node_features] -> y [N][2].
  * Does not modify x.  Equivalent to models/gnn.py:267-350 (MSGNN) or :102-152 (GNN). */

@@ -247,6 +247,8 @@ int set_error(int code, const char* msg);
 hipError_t launch_set_slots(const SlotArgs& a, hipStream_t st);
 hipError_t launch_set_io(RolloutIO* dst, const RolloutIO& v, hipStream_t st);
 hipError_t launch_init_state(const InitArgs& a, hipStream_t st);
+hipError_t launch_copy_rows(const float* src, const int* srows, float* dst, const int* drows, int n, int width,
+                            hipStream_t st);
 
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
 template <int NT> hipError_t prepare_kernels();

@@ -31,6 +31,29 @@ __global__ void k_set_io(RolloutIO* dst, RolloutIO v) {
   if (threadIdx.x == 0) *dst = v;
 }
 
+// Halo exchange row moves: dst[drow(i)] = src[srow(i)] for i < n, rows of `width` floats
+// (multiple of 4); a null index array is the identity (contiguous staging buffer).
+__global__ __launch_bounds__(kBlock) void k_copy_rows(const float* __restrict__ src, const int* __restrict__ srows,
+                                                      float* __restrict__ dst, const int* __restrict__ drows,
+                                                      int n, int width) {
+  const int w4 = width / 4;
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)n * w4) return;
+  const int r = (int)(i / w4), c = (int)(i % w4) * 4;
+  const size_t s = (size_t)(srows ? srows[r] : r) * width + c;
+  const size_t d = (size_t)(drows ? drows[r] : r) * width + c;
+  *reinterpret_cast<float4*>(dst + d) = *reinterpret_cast<const float4*>(src + s);
+}
+
+hipError_t launch_copy_rows(const float* src, const int* srows, float* dst, const int* drows, int n, int width,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const long total = (long)n * (width / 4);
+  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, src, srows,
+                     dst, drows, n, width);
+  return hipGetLastError();
+}
+
 hipError_t launch_init_state(const InitArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_init_state, dim3(cdiv(a.N > 0 ? a.N : 1, kBlock)), dim3(kBlock), 0, st, a);
   return hipGetLastError();

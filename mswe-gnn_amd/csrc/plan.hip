@@ -9,6 +9,9 @@
 //   update_batch_multiscale training/train.py:31-65 (batched node_ptr layout)
 #include <cmath>
 #include <cstdio>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -222,9 +225,55 @@ struct Proc {                   // one SWEGNN layer bound to a scale (or an intr
   int par = 0;                  // buffer set (execution index & 1)
 };
 
+// RCCL, bound at run time: the copy already in the process (PyTorch's) or librccl.so.1.
+struct RcclApi {
+  ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*groupStart)() = nullptr;
+  ncclResult_t (*groupEnd)() = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*errStr)(ncclResult_t) = nullptr;
+  bool ok = false;
+};
+static RcclApi& rccl() {
+  static RcclApi api = [] {
+    RcclApi a;
+    void* h = RTLD_DEFAULT;
+    if (!dlsym(h, "ncclSend")) {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) return a;
+    }
+    a.getUniqueId = (decltype(a.getUniqueId))dlsym(h, "ncclGetUniqueId");
+    a.commInitRank = (decltype(a.commInitRank))dlsym(h, "ncclCommInitRank");
+    a.commDestroy = (decltype(a.commDestroy))dlsym(h, "ncclCommDestroy");
+    a.groupStart = (decltype(a.groupStart))dlsym(h, "ncclGroupStart");
+    a.groupEnd = (decltype(a.groupEnd))dlsym(h, "ncclGroupEnd");
+    a.send = (decltype(a.send))dlsym(h, "ncclSend");
+    a.recv = (decltype(a.recv))dlsym(h, "ncclRecv");
+    a.errStr = (decltype(a.errStr))dlsym(h, "ncclGetErrorString");
+    a.ok = a.getUniqueId && a.commInitRank && a.commDestroy && a.groupStart && a.groupEnd && a.send &&
+           a.recv && a.errStr;
+    return a;
+  }();
+  return api;
+}
+
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOP2 };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOP2, L_EXCHANGE };
+
+// Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
+// refresh the halo rows of up to two of the plan's buffers on one scale.
+enum BufId { B_U0, B_U1, B_O0, B_O1, B_T0, B_T1 };
+struct ExchangeArgs {
+  Common c;
+  int scale;
+  int nbuf;
+  int buf[2];    // BufId
+  int width[2];  // floats per row
+};
 struct Launch {
   int kind;
   int scale;                    // destination scale (bench hook)
@@ -234,6 +283,7 @@ struct Launch {
     HopArgs hop;
     PoolArgs pool;
     Hop2Args hop2;
+    ExchangeArgs xch;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
   Common& common() {
@@ -242,6 +292,7 @@ struct Launch {
       case L_EDGE_HOP: return eh.c;
       case L_HOP: return hop.c;
       case L_HOP2: return hop2.c;
+      case L_EXCHANGE: return xch.c;
       default: return pool.c;
     }
   }
@@ -283,11 +334,25 @@ struct msw_plan {
   std::vector<Launch> sched_fwd, sched_roll;  // one forward step: forward / rollout mode
   int use_graph = 1;
   int hop_pairs = 1;  // fuse hop pairs (MSW_NO_HOP_PAIRS=1 disables, for A/B measurements)
+  // partitioned mesh (msw_plan_create_part): per scale, the halo rows received from / the
+  // owned rows sent to each peer (internal rows, concatenated in peer order)
+  struct XchPeer { int peer, roff, rcount, soff, scount; };
+  struct XchScale {
+    int nrecv = 0, nsend = 0;
+    int* recv_rows = nullptr;
+    int* send_rows = nullptr;
+    std::vector<XchPeer> peers;
+  };
+  int part_rank = -1;
+  std::vector<XchScale> xch;
+  ncclComm_t comm = nullptr;
+  float *xsend = nullptr, *xrecv = nullptr;
   hipStream_t cap_stream = nullptr;
   hipGraphExec_t step_exec = nullptr;
   std::vector<void*> owned;
   ~msw_plan() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
+    if (comm && rccl().ok) (void)rccl().commDestroy(comm);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (void* q : owned) (void)hipFree(q);
   }
@@ -423,9 +488,26 @@ DecDesc dec_of(msw_plan* P, const float* x_src, bool rollout, float* y) {
 
 // One SWEGNN layer on its scale: fused edge-MLP + hop 1, then hops 2..K; the last hop
 // runs `epi` (and stores its output to `out` if non-null).  out_0 is in O[par].
+// Partitioned mesh: refresh the halo rows of `bufs` on `scale` before a gathering launch.
+void sched_exchange(msw_plan* P, std::vector<Launch>& q, int scale, std::initializer_list<std::pair<int, int>> bufs) {
+  if (P->xch.empty() || P->xch[scale].peers.empty()) return;
+  Launch L;
+  L.kind = L_EXCHANGE;
+  L.scale = scale;
+  L.xch.c = common_of(P);
+  L.xch.scale = scale;
+  for (auto& b : bufs) {
+    L.xch.buf[L.xch.nbuf] = b.first;
+    L.xch.width[L.xch.nbuf] = b.second;
+    ++L.xch.nbuf;
+  }
+  q.push_back(L);
+}
+
 void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi) {
   const ScaleCSR& g = P->sc[pr.scale];
   const Common c = common_of(P);
+  sched_exchange(P, q, pr.scale, {{pr.par ? B_U1 : B_U0, 16 * pr.h1t}, {pr.par ? B_O1 : B_O0, P->F}});
   Launch L1;
   L1.kind = L_EDGE_HOP;
   L1.scale = pr.scale;
@@ -444,6 +526,7 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   q.push_back(L1);
   const float* cur = P->T[0];
   for (int k = 2; k <= pr.K; ++k) {
+    sched_exchange(P, q, pr.scale, {{cur == P->T[0] ? B_T0 : B_T1, P->F}});
     if (g.pair_ok && k + 1 < pr.K) {  // hops k, k+1 in one launch (neither is the last)
       float* nxt = cur == P->T[0] ? P->T[1] : P->T[0];
       Launch L;
@@ -656,8 +739,8 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       if (a.last) rl.epi(R, a.epi);
       a.reg = R.done(split);
       reg = &a.reg;
-    } else if (L.kind == L_HOP2) {
-      continue;  // filters from the blob, no LDS weight region
+    } else if (L.kind == L_HOP2 || L.kind == L_EXCHANGE) {
+      continue;  // no LDS weight region
     } else if (L.kind == L_HOP) {
       HopArgs& a = L.hop;
       if (!a.last) continue;  // middle hops load their filter from the blob (k_hop<.., false>)
@@ -703,6 +786,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
     case L_HOP2:
       L.hop2.max_blocks = resident_of(P->NT, 4, 0, 0, (size_t)L.hop2.bmax * (16 * P->NT + 4) * 4, 0);
       break;
+    case L_EXCHANGE: break;
     default: caps(P, L.pool, 3, 0, 0, L.pool.reg.len); break;
   }
 }
@@ -714,13 +798,57 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
     case L_HOP2: return launch_hop2<NT>(L.hop2, st);
-    default: return launch_pool<NT>(L.pool, st);
+    case L_POOL: return launch_pool<NT>(L.pool, st);
+    default: return hipErrorInvalidValue;  // exchanges are run by run_schedule / the group driver
   }
+}
+
+float* buf_of(msw_plan* P, int id) {
+  switch (id) {
+    case B_U0: return P->U[0];
+    case B_U1: return P->U[1];
+    case B_O0: return P->O[0];
+    case B_O1: return P->O[1];
+    case B_T0: return P->T[0];
+    default: return P->T[1];
+  }
+}
+
+// RCCL transport: pack the rows every peer needs into one staging buffer, one grouped
+// send/recv per peer, unpack into the halo rows.  Stream-ordered (capturable).
+int rccl_exchange(msw_plan* P, const ExchangeArgs& a, hipStream_t st) {
+  const msw_plan::XchScale& X = P->xch[a.scale];
+  if (!P->comm) return fail(MSW_ERR_INVALID, "partitioned plan without a transport (msw_plan_set_comm)");
+  RcclApi& r = rccl();
+  for (int b = 0; b < a.nbuf; ++b) {
+    float* buf = buf_of(P, a.buf[b]);
+    const int w = a.width[b];
+    HIP_TRY(launch_copy_rows(buf, X.send_rows, P->xsend, nullptr, X.nsend, w, st));
+    ncclResult_t e = r.groupStart();
+    for (const auto& pe : X.peers) {
+      if (e == ncclSuccess && pe.scount > 0)
+        e = r.send(P->xsend + (size_t)pe.soff * w, (size_t)pe.scount * w, ncclFloat32, pe.peer, P->comm, st);
+      if (e == ncclSuccess && pe.rcount > 0)
+        e = r.recv(P->xrecv + (size_t)pe.roff * w, (size_t)pe.rcount * w, ncclFloat32, pe.peer, P->comm, st);
+    }
+    const ncclResult_t e2 = r.groupEnd();
+    if (e != ncclSuccess || e2 != ncclSuccess)
+      return fail(MSW_ERR_HIP, std::string("RCCL halo exchange: ") + r.errStr(e != ncclSuccess ? e : e2));
+    HIP_TRY(launch_copy_rows(P->xrecv, nullptr, buf, X.recv_rows, X.nrecv, w, st));
+  }
+  return MSW_OK;
 }
 
 template <int NT>
 int run_schedule(msw_plan* P, const std::vector<Launch>& q, hipStream_t st) {
-  for (const Launch& L : q) HIP_TRY(launch_one<NT>(L, st));
+  for (const Launch& L : q) {
+    if (L.kind == L_EXCHANGE) {
+      int rc = rccl_exchange(P, L.xch, st);
+      if (rc) return rc;
+    } else {
+      HIP_TRY(launch_one<NT>(L, st));
+    }
+  }
   P->kernels_per_step = (int)q.size();
   return MSW_OK;
 }
@@ -989,13 +1117,60 @@ int64_t msw_struct_size(const char* name) {
   if (!strcmp(name, "msw_model_desc")) return sizeof(msw_model_desc);
   if (!strcmp(name, "msw_graph_desc")) return sizeof(msw_graph_desc);
   if (!strcmp(name, "msw_plan_stats")) return sizeof(msw_plan_stats);
+  if (!strcmp(name, "msw_exchange_desc")) return sizeof(msw_exchange_desc);
   return -1;
 }
 
 int msw_abi_version(void) { return MSW_ABI_VERSION; }
 
-int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device,
-                    msw_plan** out_plan) {
+}  // extern "C"
+
+namespace {
+
+// Partitioned mesh: per-scale receive / send row lists (local graph rows -> internal rows).
+int build_exchange(msw_plan* P, const msw_exchange_desc* d) {
+  P->xch.assign(P->S, msw_plan::XchScale{});
+  std::vector<std::vector<int>> rr(P->S), ss(P->S);
+  for (int i = 0; i < d->num_entries; ++i) {
+    const int s = d->scale[i];
+    if (s < 0 || s >= P->S) return fail(MSW_ERR_INVALID, "exchange entry with a bad scale");
+    const ScaleCSR& c = P->sc[s];
+    msw_plan::XchPeer pe{d->peer[i], (int)rr[s].size(), (int)(d->recv_ptr[i + 1] - d->recv_ptr[i]),
+                         (int)ss[s].size(), (int)(d->send_ptr[i + 1] - d->send_ptr[i])};
+    if (pe.peer < 0 || pe.peer == P->part_rank) return fail(MSW_ERR_INVALID, "exchange entry with a bad peer");
+    auto conv = [&](const int32_t* rows, int64_t a, int64_t b, std::vector<int>& dst) -> int {
+      for (int64_t k = a; k < b; ++k) {
+        const int r = rows[k];
+        if (r < 0 || r >= P->N) return fail(MSW_ERR_INVALID, "exchange row out of range");
+        const int in = P->iperm[r];
+        if (in < c.n0 || in >= c.n0 + c.ns) return fail(MSW_ERR_INVALID, "exchange row not on the entry's scale");
+        dst.push_back(in);
+      }
+      return MSW_OK;
+    };
+    int rc;
+    if ((rc = conv(d->recv_rows, d->recv_ptr[i], d->recv_ptr[i + 1], rr[s])) ||
+        (rc = conv(d->send_rows, d->send_ptr[i], d->send_ptr[i + 1], ss[s])))
+      return rc;
+    P->xch[s].peers.push_back(pe);
+  }
+  size_t most = 1;
+  for (int s = 0; s < P->S; ++s) {
+    msw_plan::XchScale& X = P->xch[s];
+    X.nrecv = (int)rr[s].size();
+    X.nsend = (int)ss[s].size();
+    int rc;
+    if ((rc = pupload(P, &X.recv_rows, rr[s])) || (rc = pupload(P, &X.send_rows, ss[s]))) return rc;
+    most = std::max(most, (size_t)std::max(X.nrecv, X.nsend));
+  }
+  const size_t floats = most * 2 * P->F;  // widest exchanged row: U (2F)
+  int rc;
+  if ((rc = palloc(P, &P->xsend, floats)) || (rc = palloc(P, &P->xrecv, floats))) return rc;
+  return MSW_OK;
+}
+
+int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int device,
+                     const msw_exchange_desc* xch, int rank, msw_plan** out_plan) {
   if (!g || !m || !out_plan) return fail(MSW_ERR_INVALID, "null argument");
   *out_plan = nullptr;
   if (m->model_type != 0 && m->model_type != 1) return fail(MSW_ERR_INVALID, "model_type must be 0 (MSGNN) or 1 (GNN)");
@@ -1026,9 +1201,11 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     return fail(MSW_ERR_INVALID, "MSGNN needs S-1 intra-scale layers");
   if (m->model_type == 1 && m->num_processors < 1) return fail(MSW_ERR_INVALID, "GNN needs >= 1 layer");
 
-  P->hop_pairs = getenv("MSW_NO_HOP_PAIRS") ? 0 : 1;
+  P->hop_pairs = getenv("MSW_NO_HOP_PAIRS") || xch ? 0 : 1;  // a pair's halo is two rings deep
+  P->part_rank = xch ? rank : -1;
   int rc = build_graph_plan(P.get(), g);
   if (rc) return rc;
+  if (xch && (rc = build_exchange(P.get(), xch))) return rc;
   const int F = P->F, Npad = P->Npad;
 
   // ---- weights
@@ -1183,7 +1360,176 @@ int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device
     if (enc_d) HIP_TRY(hipFree(enc_d));
   }
   HIP_TRY(hipDeviceSynchronize());
+  if (xch) P->use_graph = getenv("MSW_PART_GRAPH") ? 1 : 0;  // exchanges run eagerly by default
   *out_plan = P.release();
+  return MSW_OK;
+}
+
+// BC slots (internal rows), the device I/O record and the initial state of a rollout, set
+// by kernels whose arguments carry the values: no host buffer lifetime issue, no host sync.
+int rollout_prologue(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstride,
+                     const int32_t* node_bc, int32_t n_bc, int32_t type_bc, int32_t T, float* out,
+                     hipStream_t st) {
+  if (!P || !x0 || !out) return fail(MSW_ERR_INVALID, "null argument");
+  if (n_bc > 0 && (!bc || !node_bc)) return fail(MSW_ERR_INVALID, "BC arrays missing");
+  if (n_bc > 0 && bc_tstride < T) return fail(MSW_ERR_INVALID, "BC has fewer time entries than T");
+  if (type_bc != 1 && type_bc != 2) return fail(MSW_ERR_INVALID, "type_BC must be 1 or 2 (dataset.py:499-506)");
+  HIP_TRY(hipSetDevice(P->device));
+  std::vector<int> rows;
+  for (int b = 0; b < n_bc; ++b) {
+    if (node_bc[b] < 0 || node_bc[b] >= P->N) return fail(MSW_ERR_INVALID, "node_BC out of range");
+    rows.push_back(P->iperm[node_bc[b]]);
+  }
+  if (rows != P->bc_rows_set) {
+    for (size_t i = 0; i < P->bc_rows_set.size(); i += kSlotBatch) {
+      SlotArgs sa{};
+      sa.slot = P->bc_slot_d;
+      sa.n = (int)std::min(P->bc_rows_set.size() - i, (size_t)kSlotBatch);
+      for (int k = 0; k < sa.n; ++k) { sa.row[k] = P->bc_rows_set[i + k]; sa.val[k] = -1; }
+      HIP_TRY(launch_set_slots(sa, st));
+    }
+    for (size_t i = 0; i < rows.size(); i += kSlotBatch) {
+      SlotArgs sa{};
+      sa.slot = P->bc_slot_d;
+      sa.n = (int)std::min(rows.size() - i, (size_t)kSlotBatch);
+      for (int k = 0; k < sa.n; ++k) { sa.row[k] = rows[i + k]; sa.val[k] = (int)(i + k); }
+      HIP_TRY(launch_set_slots(sa, st));
+    }
+    P->bc_rows_set = rows;
+  }
+  RolloutIO io{};
+  io.bc = bc; io.out = out; io.bc_tstride = bc_tstride; io.type_bc = type_bc; io.T = T; io.step = -1;
+  HIP_TRY(launch_set_io(P->io_d, io, st));
+  InitArgs ia{};
+  ia.x0 = x0; ia.perm = P->perm_d; ia.N = P->Npad; ia.nnf = P->nnf;
+  ia.dyn = P->dyn; ia.p = P->p; ia.X = P->X; ia.io = P->io_d; ia.bc_slot = P->bc_slot_d;
+  HIP_TRY(launch_init_state(ia, st));
+  return MSW_OK;
+}
+
+// In-process transport (msw_group_rollout): halo rows of plan k's buffer gathered straight
+// from the owning plans' buffers, using each owner's send list for k.
+int loopback_exchange(msw_plan* const* plans, int k, const ExchangeArgs& a, hipStream_t st) {
+  msw_plan* P = plans[k];
+  const msw_plan::XchScale& X = P->xch[a.scale];
+  for (const auto& pe : X.peers) {
+    if (pe.rcount == 0) continue;
+    msw_plan* Q = plans[pe.peer];
+    const msw_plan::XchScale& Y = Q->xch[a.scale];
+    const msw_plan::XchPeer* back = nullptr;
+    for (const auto& qe : Y.peers)
+      if (qe.peer == k) back = &qe;
+    if (!back || back->scount != pe.rcount)
+      return fail(MSW_ERR_INVALID, "exchange lists of plans " + std::to_string(k) + " and " +
+                                       std::to_string(pe.peer) + " disagree");
+    for (int b = 0; b < a.nbuf; ++b)
+      HIP_TRY(launch_copy_rows(buf_of(Q, a.buf[b]), Y.send_rows + back->soff, buf_of(P, a.buf[b]),
+                               X.recv_rows + pe.roff, pe.rcount, a.width[b], st));
+  }
+  return MSW_OK;
+}
+
+template <int NT>
+int group_step(msw_plan* const* plans, int n, hipStream_t st) {
+  const size_t L = plans[0]->sched_roll.size();
+  for (size_t i = 0; i < L; ++i)
+    for (int k = 0; k < n; ++k) {
+      const Launch& l = plans[k]->sched_roll[i];
+      if (l.kind == L_EXCHANGE) {
+        int rc = loopback_exchange(plans, k, l.xch, st);
+        if (rc) return rc;
+      } else {
+        HIP_TRY(launch_one<NT>(l, st));
+      }
+    }
+  return MSW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msw_plan_create(const msw_graph_desc* g, const msw_model_desc* m, int device, msw_plan** out_plan) {
+  return plan_create_impl(g, m, device, nullptr, -1, out_plan);
+}
+
+int msw_plan_create_part(const msw_graph_desc* g, const msw_model_desc* m, int device,
+                         const msw_exchange_desc* xch, int32_t rank, msw_plan** out_plan) {
+  if (!xch || rank < 0) return fail(MSW_ERR_INVALID, "exchange descriptor missing or rank < 0");
+  if (xch->num_entries < 0 || (xch->num_entries > 0 && (!xch->peer || !xch->scale || !xch->recv_ptr ||
+                                                         !xch->send_ptr)))
+    return fail(MSW_ERR_INVALID, "exchange descriptor arrays missing");
+  return plan_create_impl(g, m, device, xch, rank, out_plan);
+}
+
+int msw_comm_unique_id(char* uid128) {
+  if (!uid128) return fail(MSW_ERR_INVALID, "null argument");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  if (!rccl().ok) return fail(MSW_ERR_UNSUPPORTED, "RCCL not found in the process nor as librccl.so.1");
+  ncclUniqueId id;
+  const ncclResult_t e = rccl().getUniqueId(&id);
+  if (e != ncclSuccess) return fail(MSW_ERR_HIP, std::string("ncclGetUniqueId: ") + rccl().errStr(e));
+  memcpy(uid128, &id, sizeof(id));
+  return MSW_OK;
+}
+
+int msw_plan_set_comm(msw_plan* P, const char* uid128, int32_t nranks, int32_t rank) {
+  if (!P || !uid128) return fail(MSW_ERR_INVALID, "null argument");
+  if (P->part_rank < 0) return fail(MSW_ERR_INVALID, "plan is not partitioned (msw_plan_create_part)");
+  if (rank != P->part_rank || nranks <= rank) return fail(MSW_ERR_INVALID, "rank does not match the plan's part");
+  if (!rccl().ok) return fail(MSW_ERR_UNSUPPORTED, "RCCL not found in the process nor as librccl.so.1");
+  HIP_TRY(hipSetDevice(P->device));
+  if (P->comm) {
+    (void)rccl().commDestroy(P->comm);
+    P->comm = nullptr;
+  }
+  ncclUniqueId id;
+  memcpy(&id, uid128, sizeof(id));
+  const ncclResult_t e = rccl().commInitRank(&P->comm, nranks, id, rank);
+  if (e != ncclSuccess) {
+    P->comm = nullptr;
+    return fail(MSW_ERR_HIP, std::string("ncclCommInitRank: ") + rccl().errStr(e));
+  }
+  return MSW_OK;
+}
+
+int msw_group_rollout(msw_plan* const* plans, int32_t num_plans, const float* const* x0,
+                      const float* const* bc, const int32_t* bc_tstride, const int32_t* const* node_bc,
+                      const int32_t* n_bc, int32_t type_bc, int32_t T, float* const* out, void* stream) {
+  if (!plans || num_plans <= 0 || !x0 || !bc || !bc_tstride || !node_bc || !n_bc || !out)
+    return fail(MSW_ERR_INVALID, "null argument");
+  if (T < 0) return fail(MSW_ERR_INVALID, "T < 0");
+  const msw_plan* P0 = plans[0];
+  for (int k = 0; k < num_plans; ++k) {
+    const msw_plan* P = plans[k];
+    if (!P) return fail(MSW_ERR_INVALID, "null plan");
+    if (P->part_rank != k) return fail(MSW_ERR_INVALID, "plans[k] must be the plan of part k");
+    if (P->device != P0->device || P->NT != P0->NT) return fail(MSW_ERR_INVALID, "plans on different devices / widths");
+    if (P->sched_roll.size() != P0->sched_roll.size())
+      return fail(MSW_ERR_INVALID, "plans with different step schedules");
+    for (size_t i = 0; i < P->sched_roll.size(); ++i)
+      if (P->sched_roll[i].kind != P0->sched_roll[i].kind)
+        return fail(MSW_ERR_INVALID, "plans with different step schedules");
+    for (const auto& X : P->xch)
+      for (const auto& pe : X.peers)
+        if (pe.peer >= num_plans) return fail(MSW_ERR_INVALID, "exchange peer outside the group");
+  }
+  if (T == 0) return MSW_OK;
+  hipStream_t st = (hipStream_t)stream;
+  for (int k = 0; k < num_plans; ++k) {
+    int rc = rollout_prologue(plans[k], x0[k], bc[k], bc_tstride[k], node_bc[k], n_bc[k], type_bc, T, out[k], st);
+    if (rc) return rc;
+  }
+  for (int t = 0; t < T; ++t) {
+    int rc = P0->NT == 1 ? group_step<1>(plans, num_plans, st)
+           : P0->NT == 2 ? group_step<2>(plans, num_plans, st)
+                         : group_step<4>(plans, num_plans, st);
+    if (rc) return rc;
+  }
+  for (int k = 0; k < num_plans; ++k) {
+    plans[k]->rollout_steps += T;
+    plans[k]->forward_calls += T;
+  }
   return MSW_OK;
 }
 
@@ -1217,42 +1563,9 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
   if (!P || !x0 || (!out && T > 0)) return fail(MSW_ERR_INVALID, "null argument");
   if (T < 0) return fail(MSW_ERR_INVALID, "T < 0");
   if (T == 0) return MSW_OK;
-  if (n_bc > 0 && (!bc || !node_bc)) return fail(MSW_ERR_INVALID, "BC arrays missing");
-  if (n_bc > 0 && bc_tstride < T) return fail(MSW_ERR_INVALID, "BC has fewer time entries than T");
-  if (type_bc != 1 && type_bc != 2) return fail(MSW_ERR_INVALID, "type_BC must be 1 or 2 (dataset.py:499-506)");
-  HIP_TRY(hipSetDevice(P->device));
   hipStream_t st = (hipStream_t)stream;
-  // BC slots (internal rows) and the device I/O record, set by kernels whose arguments
-  // carry the values: no host buffer lifetime issue and no host synchronisation.
-  std::vector<int> rows;
-  for (int b = 0; b < n_bc; ++b) {
-    if (node_bc[b] < 0 || node_bc[b] >= P->N) return fail(MSW_ERR_INVALID, "node_BC out of range");
-    rows.push_back(P->iperm[node_bc[b]]);
-  }
-  if (rows != P->bc_rows_set) {
-    for (size_t i = 0; i < P->bc_rows_set.size(); i += kSlotBatch) {
-      SlotArgs sa{};
-      sa.slot = P->bc_slot_d;
-      sa.n = (int)std::min(P->bc_rows_set.size() - i, (size_t)kSlotBatch);
-      for (int k = 0; k < sa.n; ++k) { sa.row[k] = P->bc_rows_set[i + k]; sa.val[k] = -1; }
-      HIP_TRY(launch_set_slots(sa, st));
-    }
-    for (size_t i = 0; i < rows.size(); i += kSlotBatch) {
-      SlotArgs sa{};
-      sa.slot = P->bc_slot_d;
-      sa.n = (int)std::min(rows.size() - i, (size_t)kSlotBatch);
-      for (int k = 0; k < sa.n; ++k) { sa.row[k] = rows[i + k]; sa.val[k] = (int)(i + k); }
-      HIP_TRY(launch_set_slots(sa, st));
-    }
-    P->bc_rows_set = rows;
-  }
-  RolloutIO io{};
-  io.bc = bc; io.out = out; io.bc_tstride = bc_tstride; io.type_bc = type_bc; io.T = T; io.step = -1;
-  HIP_TRY(launch_set_io(P->io_d, io, st));
-  InitArgs ia{};
-  ia.x0 = x0; ia.perm = P->perm_d; ia.N = P->Npad; ia.nnf = P->nnf;
-  ia.dyn = P->dyn; ia.p = P->p; ia.X = P->X; ia.io = P->io_d; ia.bc_slot = P->bc_slot_d;
-  HIP_TRY(launch_init_state(ia, st));
+  int prc = rollout_prologue(P, x0, bc, bc_tstride, node_bc, n_bc, type_bc, T, out, st);
+  if (prc) return prc;
   if (P->use_graph) {
     if (!P->step_exec) {
       if (!P->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&P->cap_stream, hipStreamNonBlocking));

@@ -72,6 +72,12 @@ class MswPlanStats(C.Structure):
                 ("graph_captured", C.c_int32)]
 
 
+class MswExchangeDesc(C.Structure):
+    _fields_ = [("num_entries", C.c_int32), ("peer", c_int32_p), ("scale", c_int32_p),
+                ("recv_ptr", c_int64_p), ("recv_rows", c_int32_p),
+                ("send_ptr", c_int64_p), ("send_rows", c_int32_p)]
+
+
 # (name, restype, argtypes) of every entry point declared in include/mswegnn.h
 SYMBOLS = [
     ("msw_plan_create", C.c_int, [C.POINTER(MswGraphDesc), C.POINTER(MswModelDesc), C.c_int,
@@ -91,11 +97,18 @@ SYMBOLS = [
     ("msw_set_trace", C.c_int, [C.c_void_p, C.c_void_p]),
     ("msw_rollout_metrics", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, c_int64_p, C.c_int32,
                                       c_float_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("msw_plan_create_part", C.c_int, [C.POINTER(MswGraphDesc), C.POINTER(MswModelDesc), C.c_int,
+                                       C.POINTER(MswExchangeDesc), C.c_int32, C.POINTER(C.c_void_p)]),
+    ("msw_comm_unique_id", C.c_int, [C.c_char_p]),
+    ("msw_plan_set_comm", C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32]),
+    ("msw_group_rollout", C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
+                                    C.POINTER(C.c_void_p), c_int32_p, C.POINTER(c_int32_p), c_int32_p,
+                                    C.c_int32, C.c_int32, C.POINTER(C.c_void_p), C.c_void_p]),
 ]
 
 STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,
            "msw_model_desc": MswModelDesc, "msw_graph_desc": MswGraphDesc,
-           "msw_plan_stats": MswPlanStats}
+           "msw_plan_stats": MswPlanStats, "msw_exchange_desc": MswExchangeDesc}
 
 _lib = None
 

@@ -174,7 +174,9 @@ def describe_graph(model, graph):
 class EnginePlan:
     """An msw_plan: the graph (CSR per scale, pooling maps) and packed weights on one GPU."""
 
-    def __init__(self, model, graph, device):
+    def __init__(self, model, graph, device, exchange=None, rank=-1):
+        """exchange: an L.MswExchangeDesc (mswegnn/partition.py) -> the plan of part `rank`
+        of a partitioned mesh (msw_plan_create_part)."""
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("the HIP engine needs a GPU device")
@@ -184,7 +186,12 @@ class EnginePlan:
         gd, k2 = describe_graph(model, graph)
         h = C.c_void_p()
         lib = L.lib()
-        L.check(lib.msw_plan_create(C.byref(gd), C.byref(md), self.device.index or 0, C.byref(h)))
+        dev = self.device.index or 0
+        if exchange is None:
+            L.check(lib.msw_plan_create(C.byref(gd), C.byref(md), dev, C.byref(h)))
+        else:
+            L.check(lib.msw_plan_create_part(C.byref(gd), C.byref(md), dev, C.byref(exchange), int(rank),
+                                             C.byref(h)))
         self._h = h
         del k1, k2
 

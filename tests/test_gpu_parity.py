@@ -225,3 +225,31 @@ def test_rollout_metrics_kernel_vs_reference(cuda):
     m2 = rollout_metrics(p2, r2, [(0, n0), (n0, 2 * n0)], thresholds=(0.05,))
     assert rel_err(m2["rmse"].cpu(), fx["loss_RMSE_stack"]) <= 1e-5
     np.testing.assert_allclose(m2["csi"][0.05].cpu().numpy(), fx["csi_0.05_stack"], rtol=1e-6, equal_nan=True)
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_partitioned_rollout_matches_whole_mesh(cuda, parts):
+    """One mesh split over `parts` plans (mswegnn/partition.py) stepped in
+    lockstep with halo exchanges (msw_group_rollout) == the undivided rollout (and the
+    reference fixture), owned rows assembled back to graph numbering."""
+    from mswegnn.partition import PartitionedRollout
+    fx = golden("fx_small_K4_F32_rollout48")
+    g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    whole = m.rollout(g).cpu()
+    pr = PartitionedRollout(m, g, parts, cuda)
+    r = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, 48).cpu()
+    torch.cuda.synchronize()
+    assert per_step_rel(r, whole) <= REL_TOL, per_step_rel(r, whole)
+    assert per_step_rel(r, torch.from_numpy(fx["rollout"])) <= REL_TOL
+    for pl in pr.plans:
+        assert pl.stats()["rollout_steps"] >= 48
+    # wet start, single-scale GNN as well
+    gw = wet_state(make_multiscale_mesh(**mesh_config("small3"), T=6), seed=3).to(cuda)
+    m3 = _hip(build_msgnn(3, 32, 4, state=weights("msgnn3_F32_seed666")), cuda)
+    r3 = PartitionedRollout(m3, gw, parts, cuda).rollout(gw.x, gw.BC, gw.node_BC, gw.type_BC, 6).cpu()
+    assert per_step_rel(r3, torch.from_numpy(golden("fx_small3_msgnn3_wet")["rollout"])) <= REL_TOL
+    gs = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=10), seed=2).to(cuda)
+    mg = _hip(build_gnn(state=weights("gnn_F32_seed42")), cuda)
+    rg = PartitionedRollout(mg, gs, parts, cuda).rollout(gs.x, gs.BC, gs.node_BC, gs.type_BC, 10).cpu()
+    assert per_step_rel(rg, torch.from_numpy(golden("fx_gnn_small_rollout10")["rollout"])) <= REL_TOL

@@ -208,3 +208,142 @@ def test_metrics_oracle_matches_reference_fixture():
     p2, r2 = torch.stack([pred, real.flip(-1)]), torch.stack([real, pred])
     assert torch.equal(mr.rollout_loss(p2, r2, "RMSE"), torch.from_numpy(fx["loss_RMSE_stack"]))
     np.testing.assert_array_equal(mr.csi(p2, r2, 0.05).numpy(), fx["csi_0.05_stack"])
+
+
+# ------------------------------------------------------------------ single-mesh decomposition
+def _hops_part(lp, xl, exchange, hops):
+    """`hops` rounds of y[dst] += w_e * x[src] over the part's local edges, the halo refreshed
+    by `exchange` before every round and poisoned (NaN) after it, as the engine's hop chain
+    runs (mswegnn/partition.py): an owned row reached by a stale halo row turns NaN."""
+    ei = lp.graph.edge_index.numpy()
+    w = lp.graph.edge_attr.reshape(ei.shape[1], -1)[:, 0].double().numpy()
+    halo = ~lp.owned
+    for _ in range(hops):
+        exchange(xl)
+        y = np.zeros_like(xl)
+        np.add.at(y, ei[1], w[:, None] * xl[ei[0]])
+        y[halo] = np.nan
+        xl[:] = y
+    return xl
+
+
+def _hops_global(g, x, hops):
+    ei = g.edge_index.numpy()
+    w = g.edge_attr.reshape(ei.shape[1], -1)[:, 0].double().numpy()
+    for _ in range(hops):
+        y = np.zeros_like(x)
+        np.add.at(y, ei[1], w[:, None] * x[ei[0]])
+        x = y
+    return x
+
+
+@pytest.mark.parametrize("parts", [2, 3, 5])
+def test_partition_invariants_and_halo_exchange(parts):
+    from mswegnn import partition as P
+    g = make_multiscale_mesh(**mesh_config("small"), T=4)
+    owner, lps, xp = P.decompose(g, parts)
+    npt = g.node_ptr.numpy()
+    N = int(npt[-1])
+    ii = g.intra_mesh_edge_index.numpy()
+    # every node owned once; nested (a fine node lives with its parent); finest balanced
+    assert owner.min() == 0 and owner.max() == parts - 1
+    assert np.array_equal(owner[ii[1]], owner[ii[0]])
+    counts = np.bincount(owner[npt[0]:npt[1]], minlength=parts)
+    grain = -(-(npt[1] - npt[0]) // (npt[-1] - npt[-2]))  # finest cells under one coarsest cell
+    assert counts.max() - counts.min() <= 2 * grain, counts
+    seen = np.zeros(N, np.int64)
+    for lp in lps:
+        seen[lp.nodes[lp.owned]] += 1
+        # scales are contiguous and node_ptr agrees with scale_of
+        lnp = lp.graph.node_ptr.numpy()
+        for s in range(len(npt) - 1):
+            assert np.all(lp.scale_of[lnp[s]:lnp[s + 1]] == s)
+            assert np.all((lp.nodes[lnp[s]:lnp[s + 1]] >= npt[s]) & (lp.nodes[lnp[s]:lnp[s + 1]] < npt[s + 1]))
+        # in-edges of owned nodes: all of them, in reference order
+        ge = g.edge_index.numpy()
+        le = lp.nodes[lp.graph.edge_index.numpy()]
+        want = np.isin(ge[1], lp.nodes[lp.owned])
+        assert np.array_equal(le, ge[:, want])
+    assert np.all(seen == 1)
+    # exchange lists agree pairwise (counts and global ids)
+    for p in range(parts):
+        for s, peers in xp[p].items():
+            for q, (recv, send) in peers.items():
+                back_recv, back_send = xp[q][s][p]
+                assert np.array_equal(lps[p].nodes[recv], lps[q].nodes[back_send])
+                assert np.array_equal(lps[p].nodes[send], lps[q].nodes[back_recv])
+                assert np.all(owner[lps[p].nodes[recv]] == q) and np.all(lps[q].owned[back_send])
+    # 4 hops of message passing with a loopback exchange == the undivided mesh
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((N, 3))
+    ref = _hops_global(g, x.copy(), 4)
+    xls = [x[lp.nodes].copy() for lp in lps]
+
+    def loopback(p):
+        def ex(xl):
+            for s, peers in xp[p].items():
+                for q, (recv, _) in peers.items():
+                    if len(recv):
+                        xl[recv] = xls[q][xp[q][s][p][1]]
+        return ex
+    for h in range(4):  # lockstep, as msw_group_rollout runs the parts
+        for p, lp in enumerate(lps):
+            loopback(p)(xls[p])
+        for p, lp in enumerate(lps):
+            xls[p] = _hops_part(lp, xls[p], lambda xl: None, 1)
+    out = P.assemble(lps, [torch.from_numpy(a) for a in xls], N).numpy()
+    assert np.isfinite(out).all()
+    np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
+
+
+def _exchange_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from mswegnn import partition as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = make_multiscale_mesh(**mesh_config("small"), T=4)
+        owner, lps, xp = P.decompose(g, world)
+        N = g.num_nodes
+        x = np.random.default_rng(0).standard_normal((N, 3))
+        lp = lps[rank]
+
+        def ex(xl):  # the RCCL exchange's pattern: per scale, grouped send/recv per peer
+            for s in sorted(xp[rank]):
+                reqs, bufs = [], []
+                for q in sorted(xp[rank][s]):
+                    recv, send = xp[rank][s][q]
+                    if len(send):
+                        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(xl[send])), q))
+                    if len(recv):
+                        b = torch.empty(len(recv), xl.shape[1], dtype=torch.float64)
+                        reqs.append(dist.irecv(b, q))
+                        bufs.append((recv, b))
+                for r in reqs:
+                    r.wait()
+                for recv, b in bufs:
+                    xl[recv] = b.numpy()
+        out = _hops_part(lp, x[lp.nodes].copy(), ex, 4)
+        outs = [None] * world
+        dist.all_gather_object(outs, torch.from_numpy(out))
+        if rank == 0:
+            full = P.assemble(lps, outs, N).numpy()
+            q.put(float(np.abs(full - _hops_global(g, x.copy(), 4)).max()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_partition_halo_exchange_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    err = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert err <= 1e-12, err
