@@ -225,18 +225,20 @@ int msw_bench_kernel(msw_plan* plan, int32_t kernel, int32_t scale, int32_t iter
                      int64_t* units_out, void* stream);
 
 /* On-device rollout evaluation (the reference's test-time metrics, finest scale only;
- * utils/miscellaneous.py:123-199, training/loss.py:8-35).  pred, real: device [N][2][T]
- * (graph numbering, as msw_rollout writes them); fine_ranges: host int64 [num_sims][2],
- * the finest-scale row range of each simulation (node_ptr[g][0], node_ptr[g][1]);
- * thresholds: host float [n_thr] (n_thr <= 4) water-depth thresholds.
+ * utils/miscellaneous.py:116-199, training/loss.py:8-35,120-169).  pred, real: device
+ * [N][2][T] (graph numbering, as msw_rollout writes them); fine_ranges: host int64
+ * [num_sims][2], the finest-scale row range of each simulation (node_ptr[g][0],
+ * node_ptr[g][1]); thresholds: host float [n_thr] (n_thr <= 4) water-depth thresholds;
+ * area: device float [N] cell areas by graph row (data.area), or NULL.
  * Outputs (device, ZEROED by the caller, accumulated with atomics):
- *   sums   double [num_sims][T][9]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, the same four
- *          over rows with dh != 0 or dv != 0 (mask_on_water), that row count;
+ *   sums   double [num_sims][T][10]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, the same four
+ *          over rows with dh != 0 or dv != 0 (mask_on_water), that row count, and the
+ *          stored volume sum(area * h_pred) (0 when area is NULL);
  *   counts uint64 [num_sims][T][n_thr][4]: TP, TN, FP, FN of h_pred > thr vs h_real > thr.
  * Stream-ordered, no host synchronisation; needs no plan. */
 int msw_rollout_metrics(const float* pred, const float* real, int32_t T, const int64_t* fine_ranges,
-                        int32_t num_sims, const float* thresholds, int32_t n_thr, double* sums,
-                        uint64_t* counts, void* stream);
+                        int32_t num_sims, const float* thresholds, int32_t n_thr, const float* area,
+                        double* sums, uint64_t* counts, void* stream);
 
 /* Diagnostics: route per-phase timestamps of wave 0 of workgroup 0 of every launch to the
  * device buffer `buf` (uint64[20]: {shader clock, 100 MHz clock} for phase marks 0..9).

@@ -4,6 +4,9 @@
 //   get_rollout_loss (RMSE / MAE, all nodes or only_where_water)  utils/miscellaneous.py:177-199,
 //                                                                  training/loss.py:8-35
 //   confusion matrix -> CSI / F1 at water-depth thresholds        utils/miscellaneous.py:123-169
+//   stored water volume sum(area * h) per step, the core of the mass-conservation metric
+//   get_mass_conservation_loss / conservation_loss      utils/miscellaneous.py:116-121,
+//                                                         training/loss.py:120-169
 // The kernel produces per-(simulation, step) partial sums in fp64 and exact integer counts;
 // the host side (mswegnn/metrics.py) forms the reference's ratios.
 #include <hip/hip_runtime.h>
@@ -16,6 +19,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kTChunk = 32;    // time steps per workgroup (blockIdx.y)
 constexpr int kMaxThr = 4;
+constexpr int kSums = 10;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -24,17 +28,18 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // One thread = one fine-scale row of simulation g, all steps of the block's time chunk.
-// sums[g][t][9]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, and the same four over the rows
-// where dh != 0 or dv != 0 (mask_on_water), then that row count.
+// sums[g][t][10]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, the same four over the rows where
+// dh != 0 or dv != 0 (mask_on_water), that row count, sum area * h_pred (0 without area).
 // counts[g][t][k][4]: TP, TN, FP, FN of (pred_h > thr_k) vs (real_h > thr_k).
 struct MetricArgs {
   const float* pred;
   const float* real;
+  const float* area;            // [rows] by graph row, or null
   int T;
   int row0, nrows;  // fine-scale rows [row0, row0 + nrows) of this simulation
   int nthr;
   float thr[kMaxThr];
-  double* sums;                 // this simulation's [T][9]
+  double* sums;                 // this simulation's [T][kSums]
   unsigned long long* counts;   // this simulation's [T][nthr][4]
 };
 
@@ -44,6 +49,7 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
   const size_t n = (size_t)a.row0 + (valid ? i : 0);
   const int lane = threadIdx.x & 63;
   const int t0 = blockIdx.y * kTChunk;
+  const double ar = valid && a.area ? (double)a.area[n] : 0.0;
   for (int t = t0; t < t0 + kTChunk && t < a.T; ++t) {
     float dh = 0.f, dv = 0.f, ph = 0.f, rh = 0.f;
     if (valid) {
@@ -53,7 +59,7 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
       dv = a.pred[(n * 2 + 1) * a.T + t] - a.real[(n * 2 + 1) * a.T + t];
     }
     const bool wet = valid && (dh != 0.f || dv != 0.f);
-    double v[9];
+    double v[kSums];
     v[0] = fabs((double)dh);
     v[1] = fabs((double)dv);
     v[2] = (double)dh * dh;
@@ -63,11 +69,12 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
     v[6] = wet ? v[2] : 0.0;
     v[7] = wet ? v[3] : 0.0;
     v[8] = wet ? 1.0 : 0.0;
+    v[9] = ar * (double)ph;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) v[k] = wave_sum(v[k]);
+    for (int k = 0; k < kSums; ++k) v[k] = wave_sum(v[k]);
     if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < 9; ++k) atomicAdd(a.sums + (size_t)t * 9 + k, v[k]);
+      for (int k = 0; k < kSums; ++k) atomicAdd(a.sums + (size_t)t * kSums + k, v[k]);
     }
     for (int k = 0; k < a.nthr; ++k) {
       const bool p = ph > a.thr[k], r = rh > a.thr[k];
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
 
 extern "C" int msw_rollout_metrics(const float* pred, const float* real, int32_t T,
                                    const int64_t* fine_ranges, int32_t num_sims,
-                                   const float* thresholds, int32_t n_thr, double* sums,
+                                   const float* thresholds, int32_t n_thr, const float* area, double* sums,
                                    uint64_t* counts, void* stream) {
   if (!pred || !real || !fine_ranges || !sums || (n_thr > 0 && (!thresholds || !counts)))
     return msw::set_error(MSW_ERR_INVALID, "null argument");
@@ -102,13 +109,14 @@ extern "C" int msw_rollout_metrics(const float* pred, const float* real, int32_t
     MetricArgs a{};
     a.pred = pred;
     a.real = real;
+    a.area = area;
     a.T = T;
     a.row0 = (int)fine_ranges[2 * g];
     a.nrows = (int)(fine_ranges[2 * g + 1] - fine_ranges[2 * g]);
     if (a.nrows < 0) return msw::set_error(MSW_ERR_INVALID, "fine range end < start");
     a.nthr = n_thr;
     for (int k = 0; k < n_thr; ++k) a.thr[k] = thresholds[k];
-    a.sums = sums + (size_t)g * T * 9;
+    a.sums = sums + (size_t)g * T * kSums;
     a.counts = reinterpret_cast<unsigned long long*>(counts) + (size_t)g * T * (n_thr > 0 ? n_thr : 1) * 4;
     if (a.nrows == 0) continue;
     const dim3 grid((a.nrows + kThreads - 1) / kThreads, (T + kTChunk - 1) / kTChunk);

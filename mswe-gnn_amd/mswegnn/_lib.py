@@ -96,7 +96,8 @@ SYMBOLS = [
                                    C.c_void_p]),
     ("msw_set_trace", C.c_int, [C.c_void_p, C.c_void_p]),
     ("msw_rollout_metrics", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, c_int64_p, C.c_int32,
-                                      c_float_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+                                      c_float_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]),
     ("msw_plan_create_part", C.c_int, [C.POINTER(MswGraphDesc), C.POINTER(MswModelDesc), C.c_int,
                                        C.POINTER(MswExchangeDesc), C.c_int32, C.POINTER(C.c_void_p)]),
     ("msw_comm_unique_id", C.c_int, [C.c_char_p]),

@@ -264,6 +264,10 @@ def make_multiscale_mesh(n_coarse=3, num_scales=4, seed=0, T=48, previous_t=3,
         y=torch.zeros(N, 2, T),
         temporal_res=torch.tensor(120),
         previous_t=torch.tensor(previous_t),
+        # raw cell areas [m^2] and BC edge length [m] per scale (the reference's data.area /
+        # data.edge_BC_length, used by the mass-conservation metric, loss.py:120-169)
+        area=torch.from_numpy(np.concatenate([sc["area"] for sc in scales]).astype(np.float32)),
+        edge_BC_length=torch.tensor([sc["bc_edge_len"] for sc in scales], dtype=torch.float32),
     )
 
 
@@ -276,7 +280,8 @@ def make_single_scale_mesh(n_coarse=3, refinements=3, seed=0, T=10, previous_t=3
     return Graph(x=g.x[:n0].clone(), edge_index=g.edge_index[:, :e0].clone(),
                  edge_attr=g.edge_attr[:e0].clone(), BC=g.BC.clone(), node_BC=g.node_BC.clone(),
                  type_BC=g.type_BC.clone(), y=torch.zeros(n0, 2, T),
-                 temporal_res=g.temporal_res, previous_t=g.previous_t)
+                 temporal_res=g.temporal_res, previous_t=g.previous_t,
+                 area=g.area[:n0].clone(), edge_BC_length=g.edge_BC_length[:1].clone())
 
 
 def wet_state(graph, seed=0, depth=0.8, frac=0.35, previous_t=3, all_wet=False):

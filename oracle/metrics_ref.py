@@ -8,6 +8,8 @@ functions.
   get_rollout_loss        utils/miscellaneous.py:177-199 (+ get_masked_diff :171-175)
   get_binary_rollouts     utils/miscellaneous.py:123-136
   get_rollout_confusion_matrix / get_CSI / get_F1   utils/miscellaneous.py:138-169
+  get_mass_conservation_loss  utils/miscellaneous.py:116-121 -> conservation_loss
+                              training/loss.py:120-169 -> get_inflow_volume dataset.py:577-591
 """
 import torch
 
@@ -55,3 +57,26 @@ def f1(pred, real, thr):
     """utils/miscellaneous.py:162-169"""
     TP, TN, FP, FN = confusion(pred, real, thr)
     return TP / (TP + 0.5 * (FN + FP))
+
+
+def inflow_volume(bc_t, edge_bc_length, temporal_res):
+    """utils/dataset.py:577-591: sum(|q| * L_bc) * 60 s * temporal_res [m^3]"""
+    return (bc_t * edge_bc_length).sum() * (60 * temporal_res)
+
+
+def conservation_loss(pred_wd, input_wd, area, node_bc, bc_t, edge_bc_length, temporal_res):
+    """training/loss.py:120-169 (single multi-scale graph; area already the finest rows)"""
+    area = area if area.dim() == 2 else area.unsqueeze(1)
+    delta = pred_wd - input_wd
+    predicted = (area * delta).sum()
+    inflow = inflow_volume(bc_t, edge_bc_length, temporal_res)
+    correction = (area * delta)[node_bc].sum()
+    return (predicted - inflow - correction) / 1e6
+
+
+def mass_conservation_loss(rollout, area_all, node_ptr, BC, node_bc, edge_bc_length, temporal_res):
+    """utils/miscellaneous.py:116-121: rollout = finest rows [n0, 2, T]; BC [n_BC, >= T+1]"""
+    area = area_all[node_ptr[0]:node_ptr[1]]
+    return torch.stack([conservation_loss(rollout[:, 0::2, t], rollout[:, 0::2, t - 1], area, node_bc,
+                                          (BC[:, t] + BC[:, t + 1]) / 2, edge_bc_length, temporal_res)
+                        for t in range(1, rollout.shape[-1])])

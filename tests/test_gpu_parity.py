@@ -212,7 +212,11 @@ def test_rollout_metrics_kernel_vs_reference(cuda):
     n0 = int(fx["n0"])
     real = torch.from_numpy(golden("fx_small_K4_F32_rollout48")["rollout"])
     pred = torch.from_numpy(golden("fx_small_K2_F16_rollout48")["rollout"])
-    m = rollout_metrics(pred.to(cuda), real.to(cuda), [(0, n0)], thresholds=(0.05, 0.3))
+    mass = dict(area=torch.from_numpy(fx["mass_area"]), node_bc=[fx["mass_node_bc"]], bc=[fx["mass_bc"]],
+                edge_bc_length=[fx["mass_edge_bc_length"]], temporal_res=float(fx["mass_temporal_res"]))
+    m = rollout_metrics(pred.to(cuda), real.to(cuda), [(0, n0)], thresholds=(0.05, 0.3), mass=mass)
+    # mass conservation: fp64 volume sums vs the reference's fp32 sums (1e-4 of the largest)
+    assert rel_err(m["mass_loss"][0].cpu(), fx["mass_loss_pred"]) <= 1e-4, m["mass_loss"][0][:4]
     for key, ref in (("rmse", "loss_RMSE"), ("mae", "loss_MAE"), ("rmse_water", "loss_RMSE_water"),
                      ("mae_water", "loss_MAE_water")):
         assert rel_err(m[key][0].cpu(), fx[ref]) <= 1e-5, key

@@ -208,6 +208,13 @@ def test_metrics_oracle_matches_reference_fixture():
     p2, r2 = torch.stack([pred, real.flip(-1)]), torch.stack([real, pred])
     assert torch.equal(mr.rollout_loss(p2, r2, "RMSE"), torch.from_numpy(fx["loss_RMSE_stack"]))
     np.testing.assert_array_equal(mr.csi(p2, r2, 0.05).numpy(), fx["csi_0.05_stack"])
+    # mass conservation (get_mass_conservation_loss), bit-exact in the reference's fp32 order
+    npt = torch.tensor([0, n0])
+    args = (torch.from_numpy(fx["mass_area"]), npt, torch.from_numpy(fx["mass_bc"]),
+            torch.from_numpy(fx["mass_node_bc"]).long(), torch.from_numpy(fx["mass_edge_bc_length"]),
+            torch.from_numpy(fx["mass_temporal_res"]))
+    assert torch.equal(mr.mass_conservation_loss(pred, *args), torch.from_numpy(fx["mass_loss_pred"]))
+    assert torch.equal(mr.mass_conservation_loss(real, *args), torch.from_numpy(fx["mass_loss_real"]))
 
 
 # ------------------------------------------------------------------ single-mesh decomposition
