@@ -205,13 +205,26 @@ struct Hop2Args {
 };
 
 // Mean pooling into the coarse rows + projection of the next processor.
+// Children of one coarse row (32 B, one 16-B + one 8-B load): the first kPoolInline
+// internal fine rows, the count, and where the full list starts in PoolArgs::child.
+constexpr int kPoolInline = 4;
+struct alignas(16) PoolRec {
+  int c[kPoolInline];
+  int cnt, off, pad[2];
+};
+
 struct PoolArgs {
   Common c;
   WReg reg;
   int max_blocks;                  // grid cap of the grid-stride variant (resident workgroups)
   int fit_blocks;                  // workgroups of the one-tile-per-wave variant the chip holds
-  int n0;                  // first internal row of the coarse scale
-  const LaneRec* recs; int ntiles;  // edge lanes = children, node lanes = coarse nodes
+  int n0, ns;              // internal rows [n0, n0 + ns) of the coarse scale
+  int rows;                // 1: row layout (k_pool), 0: edge tiles (k_pool_edge)
+  int ntiles;              // tiles of the chosen layout
+  const PoolRec* recs;     // row layout: 16 consecutive coarse rows per tile, one record each
+  const LaneRec* erecs;    // edge tiles: children <= 16 per tile (16 lane records per tile)
+  int rtiles, etiles;      // tile counts of the two layouts
+  const int* child;        // internal fine rows, in reference (intra edge) order
   const float* in;         // x_down
   const float* xs;
   NpDesc np;

@@ -887,17 +887,100 @@ __global__ __launch_bounds__(kBlock) void k_hop2(Hop2Args a) {
 
 // ---------------------------------------------------------------------------- pooling
 // scatter(x[fine], coarse, reduce='mean') (gnn.py:256): children summed in edge order,
-// divided by max(count, 1); then the projection of the next processor.  Tiles of coarse
-// nodes with <= 16 children in all: lane j loads child j, the coarse lanes sum.
+// divided by max(count, 1); then the projection of the next processor.  A wave tile is 16
+// consecutive coarse rows: lane (row j, group g) walks its own row's children (CSR) and
+// sums feature slice g of each -- no lane exchange, every MFMA row of the projection used
+// (an edge-tile layout would hold only 4 coarse rows of 4 children each).
 template <int NT, bool LOOP>
 __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int stride = gridDim.x * kWaves;
+  int tile = blockIdx.x * kWaves + w;
+  Common c = a.c;
+  MSW_MARK(c, 0);
+  struct Rows {
+    f32x4 acc[NT], xs[NT];
+    size_t n;
+    bool nv;
+  };
+  auto load = [&](Rows& r, int t, int j, int g) {
+    const int i = 16 * t + j;
+    r.nv = i < a.ns;
+    r.n = (size_t)a.n0 + (r.nv ? i : 0);
+    int4 rc = *reinterpret_cast<const int4*>(a.recs + 16 * t + j);
+    const int2 ro = *reinterpret_cast<const int2*>(&a.recs[16 * t + j].cnt);
+    asm volatile("" : "+v"(rc.x));  // keep the record one unconditional 16-B load
+    const int cnt = ro.x, off = ro.y;
+    // unconditional loads (absent children re-read child 0 / the row itself): predicated
+    // loads made the compiler drain the memory counter before each one
+    const int c0 = cnt > 0 ? rc.x : (int)r.n;
+    const int ci[kPoolInline] = {c0, cnt > 1 ? rc.y : c0, cnt > 2 ? rc.z : c0, cnt > 3 ? rc.w : c0};
+    f32x4 x[kPoolInline][NT];
+#pragma unroll
+    for (int k = 0; k < kPoolInline; ++k) load_row<NT>(x[k], a.in + (size_t)ci[k] * F, g);
+    load_row<NT>(r.xs, a.xs + r.n * F, g);
+#pragma unroll
+    for (int t2 = 0; t2 < NT; ++t2) r.acc[t2] = zero4();
+#pragma unroll
+    for (int k = 0; k < kPoolInline; ++k) {
+#pragma unroll
+      for (int t2 = 0; t2 < NT; ++t2) {
+        const f32x4 s2 = r.acc[t2] + x[k][t2];
+        r.acc[t2] = k < cnt ? s2 : r.acc[t2];
+      }
+    }
+    for (int k = kPoolInline; k < cnt; ++k) {  // more children than the record holds
+      f32x4 y[NT];
+      load_row<NT>(y, a.in + (size_t)a.child[off + k] * F, g);
+#pragma unroll
+      for (int t2 = 0; t2 < NT; ++t2) r.acc[t2] = r.acc[t2] + y[t2];
+    }
+    const float fc = (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+    for (int t2 = 0; t2 < NT; ++t2) r.acc[t2] = r.acc[t2] / fc;
+  };
+  if constexpr (!LOOP) {
+    Rows r0;
+    load(r0, tile < a.ntiles ? tile : 0, j, g);
+    MSW_MARK(c, 1);
+    if constexpr (kStaged<NT>) {
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      c.W = smem;
+    }
+    MSW_MARK(c, 2);
+    if (tile < a.ntiles) np_project<NT>(r0.xs, r0.acc, a.np, c.W, r0.n, r0.nv, lane, g);
+  } else {
+    if constexpr (kStaged<NT>) {
+      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      c.W = smem;
+    }
+    for (; tile < a.ntiles; tile += stride) {
+      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+      Rows q;
+      load(q, tile, jj, gg);
+      np_project<NT>(q.xs, q.acc, a.np, c.W, q.n, q.nv, ln, gg);
+    }
+  }
+  MSW_MARK(c, 9);
+}
+
+// Small levels (the whole grid resident at once): edge tiles of coarse nodes with <= 16
+// children in all, lane j loads child j, the coarse lanes sum through LDS -- four times
+// the waves of the row layout, each with a shorter load chain (measured faster while the
+// launch is latency-bound).
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
   __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int stride = gridDim.x * kWaves;
   int tile = blockIdx.x * kWaves + w;
   Common c = a.c;
   MSW_MARK(c, 0);
@@ -906,7 +989,7 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
     f32x4 x[NT], xs[NT];
   };
   auto load = [&](Rows& r, int t, int j, int g) {
-    r.L = lanes_of(load_rec(a.recs, t, j), t, j, a.n0);
+    r.L = lanes_of(load_rec(a.erecs, t, j), t, j, a.n0);
     load_row<NT>(r.x, a.in + r.L.sr * F, g);
     load_row<NT>(r.xs, a.xs + r.L.n * F, g);
   };
@@ -922,30 +1005,16 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
     for (int t = 0; t < NT; ++t) acc[t] = acc[t] / cnt;
     np_project<NT>(r.xs, acc, a.np, c.W, L.n, L.nv, lane, g);
   };
-  if constexpr (!LOOP) {
-    Rows r0;
-    load(r0, tile < a.ntiles ? tile : 0, j, g);
-    MSW_MARK(c, 1);
-    if constexpr (kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
-      __syncthreads();
-      c.W = smem;
-    }
-    MSW_MARK(c, 2);
-    if (tile < a.ntiles) run(r0, j, lane, g);
-  } else {
-    if constexpr (kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
-      __syncthreads();
-      c.W = smem;
-    }
-    for (; tile < a.ntiles; tile += stride) {
-      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
-      Rows q;
-      load(q, tile, jj, gg);
-      run(q, jj, ln, gg);
-    }
+  Rows r0;
+  load(r0, tile < a.ntiles ? tile : 0, j, g);
+  MSW_MARK(c, 1);
+  if constexpr (kStaged<NT>) {
+    stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+    __syncthreads();
+    c.W = smem;
   }
+  MSW_MARK(c, 2);
+  if (tile < a.ntiles) run(r0, j, lane, g);
   MSW_MARK(c, 9);
 }
 
@@ -998,7 +1067,8 @@ hipError_t prepare_kernels() {
       (const void*)k_edge_hop<NT, 1, true>, (const void*)k_edge_hop<NT, -1, true>,
       (const void*)k_hop<NT, 1, true, false>, (const void*)k_hop<NT, -1, true, false>,
       (const void*)k_hop<NT, 1, true, true>, (const void*)k_hop<NT, -1, true, true>,
-      (const void*)k_pool<NT, false>, (const void*)k_pool<NT, true>, (const void*)k_hop2<NT>};
+      (const void*)k_pool<NT, false>, (const void*)k_pool<NT, true>, (const void*)k_pool_edge<NT>,
+      (const void*)k_hop2<NT>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     if (e != hipSuccess) return e;
@@ -1067,8 +1137,12 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
 template <int NT>
 hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(tile_grid(a)), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.reg.len);
+  if (!a.rows) {
+    hipLaunchKernelGGL((k_pool_edge<NT>), dim3(cdiv(a.ntiles, kWaves)), dim3(kBlock), sh, st, a);
+    return hipGetLastError();
+  }
+  const dim3 grid(tile_grid(a)), block(kBlock);
   if (tile_loop(a))
     hipLaunchKernelGGL((k_pool<NT, true>), grid, block, sh, st, a);
   else
@@ -1103,6 +1177,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
       return !last ? (const void*)k_hop<NT, 1, false, LOOP>
                    : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
     case 3: return (const void*)k_pool<NT, LOOP>;
+    case 5: return (const void*)k_pool_edge<NT>;
     default: return (const void*)k_hop2<NT>;
   }
 }

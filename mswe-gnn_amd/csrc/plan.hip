@@ -203,8 +203,10 @@ struct ScaleCSR {
 
 struct LevelMaps {              // level l: coarse scale l+1, fine scale l
   int I = 0;
-  LaneRec* pool_recs = nullptr; // coarse nodes (scale l+1) and their children (<= 16 per tile)
-  int pool_ntiles = 0;
+  PoolRec* pool_recs = nullptr; // per coarse row (scale l+1): its children (engine.h PoolRec)
+  LaneRec* pool_erecs = nullptr; // edge tiles of coarse nodes and their children (<= 16 per tile)
+  int pool_etiles = 0;
+  int* pool_child = nullptr;    // internal fine rows, reference order
   LaneRec* un_recs = nullptr;   // fine nodes (scale l) and their coarse parents
   int un_ntiles = 0;
 };
@@ -601,7 +603,10 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
       L.kind = L_POOL;
       L.scale = i + 1;
       PoolArgs& pa = L.pool;
-      pa.c = c; pa.n0 = P->sc[i + 1].n0; pa.recs = m.pool_recs; pa.ntiles = m.pool_ntiles;
+      pa.c = c; pa.n0 = P->sc[i + 1].n0; pa.ns = P->sc[i + 1].ns;
+      pa.rtiles = (pa.ns + 15) / 16; pa.etiles = m.pool_etiles;
+      pa.rows = 1; pa.ntiles = pa.rtiles;  // set_grid_cap picks the layout
+      pa.recs = m.pool_recs; pa.erecs = m.pool_erecs; pa.child = m.pool_child;
       pa.in = P->xdown; pa.xs = P->xs;
       pa.np = np_of(P, P->procs[i + 1]);
       q.push_back(L);
@@ -787,7 +792,15 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       L.hop2.max_blocks = resident_of(P->NT, 4, 0, 0, (size_t)L.hop2.bmax * (16 * P->NT + 4) * 4, 0);
       break;
     case L_EXCHANGE: break;
-    default: caps(P, L.pool, 3, 0, 0, L.pool.reg.len); break;
+    default: {
+      // edge tiles while they all fit on the chip at once (latency-bound launch), else rows
+      PoolArgs& a = L.pool;
+      const int fe = resident_of(P->NT, 5, 0, 0, (size_t)a.reg.len * 4, 0);
+      a.rows = !(fe > 0 && (a.etiles + kWaves - 1) / kWaves <= fe) || getenv("MSW_POOL_ROWS") != nullptr;
+      a.ntiles = a.rows ? a.rtiles : a.etiles;
+      caps(P, a, 3, 0, 0, a.reg.len);
+      break;
+    }
   }
 }
 
@@ -1048,10 +1061,20 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       csr_build(cs.ns, ck, rp, order);
       std::vector<int> child(m.I);
       for (int i = 0; i < m.I; ++i) child[i] = fv[order[i]];
+      std::vector<PoolRec> pr((size_t)(cs.ns + 15) / 16 * 16);
+      for (size_t i = 0; i < pr.size(); ++i) {
+        PoolRec& r = pr[i];
+        const int b = i < (size_t)cs.ns ? rp[i] : 0, e = i < (size_t)cs.ns ? rp[i + 1] : 0;
+        r.cnt = e - b;
+        r.off = b;
+        for (int k = 0; k < kPoolInline; ++k) r.c[k] = k < e - b ? child[b + k] : -1;
+      }
       std::vector<TileRange> pt;
       if ((rc = build_tiles(rp, pt))) return rc;
-      m.pool_ntiles = (int)pt.size();
-      if ((rc = pupload(P, &m.pool_recs, make_recs(rp, child, cs.n0, pt, nullptr)))) return rc;
+      m.pool_etiles = (int)pt.size();
+      if ((rc = pupload(P, &m.pool_erecs, make_recs(rp, child, cs.n0, pt, nullptr)))) return rc;
+      if (child.empty()) child.push_back(0);
+      if ((rc = pupload(P, &m.pool_recs, pr)) || (rc = pupload(P, &m.pool_child, child))) return rc;
       csr_build(fs.ns, fk, rp, order);
       std::vector<int> us(m.I);
       for (int i = 0; i < m.I; ++i) us[i] = cv[order[i]];
