@@ -27,7 +27,7 @@ def _newer(a, b):
 def build(force=False, verbose=True, variant=""):
     """variant "trace": diagnostic library lib/libmswegnn_trace.so (-DMSW_TRACE)."""
     odir = os.path.join(HERE, "_obj" + (f"_{variant}" if variant else ""))
-    extra = ["-DMSW_TRACE"] if variant == "trace" else []
+    extra = {"trace": ["-DMSW_TRACE"], "w8": ["-DMSW_WAVES=8"], "w2": ["-DMSW_WAVES=2"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     objs, cmds = [], []

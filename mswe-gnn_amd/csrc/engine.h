@@ -9,7 +9,10 @@ namespace msw {
 
 constexpr int kMaxLayers = 4;
 constexpr int kRowsPerWave = 16;  // v_mfma_f32_16x16x4_f32: 16 rows (nodes / edges) per wave
-constexpr int kWaves = 4;         // waves per 256-thread block
+#ifndef MSW_WAVES
+#define MSW_WAVES 4
+#endif
+constexpr int kWaves = MSW_WAVES;  // waves per block (tiles per workgroup)
 constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
 constexpr int kMaxScales = 8;
 

@@ -25,6 +25,11 @@ namespace msw {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 64 * kWaves;
+// Grid-stride (LOOP) variants of the tile kernels run 8-wave workgroups when their weights
+// are staged in LDS (F <= 32): one staged copy per 8 waves instead of per 4 halves the
+// staging traffic of a large mesh and the LDS the copies take.
+template <int NT, bool LOOP>
+constexpr int waves_of() { return LOOP && NT <= 2 ? 8 : kWaves; }
 
 #define MSW_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
@@ -347,9 +352,10 @@ __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& 
 // cover [first, last) floats of the region; a partial final chunk reads up to 255 floats
 // past the region (the blob and the LDS allocation are padded for it).
 constexpr int kChunk = 256;
+template <int WV = kWaves>
 __device__ __forceinline__ void stage_glds(float* smem, const float* __restrict__ W, WReg r, int first, int last) {
   const int lane = threadIdx.x & 63;
-  for (int ch = first / kChunk + wave_id(); ch * kChunk < last; ch += kWaves)
+  for (int ch = first / kChunk + wave_id(); ch * kChunk < last; ch += WV)
     __builtin_amdgcn_global_load_lds(
         (const __attribute__((address_space(1))) void*)(W + r.off + ch * kChunk + lane * 4),
         (__attribute__((address_space(3))) void*)(smem + ch * kChunk), 16, 0, 0);
@@ -669,14 +675,15 @@ __device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const EdgeHopR
   }
 }
 template <int NT, int ACT, bool LOOP>
-__global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
+__global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_edge_hop(EdgeHopArgs a) {
+  constexpr int WV = waves_of<NT, LOOP>();
   // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
   constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
-  __shared__ __attribute__((aligned(16))) float slab[kWaves][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float slab[WV][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int stride = gridDim.x * kWaves;
-  int tile = blockIdx.x * kWaves + w;
+  const int stride = gridDim.x * WV;
+  int tile = blockIdx.x * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   f32x4 wf[NT][NT];
@@ -690,10 +697,10 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
     // stream into LDS behind the MLP and are waited for at the epilogue barrier
     const bool split = kStaged<NT> && a.reg.split < a.reg.len;
     if constexpr (kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.split);
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.split);
       __syncthreads();
       c.W = smem;
-      if (split) stage_glds(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg.len);
+      if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg.len);
     }
     MSW_MARK(c, 2);
     f32x4 res[NT];
@@ -702,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_hop(EdgeHopArgs a) {
     if (live) edge_hop_finish<NT, ACT>(res, r, a, c, lane, g);
   } else {
     if constexpr (kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -732,24 +739,30 @@ struct HopRows {
   EpiPre<NT> pre;  // LAST only
 };
 template <int NT, bool LAST>
-__device__ __forceinline__ void hop_load(HopRows<NT>& r, const HopArgs& a, int tile, int j, int g) {
+__device__ __forceinline__ void hop_gather(HopRows<NT>& r, const HopArgs& a, const LaneRec& rec, int tile, int j,
+                                           int g) {
   constexpr int F = 16 * NT;
-  r.L = lanes_of(load_rec(a.recs, tile, j), tile, j, a.n0);
+  r.L = lanes_of(rec, tile, j, a.n0);
   load_row<NT>(r.os, a.in + r.L.sr * F, g);
   load_row<NT>(r.sv, a.s + r.L.p * F, g);
   load_row<NT>(r.inn, a.in + r.L.n * F, g);
   if constexpr (LAST) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, r.L.n, g);
 }
+template <int NT, bool LAST>
+__device__ __forceinline__ void hop_load(HopRows<NT>& r, const HopArgs& a, int tile, int j, int g) {
+  hop_gather<NT, LAST>(r, a, load_rec(a.recs, tile, j), tile, j, g);
+}
 template <int NT, int ACT, bool LAST, bool LOOP>
-__global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
+__global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_hop(HopArgs a) {
 #pragma clang fp contract(off)
+  constexpr int WV = waves_of<NT, LOOP>();
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
-  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float slab_all[WV][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int stride = gridDim.x * kWaves;
-  int tile = blockIdx.x * kWaves + w;
+  const int stride = gridDim.x * WV;
+  int tile = blockIdx.x * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   f32x4 wf[NT][NT];
@@ -787,7 +800,7 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
     hop_load<NT, LAST>(r, a, live ? tile : 0, j, g);
     MSW_MARK(c, 1);
     // the epilogue's operands stream into LDS alongside the tile's gathers
-    if constexpr (LAST && kStaged<NT>) stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+    if constexpr (LAST && kStaged<NT>) stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
     f32x4 res[NT];
     if (live) core(r, j, lane, g, res);
     if constexpr (LAST && kStaged<NT>) {
@@ -798,17 +811,43 @@ __global__ __launch_bounds__(kBlock) void k_hop(HopArgs a) {
     if (live) finish(res, r, lane, g);
   } else {
     if constexpr (LAST && kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
-    for (; tile < a.ntiles; tile += stride) {
-      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+    // middle hops, software pipeline: tile i+1's gathers and tile i+2's lane record are in
+    // flight while tile i computes (the record round trip no longer stalls the wave); the
+    // last hop keeps one tile in flight (its epilogue prefetch would double the registers)
+    if (LAST) {
+      for (; tile < a.ntiles; tile += stride) {
+        const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+        HopRows<NT> q;
+        hop_load<NT, LAST>(q, a, tile, jj, gg);
+        f32x4 res[NT];
+        core(q, jj, ln, gg, res);
+        finish(res, q, ln, gg);
+      }
+    } else if (tile < a.ntiles) {
       HopRows<NT> q;
-      hop_load<NT, LAST>(q, a, tile, jj, gg);
-      f32x4 res[NT];
-      core(q, jj, ln, gg, res);
-      finish(res, q, ln, gg);
+      hop_load<NT, LAST>(q, a, tile, j, g);
+      int t1 = tile + stride;
+      LaneRec rn = load_rec(a.recs, t1 < a.ntiles ? t1 : tile, j);
+      for (;;) {
+        const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+        const bool more = t1 < a.ntiles;
+        HopRows<NT> qn;
+        if (more) {
+          hop_gather<NT, LAST>(qn, a, rn, t1, jj, gg);
+          const int t2 = t1 + stride;
+          rn = load_rec(a.recs, t2 < a.ntiles ? t2 : t1, jj);
+        }
+        f32x4 res[NT];
+        core(q, jj, ln, gg, res);
+        finish(res, q, ln, gg);
+        if (!more) break;
+        q = qn;
+        t1 += stride;
+      }
     }
   }
   MSW_MARK(c, 9);
@@ -892,13 +931,14 @@ __global__ __launch_bounds__(kBlock) void k_hop2(Hop2Args a) {
 // sums feature slice g of each -- no lane exchange, every MFMA row of the projection used
 // (an edge-tile layout would hold only 4 coarse rows of 4 children each).
 template <int NT, bool LOOP>
-__global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
+__global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_pool(PoolArgs a) {
 #pragma clang fp contract(off)
+  constexpr int WV = waves_of<NT, LOOP>();
   constexpr int F = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int stride = gridDim.x * kWaves;
-  int tile = blockIdx.x * kWaves + w;
+  const int stride = gridDim.x * WV;
+  int tile = blockIdx.x * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   struct Rows {
@@ -947,7 +987,7 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
     load(r0, tile < a.ntiles ? tile : 0, j, g);
     MSW_MARK(c, 1);
     if constexpr (kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -955,7 +995,7 @@ __global__ __launch_bounds__(kBlock) void k_pool(PoolArgs a) {
     if (tile < a.ntiles) np_project<NT>(r0.xs, r0.acc, a.np, c.W, r0.n, r0.nv, lane, g);
   } else {
     if constexpr (kStaged<NT>) {
-      stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
     }
@@ -1060,17 +1100,19 @@ constexpr size_t lds_bytes(int floats) {
 // Allow the dynamic weight regions past the 64 KB default (gfx950: 160 KB per CU).
 template <int NT>
 hipError_t prepare_kernels() {
-  const int mx = 160 * 1024 - kWaves * kRowsPerWave * (16 * 2 * NT + 16 * NT + 4) * (int)sizeof(float);
-  const void* fns[] = {
-      (const void*)k_encode<NT, 1>, (const void*)k_encode<NT, -1>,
-      (const void*)k_edge_hop<NT, 1, false>, (const void*)k_edge_hop<NT, -1, false>,
-      (const void*)k_edge_hop<NT, 1, true>, (const void*)k_edge_hop<NT, -1, true>,
-      (const void*)k_hop<NT, 1, true, false>, (const void*)k_hop<NT, -1, true, false>,
-      (const void*)k_hop<NT, 1, true, true>, (const void*)k_hop<NT, -1, true, true>,
-      (const void*)k_pool<NT, false>, (const void*)k_pool<NT, true>, (const void*)k_pool_edge<NT>,
-      (const void*)k_hop2<NT>};
-  for (const void* f : fns) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+  // the largest static slab (edge-MLP rows) of a workgroup of `wv` waves
+  auto mx = [](int wv) { return 160 * 1024 - wv * kRowsPerWave * (16 * 2 * NT + 16 * NT + 4) * (int)sizeof(float); };
+  constexpr int WL = waves_of<NT, true>();
+  const std::pair<const void*, int> fns[] = {
+      {(const void*)k_encode<NT, 1>, kWaves}, {(const void*)k_encode<NT, -1>, kWaves},
+      {(const void*)k_edge_hop<NT, 1, false>, kWaves}, {(const void*)k_edge_hop<NT, -1, false>, kWaves},
+      {(const void*)k_edge_hop<NT, 1, true>, WL}, {(const void*)k_edge_hop<NT, -1, true>, WL},
+      {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
+      {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
+      {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
+      {(const void*)k_pool_edge<NT>, kWaves}, {(const void*)k_hop2<NT>, kWaves}};
+  for (const auto& f : fns) {
+    hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1102,9 +1144,9 @@ static inline int tile_grid(const A& a) {
 template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(tile_grid(a)), block(kBlock);
-  const size_t sh = lds_bytes<NT>(a.reg.len);
   const bool loop = tile_loop(a);
+  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  const size_t sh = lds_bytes<NT>(a.reg.len);
   if (a.c.prelu) {
     if (loop) hipLaunchKernelGGL((k_edge_hop<NT, 1, true>), grid, block, sh, st, a);
     else hipLaunchKernelGGL((k_edge_hop<NT, 1, false>), grid, block, sh, st, a);
@@ -1117,8 +1159,8 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  const dim3 grid(tile_grid(a)), block(kBlock);
   const bool loop = tile_loop(a);
+  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
   if (!a.last) {
     if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_hop<NT, 1, false, false>), grid, block, 0, st, a);
@@ -1142,8 +1184,9 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_pool_edge<NT>), dim3(cdiv(a.ntiles, kWaves)), dim3(kBlock), sh, st, a);
     return hipGetLastError();
   }
-  const dim3 grid(tile_grid(a)), block(kBlock);
-  if (tile_loop(a))
+  const bool loop = tile_loop(a);
+  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  if (loop)
     hipLaunchKernelGGL((k_pool<NT, true>), grid, block, sh, st, a);
   else
     hipLaunchKernelGGL((k_pool<NT, false>), grid, block, sh, st, a);
@@ -1186,7 +1229,8 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlock, dyn) != hipSuccess)
+  const int block = 64 * (loop && kind >= 1 && kind <= 3 ? waves_of<NT, true>() : kWaves);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
