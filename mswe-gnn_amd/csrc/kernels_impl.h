@@ -243,7 +243,6 @@ __device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, c
     for (int k = 0; k < kMaxDyn; ++k) p.xd[k] = k < c.dyn ? xr[k] : 0.f;
   }
 }
-
 // tanh(x_up) -> node_decoder -> + learned residual -> ReLU -> small-depth mask
 // (gnn.py:335-348, models.py:50-91); rollout mode: use_prediction + BC of the next step
 // (dataset.py:486-529) and the rollout write (train.py:88-95).
@@ -539,11 +538,11 @@ __device__ __forceinline__ int opaque_lane() {
 // kernel start; apply_filter_regs = apply_filter with the operand already in registers.
 template <int NT>
 __device__ __forceinline__ void load_filter(f32x4 (&wf)[NT][NT], const float* W, int filt_a, int lane) {
-  if (filt_a < 0) return;
+  const int fa = filt_a >= 0 ? filt_a : 0;  // unconditional (unused without a filter)
 #pragma unroll
   for (int to = 0; to < NT; ++to)
 #pragma unroll
-    for (int ti = 0; ti < NT; ++ti) wf[to][ti] = ld4(W + filt_a + ((size_t)(to * NT + ti) * 64 + lane) * 4);
+    for (int ti = 0; ti < NT; ++ti) wf[to][ti] = ld4(W + fa + ((size_t)(to * NT + ti) * 64 + lane) * 4);
 }
 template <int NT>
 __device__ __forceinline__ void apply_filter_regs(f32x4 (&res)[NT], const f32x4 (&agg)[NT], int filt_a,
@@ -584,20 +583,21 @@ __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopA
   r.L = lanes_of(load_rec(a.recs, tile, j), tile, j, a.n0);
   const Lanes& L = r.L;
   const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  const float* Ub = a.U + L.sr * hs;
+  const float* Vb = a.V + L.n * hs;
+  const float* Pb = a.Pe ? a.Pe + L.p * hs : z;
 #pragma unroll
-  for (int t = 0; t < T2; ++t) {
+  for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
     const int off = 16 * t + 4 * g;
     const bool on = t < a.h1t;
-    r.Us[t] = on ? ld4(a.U + L.sr * hs + off) : zero4();
-    r.Vn[t] = on ? ld4(a.V + L.n * hs + off) : zero4();
-    r.Ps[t] = (on && a.Pe) ? ld4(a.Pe + L.p * hs + off) : zero4();
+    r.Us[t] = ld4((on ? Ub : z) + off);
+    r.Vn[t] = ld4((on ? Vb : z) + off);
+    r.Ps[t] = ld4((on ? Pb : z) + off);
   }
   load_row<NT>(r.os, a.in + L.sr * F, g);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    r.inn[t] = a.own_zero ? zero4() : ld4(a.in + L.n * F + 16 * t + 4 * g);
-    r.sk[t] = a.skip ? ld4(a.skip + L.n * F + 16 * t + 4 * g) : zero4();
-  }
+  load_row<NT>(r.inn, a.own_zero ? z : a.in + L.n * F, g);
+  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
   if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
 }
 template <int NT, int ACT, int XS>
@@ -853,75 +853,195 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_hop(HopArgs a) 
   MSW_MARK(c, 9);
 }
 
-// ---------------------------------------------------------------------------- hop pair
-// Hops k and k+1 (both before the layer's last hop) in one launch (engine.h Hop2Args).
-// Grid-stride over workgroup blocks; every wave of a workgroup walks the same blocks, so
-// the barriers are uniform.  Filters come straight from the blob into registers.
+// ---------------------------------------------------------------------------- hop chain
+// Hops k .. k+M-1 in one launch (engine.h HopMArgs).  Grid-stride over workgroup blocks;
+// every wave of a workgroup walks the same blocks and levels, so the barriers are uniform.
+// chain_waves<NT>() waves per workgroup: a level's halo tiles run one per wave (their
+// gathers in parallel); waves 0 .. kWaves-1 also own the final level's tiles, whose
+// records, s rows and epilogue inputs are loaded at block start, behind level 1.
+template <int NT, int M>
+struct ChainFilt {  // the M filters in registers (F <= 32); F = 64 reads them from the blob
+  f32x4 w[NT <= 2 ? M : 1][NT][NT];
+};
+template <int NT, int M>
+__device__ __forceinline__ void chain_filter(f32x4 (&res)[NT], const f32x4 (&agg)[NT], const ChainFilt<NT, M>& cf,
+                                             int l, const HopMArgs& a, int lane) {
+  if constexpr (NT <= 2) {
+    apply_filter_regs<NT>(res, agg, a.filt[l], cf.w[l]);
+  } else {
+    apply_filter<NT>(res, agg, a.filt[l], a.c.W, lane);
+  }
+}
+// A level tile of this wave: its lane record {src, p, dl, n}, {bl, q} and s rows.
+constexpr int kPre1 = 2;  // level-1 tiles per wave fetched up front (~11 per block of 4 tiles / 8 waves)
 template <int NT>
-__global__ __launch_bounds__(kBlock) void k_hop2(Hop2Args a) {
+struct LvPre {
+  int4 r0, r1;
+  f32x4 sv[NT];
+};
+// The load is unconditional (t must be a valid tile; callers clamp it) and `ok` selects
+// afterwards: a predicated load made the compiler drain the memory counter behind each one.
+template <int NT>
+__device__ __forceinline__ void lv_rec(LvPre<NT>& q, const HopMArgs& a, int t, bool ok, int j) {
+  const int4* rp = reinterpret_cast<const int4*>(a.lv + (size_t)t * kRowsPerWave + j);
+  const int4 r0 = rp[0], r1 = rp[1];
+  q.r0 = ok ? r0 : int4{-1, 0, 0, -1};
+  q.r1 = ok ? r1 : int4{0, 0, 0, 0};
+}
+// a tile with a node in lane 0 (wave-uniform test; padding tiles and absent slots have none)
+template <int NT>
+__device__ __forceinline__ bool lv_live(const LvPre<NT>& q) {
+  return __builtin_amdgcn_readfirstlane(q.r0.w) >= 0;
+}
+template <int NT>
+__device__ __forceinline__ void lv_s(LvPre<NT>& q, const HopMArgs& a, int g) {
+  load_row<NT>(q.sv, a.s + (size_t)(q.r0.x >= 0 ? q.r0.y : 0) * 16 * NT, g);
+}
+// One level tile: message, segmented sum, filter of hop l; result row to `to` (LDS set).
+template <int NT, int M>
+__device__ __forceinline__ void lv_hop(const LvPre<NT>& q, const f32x4 (&os)[NT], const f32x4 (&inn)[NT], float* to,
+                                       float* slab, float* my, const ChainFilt<NT, M>& cf, int l,
+                                       const HopMArgs& a, int lane, int g) {
 #pragma clang fp contract(off)
+  constexpr int XS = 16 * NT + 4;
+  const bool ev = q.r0.x >= 0, nv = q.r0.w >= 0;
+  f32x4 od[NT];
+  store_row<NT>(my, inn, NT, g);
+  wave_lds_sync();
+  load_row<NT>(od, slab + (ev ? q.r0.z : 0) * XS, g);
+  put_message<NT>(my, os, od, q.sv, ev, a.grad, a.upwind, g);
+  f32x4 agg[NT], res[NT];
+  const int q0 = q.r1.y & 255, q1 = nv ? (q.r1.y >> 8) : q0;
+  gather_messages<NT, XS>(agg, slab, q0, q1, g);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) res[t] = inn[t];
+  chain_filter<NT, M>(res, agg, cf, l, a, lane);
+  if (nv) store_row<NT>(to + (size_t)q.r1.x * XS, res, NT, g);
+}
+template <int NT, int ACT, int M, bool LAST>
+__global__ __launch_bounds__(64 * chain_waves<NT>()) void k_hopm(HopMArgs a) {
+#pragma clang fp contract(off)
+  constexpr int WV = chain_waves<NT>();
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
-  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
-  extern __shared__ __attribute__((aligned(16))) float outB[];  // [bmax][XS] = out_{k+1} on B
+  __shared__ __attribute__((aligned(16))) float slab_all[WV][kRowsPerWave][XS];
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // [weights][buf0][buf1]
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const Common& c = a.c;
-  f32x4 wf1[NT][NT], wf2[NT][NT];
-  load_filter<NT>(wf1, c.W, a.filt1, lane);
-  load_filter<NT>(wf2, c.W, a.filt2, lane);
+  Common c = a.c;
+  MSW_MARK(c, 0);
+  ChainFilt<NT, M> cf;
+  if constexpr (LAST && kStaged<NT>) stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);  // waited at level 1's barrier
+  float* const buf[2] = {smem + a.wfloats, smem + a.wfloats + (size_t)a.bmax * XS};
   float* slab = &slab_all[w][0][0];
   float* my = slab + j * XS;
+  bool staged = !(LAST && kStaged<NT>);
   for (int blk = blockIdx.x; blk < a.nblocks; blk += gridDim.x) {
-    // level-2 tile of this wave: records and s rows first (they do not depend on level 1)
-    const int tile2 = blk * kWaves + w;
-    const bool live2 = tile2 < a.ntiles;
-    const int ts = live2 ? tile2 : 0;
-    const Lanes L2 = lanes_of(load_rec(a.recs, ts, j), ts, j, a.n0);
-    const int2 sd = a.l2[(size_t)ts * kRowsPerWave + j];
+    // final level of this wave (its own tile): everything that does not depend on the levels
+    const int tile = blk * kWaves + w;
+    const bool live = w < kWaves && tile < a.ntiles;
+    const int ts = live ? tile : 0;
+    const Lanes LF = lanes_of(load_rec(a.recs, ts, j), ts, j, a.n0);
+    const int2 sd = a.lf[(size_t)ts * kRowsPerWave + j];
     const int a0 = a.a0[blk];
-    f32x4 sv2[NT];
-    load_row<NT>(sv2, a.s + L2.p * F, g);
-    // ---- level 1: out_{k+1} on B (whole in-neighbourhoods, k_hop arithmetic)
-    const int t_end = a.l1_off[blk + 1];
-    for (int t1 = a.l1_off[blk] + w; t1 < t_end; t1 += kWaves) {
-      const int4* rp = reinterpret_cast<const int4*>(a.l1 + (size_t)t1 * kRowsPerWave + j);
-      const int4 r0 = rp[0], r1 = rp[1];  // {src, p, dl, n}, {bl, q, -, -}
-      const bool ev = r0.x >= 0, nv = r0.w >= 0;
-      const size_t sr = (size_t)(ev ? r0.x : a.n0), nn = (size_t)(nv ? r0.w : a.n0);
-      f32x4 os[NT], sv[NT], inn[NT], od[NT];
-      load_row<NT>(os, a.in + sr * F, g);
-      load_row<NT>(sv, a.s + (size_t)(ev ? r0.y : 0) * F, g);
-      load_row<NT>(inn, a.in + nn * F, g);
-      store_row<NT>(my, inn, NT, g);
-      wave_lds_sync();
-      load_row<NT>(od, slab + (ev ? r0.z : 0) * XS, g);
-      put_message<NT>(my, os, od, sv, ev, a.grad, a.upwind, g);
-      f32x4 agg[NT], res[NT];
-      const int q0 = r1.y & 255, q1 = nv ? (r1.y >> 8) : q0;
-      gather_messages<NT, XS>(agg, slab, q0, q1, g);
+    f32x4 svF[NT];
+    load_row<NT>(svF, a.s + LF.p * F, g);
+    EpiPre<NT> pre;
+    if constexpr (LAST) epi_prefetch<NT>(pre, a.epi, c, a.xs, LF.n, g);
+    // ---- levels 1 .. M-1: out_{k+l} on D_l into buf[(l-1) & 1].  The first kPre1 level-1
+    // tiles and the first level-2 tile of this wave are fetched up front (records, then s
+    // rows and level 1's HBM gathers, all in flight together); further tiles (rare) load
+    // on the spot.
+    // level l's tiles of this block: lv_base + blk * lv_tiles + slot (fixed stride: no
+    // offset load in front of the records); empty padding tiles have no node in lane 0
+    const int n1 = a.lv_tiles[0], b1 = a.lv_base[0] + blk * n1;
+    LvPre<NT> p1[kPre1], p2;
+    f32x4 os1[kPre1][NT], in1[kPre1][NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) res[t] = inn[t];
-      apply_filter_regs<NT>(res, agg, a.filt1, wf1);
-      if (nv) store_row<NT>(outB + (size_t)r1.x * XS, res, NT, g);
+    for (int u = 0; u < kPre1; ++u) {
+      const int sl = w + u * WV;
+      lv_rec<NT>(p1[u], a, b1 + (sl < n1 ? sl : n1 - 1), sl < n1, j);
     }
+    const int n2 = M > 2 ? a.lv_tiles[1] : 0, b2 = M > 2 ? a.lv_base[1] + blk * n2 : 0;
+    if constexpr (M > 2) lv_rec<NT>(p2, a, b2 + (w < n2 ? w : n2 - 1), w < n2, j);
+    MSW_MARK(c, 2);
+    // the filters (blob -> registers) go out behind the records: issued first, their
+    // register writes held the records back (the compiler waited on them)
+    if constexpr (NT <= 2) {
+#pragma unroll
+      for (int l = 0; l < M; ++l) load_filter<NT>(cf.w[l], a.c.W, a.filt[l], lane);
+    }
+    MSW_MARK(c, 3);
+#pragma unroll
+    for (int u = 0; u < kPre1; ++u) {
+      lv_s<NT>(p1[u], a, g);
+      load_row<NT>(os1[u], a.in + (size_t)(p1[u].r0.x >= 0 ? p1[u].r0.x : a.n0) * F, g);
+      load_row<NT>(in1[u], a.in + (size_t)(p1[u].r0.w >= 0 ? p1[u].r0.w : a.n0) * F, g);
+    }
+    if constexpr (M > 2) lv_s<NT>(p2, a, g);
+    MSW_MARK(c, 1);
+#pragma unroll
+    for (int u = 0; u < kPre1; ++u)
+      if (lv_live(p1[u])) lv_hop<NT, M>(p1[u], os1[u], in1[u], buf[0], slab, my, cf, 0, a, lane, g);
+    for (int t = w + kPre1 * WV; t < n1; t += WV) {
+      LvPre<NT> q;
+      f32x4 os[NT], inn[NT];
+      lv_rec<NT>(q, a, b1 + t, true, j);
+      if (!lv_live(q)) continue;
+      lv_s<NT>(q, a, g);
+      load_row<NT>(os, a.in + (size_t)(q.r0.x >= 0 ? q.r0.x : a.n0) * F, g);
+      load_row<NT>(inn, a.in + (size_t)(q.r0.w >= 0 ? q.r0.w : a.n0) * F, g);
+      lv_hop<NT, M>(q, os, inn, buf[0], slab, my, cf, 0, a, lane, g);
+    }
+    MSW_MARK(c, 4);
     __syncthreads();
-    // ---- level 2: out_{k+2} on A from B in LDS
-    if (live2) {
-      const int nl = L2.nv ? (int)(L2.n - a.n0) - a0 : 0;
-      f32x4 os[NT], od[NT], inn[NT];
-      load_row<NT>(os, outB + (size_t)(L2.ev ? sd.x : 0) * XS, g);
-      load_row<NT>(od, outB + (size_t)(L2.ev ? sd.y : 0) * XS, g);
-      load_row<NT>(inn, outB + (size_t)nl * XS, g);
-      put_message<NT>(my, os, od, sv2, L2.ev, a.grad, a.upwind, g);
-      f32x4 agg[NT], res[NT];
-      gather_messages<NT, XS>(agg, slab, L2.q0, L2.q1, g);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) res[t] = inn[t];
-      apply_filter_regs<NT>(res, agg, a.filt2, wf2);
-      if (L2.nv) store_row<NT>(a.out + L2.n * F, res, NT, g);
+    MSW_MARK(c, 5);
+    if constexpr (M > 2) {  // level 2: from buf[0] (LDS) into buf[1]
+      auto lds_hop = [&](const LvPre<NT>& q) {
+        f32x4 os[NT], inn[NT];
+        load_row<NT>(os, buf[0] + (size_t)(q.r0.x >= 0 ? q.r0.x : 0) * XS, g);
+        load_row<NT>(inn, buf[0] + (size_t)(q.r0.w >= 0 ? q.r0.w : 0) * XS, g);
+        lv_hop<NT, M>(q, os, inn, buf[1], slab, my, cf, 1, a, lane, g);
+      };
+      if (lv_live(p2)) lds_hop(p2);
+      for (int t = w + WV; t < n2; t += WV) {
+        LvPre<NT> q;
+        lv_rec<NT>(q, a, b2 + t, true, j);
+        if (!lv_live(q)) continue;
+        lv_s<NT>(q, a, g);
+        lds_hop(q);
+      }
+      MSW_MARK(c, 6);
+      __syncthreads();
+      MSW_MARK(c, 7);
     }
-    __syncthreads();  // outB is reused by the next block
+    if (!staged) {  // the epilogue operands' LDS-DMA was waited for at the barrier above
+      c.W = smem;
+      staged = true;
+    }
+    // ---- final level: out_{k+M} on A from buf[(M-2) & 1]
+    if (live) {
+      const float* fb = buf[(M - 2) & 1];
+      const int nl = LF.nv ? (int)(LF.n - a.n0) - a0 : 0;
+      f32x4 os[NT], od[NT], inn[NT];
+      load_row<NT>(os, fb + (size_t)(LF.ev ? sd.x : 0) * XS, g);
+      load_row<NT>(od, fb + (size_t)(LF.ev ? sd.y : 0) * XS, g);
+      load_row<NT>(inn, fb + (size_t)nl * XS, g);
+      put_message<NT>(my, os, od, svF, LF.ev, a.grad, a.upwind, g);
+      f32x4 agg[NT], res[NT];
+      gather_messages<NT, XS>(agg, slab, LF.q0, LF.q1, g);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) res[tt] = inn[tt];
+      chain_filter<NT, M>(res, agg, cf, M - 1, a, lane);
+      MSW_MARK(c, 8);
+      if constexpr (LAST) {
+        node_epilogue<NT, ACT>(res, a.epi, c, pre, a.out, (int)LF.n, LF.nv, lane, g);
+      } else {
+        if (LF.nv) store_row<NT>(a.out + LF.n * F, res, NT, g);
+      }
+    }
+    __syncthreads();  // the buffers are reused by the next block
   }
+  MSW_MARK(c, 9);
 }
 
 // ---------------------------------------------------------------------------- pooling
@@ -1097,6 +1217,16 @@ constexpr size_t lds_bytes(int floats) {
   return kStaged<NT> ? (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float) : 0;
 }
 
+template <int NT>
+static const void* hopm_kernel(int m, int last, int prelu) {
+  if (!last) return m == 3 ? (const void*)k_hopm<NT, 1, 3, false> : (const void*)k_hopm<NT, 1, 2, false>;
+  if (prelu) return m == 3 ? (const void*)k_hopm<NT, 1, 3, true> : (const void*)k_hopm<NT, 1, 2, true>;
+  return m == 3 ? (const void*)k_hopm<NT, -1, 3, true> : (const void*)k_hopm<NT, -1, 2, true>;
+}
+template <int NT>
+size_t hopm_lds(const HopMArgs& a) {
+  return ((size_t)a.wfloats + (size_t)(a.m == 3 ? 2 : 1) * a.bmax * (16 * NT + 4)) * sizeof(float);
+}
 // Allow the dynamic weight regions past the 64 KB default (gfx950: 160 KB per CU).
 template <int NT>
 hipError_t prepare_kernels() {
@@ -1110,11 +1240,20 @@ hipError_t prepare_kernels() {
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
       {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
-      {(const void*)k_pool_edge<NT>, kWaves}, {(const void*)k_hop2<NT>, kWaves}};
+      {(const void*)k_pool_edge<NT>, kWaves}};
   for (const auto& f : fns) {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
+  // hop chains: 160 KB minus their own (narrower) static slabs
+  constexpr int WC = chain_waves<NT>();
+  for (int m = 2; m <= kChainMax; ++m)
+    for (int last = 0; last < 2; ++last)
+      for (int prelu = 0; prelu < 2; ++prelu) {
+        hipError_t e = hipFuncSetAttribute(hopm_kernel<NT>(m, last, prelu), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024 - WC * kRowsPerWave * (16 * NT + 4) * (int)sizeof(float));
+        if (e != hipSuccess) return e;
+      }
   return hipSuccess;
 }
 
@@ -1193,12 +1332,13 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 template <int NT>
-hipError_t launch_hop2(const Hop2Args& a, hipStream_t st) {
+hipError_t launch_hopm(const HopMArgs& a, hipStream_t st) {
   if (a.nblocks <= 0) return hipSuccess;
+  if (a.m < 2 || a.m > kChainMax) return hipErrorInvalidValue;
   const int grid = a.max_blocks > 0 && a.nblocks > a.max_blocks ? a.max_blocks : a.nblocks;
-  const size_t sh = (size_t)a.bmax * (16 * NT + 4) * sizeof(float);
-  hipLaunchKernelGGL((k_hop2<NT>), dim3(grid), dim3(kBlock), sh, st, a);
-  return hipGetLastError();
+  void* args[] = {const_cast<HopMArgs*>(&a)};
+  return hipLaunchKernel(hopm_kernel<NT>(a.m, a.last, a.c.prelu), dim3(grid), dim3(64 * chain_waves<NT>()), args,
+                         hopm_lds<NT>(a), st);
 }
 template <int NT>
 hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
@@ -1221,15 +1361,16 @@ static const void* kernel_of(int kind, int prelu, int last) {
                    : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
     case 3: return (const void*)k_pool<NT, LOOP>;
     case 5: return (const void*)k_pool_edge<NT>;
-    default: return (const void*)k_hop2<NT>;
+    default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }
 template <int NT>
 int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
-  const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
+  const void* f = kind == 4 ? hopm_kernel<NT>(loop, last, prelu)
+                 : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
-  const int block = 64 * (loop && kind >= 1 && kind <= 3 ? waves_of<NT, true>() : kWaves);
+  const int block = kind == 4 ? 64 * chain_waves<NT>() : 64 * (loop && kind >= 1 && kind <= 3 ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1244,7 +1385,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
-  template hipError_t launch_hop2<NT>(const Hop2Args&, hipStream_t);              \
+  template hipError_t launch_hopm<NT>(const HopMArgs&, hipStream_t);              \
   template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);
 
 }  // namespace msw

@@ -192,13 +192,15 @@ struct ScaleCSR {
   LaneRec* recs = nullptr;      // [ntiles][16]
   int ntiles = 0;
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
-  // hop pairs (engine.h Hop2Args); pair_ok = false -> hops stay one launch each
-  bool pair_ok = false;
-  int pair_blocks = 0, pair_bmax = 0;
-  int* pair_l1_off = nullptr;
-  PairRec* pair_l1 = nullptr;
-  int* pair_a0 = nullptr;
-  int2* pair_l2 = nullptr;
+  // hop chains of m = 2, 3 hops (engine.h HopMArgs), indexed by m; ok = false -> not built
+  struct Chain {
+    bool ok = false;
+    int nblocks = 0, bmax = 0;
+    int lv_base[kChainMax - 1] = {}, lv_tiles[kChainMax - 1] = {};
+    PairRec* lv = nullptr;
+    int* a0 = nullptr;
+    int2* lf = nullptr;
+  } chain[kChainMax + 1];
 };
 
 struct LevelMaps {              // level l: coarse scale l+1, fine scale l
@@ -264,7 +266,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOP2, L_EXCHANGE };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOPM, L_EXCHANGE };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -284,7 +286,7 @@ struct Launch {
     EdgeHopArgs eh;
     HopArgs hop;
     PoolArgs pool;
-    Hop2Args hop2;
+    HopMArgs hopm;
     ExchangeArgs xch;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
@@ -293,7 +295,7 @@ struct Launch {
       case L_ENCODE: return enc.c;
       case L_EDGE_HOP: return eh.c;
       case L_HOP: return hop.c;
-      case L_HOP2: return hop2.c;
+      case L_HOPM: return hopm.c;
       case L_EXCHANGE: return xch.c;
       default: return pool.c;
     }
@@ -319,6 +321,7 @@ struct msw_plan {
   float* dW = nullptr;
   int* perm_d = nullptr;
   int* bc_slot_d = nullptr;
+  float* zrow_d = nullptr;
   std::vector<int> bc_rows_set;
   RolloutIO* io_d = nullptr;
   // O / U / V of consecutive SWEGNN layers alternate between two sets (Proc::par): the
@@ -335,7 +338,12 @@ struct msw_plan {
   int kernels_per_step = 0;
   std::vector<Launch> sched_fwd, sched_roll;  // one forward step: forward / rollout mode
   int use_graph = 1;
-  int hop_pairs = 1;  // fuse hop pairs (MSW_NO_HOP_PAIRS=1 disables, for A/B measurements)
+  // Hop chains (several hops per launch, halo recomputed in LDS) are off by default:
+  // measured on MI355X (graph replay) one launch per hop is 0.7-1.6 % faster on zenodo4,
+  // the batch of 8 and dk15 (profiles/r01_v7/ab_chains.txt).  MSW_HOP_CHAINS=m (2 or 3)
+  // turns chains of up to m hops on.
+  int hop_pairs = 0;
+  int chain_max = kChainMax;
   // partitioned mesh (msw_plan_create_part): per scale, the halo rows received from / the
   // owned rows sent to each peer (internal rows, concatenated in peer order)
   struct XchPeer { int peer, roff, rcount, soff, scount; };
@@ -468,7 +476,7 @@ NpDesc np_none() {
 
 Common common_of(msw_plan* P) {
   Common c{};
-  c.W = P->dW; c.perm = P->perm_d; c.nnf = P->nnf; c.dyn = P->dyn; c.p = P->p;
+  c.W = P->dW; c.perm = P->perm_d; c.nnf = P->nnf; c.dyn = P->dyn; c.p = P->p; c.zrow = P->zrow_d;
   c.nstat_raw = P->nstat_raw; c.with_wl = P->with_wl; c.prelu = P->prelu;
   return c;
 }
@@ -506,6 +514,38 @@ void sched_exchange(msw_plan* P, std::vector<Launch>& q, int scale, std::initial
   q.push_back(L);
 }
 
+// Floats of a launch's epilogue operand region, as Relocator::epi lays it out (before its
+// de-duplication: an upper bound), in whole 1-KB LDS-DMA chunks.
+int epi_floats(const msw_plan* P, const Epilogue& e) {
+  if (P->NT > 2) return 0;  // F = 64: read from the blob in place
+  const int NT = P->NT;
+  int n = 0;
+  auto add = [&](int off, int len) { if (off >= 0) n += (len + 3) & ~3; };
+  add(e.np.a_u, e.np.h1t * 2 * NT * 256);
+  add(e.np.a_v, e.np.h1t * 2 * NT * 256);
+  add(e.np.a_o, NT * NT * 256);
+  add(e.uu_a, e.uu_h1t * 2 * NT * 256);
+  if (e.dec.on) {
+    for (int i = 0; i < e.dec.dec.n; ++i) {
+      add(e.dec.dec.l[i].a_off, e.dec.dec.l[i].tout * e.dec.dec.l[i].tin * 256);
+      add(e.dec.dec.l[i].b_off, 16 * e.dec.dec.l[i].tout);
+    }
+    add(e.dec.resw_off, 2 * P->p);
+  }
+  return (n + 255) / 256 * 256;
+}
+// LDS of an m-hop chain launch on scale g: static slab + epilogue operands + level buffers.
+size_t chain_lds(const msw_plan* P, const ScaleCSR::Chain& ch, int m, int last_floats) {
+  const int WV = P->NT <= 2 ? chain_waves<2>() : chain_waves<4>();
+  const size_t row = (size_t)(16 * P->NT + 4) * sizeof(float);
+  return (size_t)WV * kRowsPerWave * row + (size_t)last_floats * sizeof(float) +
+         (size_t)(m == 3 ? 2 : 1) * ch.bmax * row;
+}
+bool chain_fits(const msw_plan* P, const ScaleCSR& g, int m, bool last, const Epilogue& epi) {
+  if (m < 2 || m > kChainMax || !g.chain[m].ok) return false;
+  return chain_lds(P, g.chain[m], m, last ? epi_floats(P, epi) : 0) <= 160 * 1024;
+}
+
 void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi) {
   const ScaleCSR& g = P->sc[pr.scale];
   const Common c = common_of(P);
@@ -527,40 +567,47 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   eh.epi = epi;
   q.push_back(L1);
   const float* cur = P->T[0];
-  for (int k = 2; k <= pr.K; ++k) {
+  for (int k = 2; k <= pr.K;) {
     sched_exchange(P, q, pr.scale, {{cur == P->T[0] ? B_T0 : B_T1, P->F}});
-    if (g.pair_ok && k + 1 < pr.K) {  // hops k, k+1 in one launch (neither is the last)
-      float* nxt = cur == P->T[0] ? P->T[1] : P->T[0];
-      Launch L;
-      L.kind = L_HOP2;
-      L.scale = pr.scale;
-      Hop2Args& h = L.hop2;
-      h.c = c;
-      h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles; h.l2 = g.pair_l2; h.nblocks = g.pair_blocks;
-      h.l1_off = g.pair_l1_off; h.l1 = g.pair_l1; h.a0 = g.pair_a0; h.bmax = g.pair_bmax;
-      h.s = P->s; h.in = cur; h.out = nxt;
-      h.filt1 = pr.filt.empty() ? -1 : pr.filt[k - 1];
-      h.filt2 = pr.filt.empty() ? -1 : pr.filt[k];
-      h.grad = pr.with_gradient; h.upwind = pr.upwind;
-      q.push_back(L);
-      cur = nxt;
-      ++k;
-      continue;
+    // hops k .. k+m-1 as one chain where the scale has one: the longest that fits, never
+    // leaving a single hop behind it (4 hops -> 2 + 2)
+    const int rem = pr.K - k + 1;
+    int m = 1;
+    for (int mm = std::min({rem, P->chain_max, kChainMax}); mm >= 2; --mm) {
+      if (rem - mm == 1) continue;
+      if (chain_fits(P, g, mm, k + mm - 1 == pr.K, epi)) { m = mm; break; }
     }
-    float* nxt = (k == pr.K) ? out : (cur == P->T[0] ? P->T[1] : P->T[0]);
+    const bool last = k + m - 1 == pr.K;
+    float* nxt = last ? out : (cur == P->T[0] ? P->T[1] : P->T[0]);
     Launch L;
-    L.kind = L_HOP;
     L.scale = pr.scale;
-    HopArgs& h = L.hop;
-    h.c = c;
-    h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
-    h.s = P->s; h.xs = P->xs;
-    h.in = cur; h.out = nxt; h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
-    h.grad = pr.with_gradient; h.upwind = pr.upwind;
-    h.last = k == pr.K;
-    h.epi = epi;
+    if (m >= 2) {
+      const ScaleCSR::Chain& ch = g.chain[m];
+      L.kind = L_HOPM;
+      HopMArgs& h = L.hopm;
+      h.c = c;
+      h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles; h.lf = ch.lf; h.nblocks = ch.nblocks; h.m = m;
+      for (int l = 0; l < kChainMax - 1; ++l) { h.lv_base[l] = ch.lv_base[l]; h.lv_tiles[l] = ch.lv_tiles[l]; }
+      h.lv = ch.lv; h.a0 = ch.a0; h.bmax = ch.bmax;
+      h.s = P->s; h.xs = P->xs; h.in = cur; h.out = nxt;
+      for (int i = 0; i < kChainMax; ++i) h.filt[i] = (i < m && !pr.filt.empty()) ? pr.filt[k - 1 + i] : -1;
+      h.grad = pr.with_gradient; h.upwind = pr.upwind;
+      h.last = last;
+      h.epi = epi;
+    } else {
+      L.kind = L_HOP;
+      HopArgs& h = L.hop;
+      h.c = c;
+      h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
+      h.s = P->s; h.xs = P->xs;
+      h.in = cur; h.out = nxt; h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
+      h.grad = pr.with_gradient; h.upwind = pr.upwind;
+      h.last = last;
+      h.epi = epi;
+    }
     q.push_back(L);
     cur = nxt;
+    k += m;
   }
 }
 
@@ -744,8 +791,16 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       if (a.last) rl.epi(R, a.epi);
       a.reg = R.done(split);
       reg = &a.reg;
-    } else if (L.kind == L_HOP2 || L.kind == L_EXCHANGE) {
+    } else if (L.kind == L_EXCHANGE) {
       continue;  // no LDS weight region
+    } else if (L.kind == L_HOPM) {
+      HopMArgs& a = L.hopm;  // filters stay blob offsets (loaded into registers)
+      if (!a.last) continue;
+      RegionBuilder R(P->blob, 0);
+      rl.epi(R, a.epi);
+      a.reg = R.done();
+      a.wfloats = (a.reg.len + 255) / 256 * 256;
+      reg = &a.reg;
     } else if (L.kind == L_HOP) {
       HopArgs& a = L.hop;
       if (!a.last) continue;  // middle hops load their filter from the blob (k_hop<.., false>)
@@ -788,9 +843,12 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     case L_EDGE_HOP: caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len); break;
     case L_HOP: caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len); break;
-    case L_HOP2:
-      L.hop2.max_blocks = resident_of(P->NT, 4, 0, 0, (size_t)L.hop2.bmax * (16 * P->NT + 4) * 4, 0);
+    case L_HOPM: {
+      HopMArgs& a = L.hopm;
+      const size_t dyn = ((size_t)a.wfloats + (size_t)(a.m == 3 ? 2 : 1) * a.bmax * (16 * P->NT + 4)) * 4;
+      a.max_blocks = resident_of(P->NT, 4, a.c.prelu, a.last, dyn, a.m);
       break;
+    }
     case L_EXCHANGE: break;
     default: {
       // edge tiles while they all fit on the chip at once (latency-bound launch), else rows
@@ -810,7 +868,7 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_ENCODE: return launch_encode<NT>(L.enc, st);
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
-    case L_HOP2: return launch_hop2<NT>(L.hop2, st);
+    case L_HOPM: return launch_hopm<NT>(L.hopm, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
     default: return hipErrorInvalidValue;  // exchanges are run by run_schedule / the group driver
   }
@@ -878,7 +936,7 @@ int schedule_dispatch(msw_plan* P, const std::vector<Launch>& q, hipStream_t st)
 void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
   for (Launch& L : q) {
     if (L.kind == L_ENCODE) L.enc.x = x;
-    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi : nullptr;
+    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi : L.kind == L_HOPM ? &L.hopm.epi : nullptr;
     if (e && e->dec.on) {
       e->dec.X = x;
       e->dec.y = y;
@@ -888,80 +946,112 @@ void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
 
 constexpr int kPairMaxTiles = 1024;
 
-// Level-1 / level-2 structures of the hop-pair kernel for one scale (engine.h Hop2Args).
+// Level structures of the m-hop chain kernel for one scale (engine.h HopMArgs).
 // rowptr / so: the scale's CSR by destination (local rows / internal source rows);
-// pcsr: tile-padded slot -> CSR position.  Leaves pair_ok = false when a workgroup's B set
-// would not fit the LDS budget (the schedule then keeps one launch per hop).
-int build_pairs(msw_plan* P, ScaleCSR& c, const std::vector<int>& rowptr, const std::vector<int>& so,
-                const std::vector<TileRange>& tl, const std::vector<int>& pcsr) {
+// pcsr: tile-padded slot -> CSR position.  Leaves chain[m].ok = false when a workgroup's
+// buffers would not fit the LDS budget (the schedule then uses shorter chains / single hops).
+int build_chain(msw_plan* P, ScaleCSR& c, const std::vector<int>& rowptr, const std::vector<int>& so,
+                const std::vector<TileRange>& tl, const std::vector<int>& pcsr, int m) {
   const int ns = c.ns, n0 = c.n0, nt = (int)tl.size();
   // only where a launch is latency-bound: on larger scales the halo recomputation costs
-  // more than the saved launch (measured: zenodo4 +1 %, batch of 8 / dk15 -2..-4 % when
-  // every scale pairs; the finest zenodo4 scale has ~2k tiles)
+  // more than the saved launch (measured with pairs: zenodo4 +1 %, batch of 8 / dk15
+  // -2..-4 % when every scale pairs; the finest zenodo4 scale has ~2k tiles)
   if (nt == 0 || nt > kPairMaxTiles) return MSW_OK;
   std::vector<int> slot_of_csr(rowptr[ns], -1);
   for (size_t q = 0; q < pcsr.size(); ++q)
     if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
   const int nb = (nt + kWaves - 1) / kWaves;
-  std::vector<int> stamp(ns, -1), bidx(ns, -1), B, l1_off(nb + 1, 0), a0(nb);
-  std::vector<PairRec> l1;
-  std::vector<int2> l2((size_t)nt * kRowsPerWave, int2{0, 0});
+  std::vector<int> stamp(ns, -1), idx(ns, -1), D, a0(nb);
+  std::vector<std::vector<int>> lvt_off(m - 1, std::vector<int>(nb + 1, 0));
+  std::vector<std::vector<PairRec>> lvt(m - 1);  // per level, tiles of every block
+  std::vector<int> lsize(m);                     // |D_l|, l = 1 .. m-1 (index 0 unused)
+  std::vector<int2> lf((size_t)nt * kRowsPerWave, int2{0, 0});
   int bmax = 0;
   for (int b = 0; b < nb; ++b) {
     const int t0 = b * kWaves, t1 = std::min(t0 + kWaves, nt);
     const int abeg = tl[t0].node0, aend = tl[t1 - 1].node0 + tl[t1 - 1].nnode;
-    B.clear();
-    for (int v = abeg; v < aend; ++v) { stamp[v] = b; bidx[v] = (int)B.size(); B.push_back(v); }
-    for (int v = abeg; v < aend; ++v)
-      for (int i = rowptr[v]; i < rowptr[v + 1]; ++i) {
-        const int u = so[i] - n0;
-        if (stamp[u] != b) { stamp[u] = b; bidx[u] = (int)B.size(); B.push_back(u); }
+    // D_m = A, D_{l-1} = D_l + in-neighbours of D_l: index = position in D_1 (prefixes)
+    D.clear();
+    for (int v = abeg; v < aend; ++v) { stamp[v] = b; idx[v] = (int)D.size(); D.push_back(v); }
+    size_t ring0 = 0;
+    for (int l = m - 1; l >= 1; --l) {
+      const size_t ring1 = D.size();
+      for (size_t i0 = ring0; i0 < ring1; ++i0) {
+        const int v = D[i0];
+        for (int i = rowptr[v]; i < rowptr[v + 1]; ++i) {
+          const int u = so[i] - n0;
+          if (stamp[u] != b) { stamp[u] = b; idx[u] = (int)D.size(); D.push_back(u); }
+        }
       }
-    bmax = std::max(bmax, (int)B.size());
-    a0[b] = abeg;
-    // level-1 tiles over B: whole in-neighbourhoods, <= 16 edges and <= 16 nodes each
-    l1_off[b] = (int)(l1.size() / kRowsPerWave);
-    size_t tbase = l1.size();
-    int nn = 0, ne = 0;
-    auto open_tile = [&]() {
-      tbase = l1.size();
-      l1.resize(tbase + kRowsPerWave, PairRec{-1, 0, 0, -1, 0, 0, 0, 0});
-      nn = ne = 0;
-    };
-    open_tile();
-    for (int v : B) {
-      const int d = rowptr[v + 1] - rowptr[v];
-      if (d > kRowsPerWave) return fail(MSW_ERR_UNSUPPORTED, "node with more than 16 in-edges");
-      if (nn == kRowsPerWave || ne + d > kRowsPerWave) open_tile();
-      PairRec* T = &l1[tbase];
-      T[nn].n = n0 + v;
-      T[nn].bl = bidx[v];
-      T[nn].q = ne | ((ne + d) << 8);
-      for (int i = rowptr[v]; i < rowptr[v + 1]; ++i, ++ne) {
-        T[ne].src = so[i];
-        T[ne].p = slot_of_csr[i];
-        T[ne].dl = nn;
-      }
-      ++nn;
+      // all in-neighbours of D_{l+1} are now in: D_l = D[0 .. size)
+      lsize[l] = (int)D.size();
+      ring0 = ring1;
+      // (the in-neighbours of nodes added before ring0 were added in an earlier pass)
     }
-    // level 2: B rows of each edge slot of the workgroup's own tiles
+    bmax = std::max(bmax, (int)D.size());
+    a0[b] = abeg;
+    // level l tiles over D_l: whole in-neighbourhoods, <= 16 edges and <= 16 nodes each
+    for (int l = 1; l < m; ++l) {
+      std::vector<PairRec>& T = lvt[l - 1];
+      lvt_off[l - 1][b] = (int)(T.size() / kRowsPerWave);
+      size_t tbase = T.size();
+      int nn = 0, ne = 0;
+      auto open_tile = [&]() {
+        tbase = T.size();
+        T.resize(tbase + kRowsPerWave, PairRec{-1, 0, 0, -1, 0, 0, 0, 0});
+        nn = ne = 0;
+      };
+      open_tile();
+      for (int di = 0; di < lsize[l]; ++di) {
+        const int v = D[di];
+        const int d = rowptr[v + 1] - rowptr[v];
+        if (d > kRowsPerWave) return fail(MSW_ERR_UNSUPPORTED, "node with more than 16 in-edges");
+        if (nn == kRowsPerWave || ne + d > kRowsPerWave) open_tile();
+        PairRec* R = &T[tbase];
+        R[nn].n = l == 1 ? n0 + v : idx[v];
+        R[nn].bl = idx[v];
+        R[nn].q = ne | ((ne + d) << 8);
+        for (int i = rowptr[v]; i < rowptr[v + 1]; ++i, ++ne) {
+          R[ne].src = l == 1 ? so[i] : idx[so[i] - n0];
+          R[ne].p = slot_of_csr[i];
+          R[ne].dl = nn;
+        }
+        ++nn;
+      }
+    }
+    // final level: set indices of each edge slot of the workgroup's own tiles
     for (int t = t0; t < t1; ++t)
       for (int jn = 0; jn < tl[t].nnode; ++jn) {
         const int v = tl[t].node0 + jn;
         for (int i = rowptr[v]; i < rowptr[v + 1]; ++i)
-          l2[(size_t)t * kRowsPerWave + (i - tl[t].edge0)] = int2{bidx[so[i] - n0], bidx[v]};
+          lf[(size_t)t * kRowsPerWave + (i - tl[t].edge0)] = int2{idx[so[i] - n0], idx[v]};
       }
   }
-  l1_off[nb] = (int)(l1.size() / kRowsPerWave);
-  const size_t lds = (size_t)bmax * (16 * P->NT + 4) * sizeof(float);
-  if (lds > 64 * 1024) return MSW_OK;  // B too large for LDS: no pairs on this scale
+  for (int l = 1; l < m; ++l) lvt_off[l - 1][nb] = (int)(lvt[l - 1].size() / kRowsPerWave);
+  // fixed stride per level: block b's tiles of level l at lv_base + b * lv_tiles (padded
+  // with empty tiles), so a kernel finds them without loading an offset first
+  ScaleCSR::Chain& ch = c.chain[m];
+  std::vector<PairRec> lv;
+  for (int l = 1; l < m; ++l) {
+    const std::vector<int>& off = lvt_off[l - 1];
+    int tmax = 1;
+    for (int b = 0; b < nb; ++b) tmax = std::max(tmax, off[b + 1] - off[b]);
+    ch.lv_base[l - 1] = (int)(lv.size() / kRowsPerWave);
+    ch.lv_tiles[l - 1] = tmax;
+    for (int b = 0; b < nb; ++b) {
+      const auto& T = lvt[l - 1];
+      lv.insert(lv.end(), T.begin() + (size_t)off[b] * kRowsPerWave, T.begin() + (size_t)off[b + 1] * kRowsPerWave);
+      lv.resize(lv.size() + (size_t)(tmax - (off[b + 1] - off[b])) * kRowsPerWave, PairRec{-1, 0, 0, -1, 0, 0, 0, 0});
+    }
+  }
+  ch.nblocks = nb;
+  ch.bmax = bmax;
+  if (chain_lds(P, ch, m, 0) > 160 * 1024) return MSW_OK;  // buffers too large: no chain of m here
   int rc;
-  if ((rc = pupload(P, &c.pair_l1_off, l1_off)) || (rc = pupload(P, &c.pair_l1, l1)) ||
-      (rc = pupload(P, &c.pair_a0, a0)) || (rc = pupload(P, &c.pair_l2, l2)))
+  if ((rc = pupload(P, &ch.lv, lv)) || (rc = pupload(P, &ch.a0, a0)) ||
+      (rc = pupload(P, &ch.lf, lf)))
     return rc;
-  c.pair_blocks = nb;
-  c.pair_bmax = bmax;
-  c.pair_ok = true;
+  ch.ok = true;
   return MSW_OK;
 }
 
@@ -1031,7 +1121,8 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     for (size_t q = 0; q < pcsr.size(); ++q)
       if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
     if ((rc = pupload(P, &c.recs, recs))) return rc;
-    if (P->hop_pairs && (rc = build_pairs(P, c, rowptr, so, tl, pcsr))) return rc;
+    for (int m = 2; P->hop_pairs && m <= P->chain_max; ++m)
+      if ((rc = build_chain(P, c, rowptr, so, tl, pcsr, m))) return rc;
   }
   // intra-scale levels
   P->lv.assign(S > 1 ? S - 1 : 0, LevelMaps{});
@@ -1093,7 +1184,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
 int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
   if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
   if (P->sched_roll.empty()) return fail(MSW_ERR_INVALID, "run a rollout before bench_kernel");
-  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP, L_HOP2};
+  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP, L_HOPM};
   if (kernel < 0 || kernel > 5) return fail(MSW_ERR_INVALID, "unknown kernel id");
   const bool unpool = kernel == 4;  // the intra-scale (unpooling) layer into `scale`
   const Launch* src = nullptr;
@@ -1109,6 +1200,7 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
   const ScaleCSR& g = P->sc[scale];
   int64_t rows = g.ns, edges = g.E;
   if (L.kind == L_HOP && L.hop.last) { L.hop.last = 0; L.hop.out = P->T[1]; }
+  if (L.kind == L_HOPM && L.hopm.last) { L.hopm.last = 0; L.hopm.out = P->T[1]; L.hopm.wfloats = 0; }
   if (L.kind == L_EDGE_HOP && L.eh.last && !unpool) { L.eh.last = 0; L.eh.out = P->T[1]; }
   if (unpool) edges = P->lv[scale].I;  // the unpool epilogue only writes the next layer's U/V/O
   if (L.kind == L_POOL) edges = P->lv[scale - 1].I;
@@ -1224,7 +1316,10 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     return fail(MSW_ERR_INVALID, "MSGNN needs S-1 intra-scale layers");
   if (m->model_type == 1 && m->num_processors < 1) return fail(MSW_ERR_INVALID, "GNN needs >= 1 layer");
 
-  P->hop_pairs = getenv("MSW_NO_HOP_PAIRS") || xch ? 0 : 1;  // a pair's halo is two rings deep
+  if (const char* cm = getenv("MSW_HOP_CHAINS")) {  // a chain's halo is m-1 rings deep: not on parts
+    P->chain_max = std::max(2, std::min(kChainMax, atoi(cm)));
+    P->hop_pairs = xch ? 0 : 1;
+  }
   P->part_rank = xch ? rank : -1;
   int rc = build_graph_plan(P.get(), g);
   if (rc) return rc;
@@ -1281,6 +1376,7 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
 
   // ---- device buffers
   if ((rc = pupload(P.get(), &P->perm_d, P->perm))) return rc;
+  if ((rc = pupload(P.get(), &P->zrow_d, std::vector<float>(kZeroRow, 0.f)))) return rc;
   std::vector<int> minus1(Npad, -1);
   if ((rc = pupload(P.get(), &P->bc_slot_d, minus1))) return rc;
   if ((rc = palloc(P.get(), &P->io_d, 1))) return rc;

@@ -82,6 +82,23 @@ def test_rollout48_vs_reference(cuda, ck, K, F):
     assert st["rollout_steps"] >= 48
 
 
+@pytest.mark.parametrize("chain", ["2", "3"])
+def test_hop_chains_match_single_hops(cuda, chain, monkeypatch):
+    """Opt-in hop chains (MSW_HOP_CHAINS, several hops per launch with the halo recomputed
+    in LDS) against the reference fixture and the default one-launch-per-hop schedule."""
+    fx = golden("fx_small_K4_F32_rollout48")
+    g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+    base = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    r0 = base.rollout(g).cpu()
+    n0 = _stats(base, g)["kernels_per_step"]
+    monkeypatch.setenv("MSW_HOP_CHAINS", chain)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    r = m.rollout(g).cpu()
+    assert _stats(m, g)["kernels_per_step"] < n0  # the chains were scheduled
+    assert per_step_rel(r, torch.from_numpy(fx["rollout"])) <= REL_TOL
+    assert per_step_rel(r, r0) <= 1e-6
+
+
 def test_rollout_zenodo_size_vs_reference(cuda):
     fx = golden("fx_zenodo4_K4_F32_rollout48")
     g = make_multiscale_mesh(**mesh_config("zenodo4"), T=48).to(cuda)

@@ -41,7 +41,7 @@ def main():
     S = desc["num_scales"]
     cases = [("encode", 0)] + [(k, s) for s in range(S) for k in ("edge_hop", "hop")] + \
         [("pool", s) for s in range(1, S)] + [("unpool", s) for s in range(S - 1)] + \
-        [("hop2", s) for s in range(1, S)]
+        [("hop2", s) for s in range(1, S)] + [("hop", s) for s in range(S)]
     for kern, scale in cases:
         try:
             for rep in range(3):  # the last repetition is reported (warm caches)
