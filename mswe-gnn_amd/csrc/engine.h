@@ -252,6 +252,22 @@ struct PoolArgs {
   NpDesc np;
 };
 
+// Epilogue of a layer's last hop on dense 16-row node tiles (large scales, plan.hip
+// sched_proc): the hop runs as a middle hop and stores its result rows (before post_act);
+// this launch applies what follows the hop (node_epilogue) to rows [n0, n0 + ns).  An edge
+// tile holds ~5 destinations of its <= 16 rows on a triangular mesh, so the epilogue's
+// MFMA chains (projections, decoder) run on 3x fewer tiles here.
+struct EpiArgs {
+  Common c;
+  WReg reg;                // epilogue operands (LDS region)
+  int max_blocks, fit_blocks;
+  int n0, ns, ntiles;      // ntiles = ceil(ns / 16)
+  const float* in;         // the last hop's result rows
+  const float* xs;
+  float* out;              // the layer's output rows (may be `in`, or null)
+  Epilogue epi;
+};
+
 struct InitArgs {
   const float* x0; const int* perm; int N, nnf, dyn, p;
   float* X;
@@ -287,13 +303,15 @@ hipError_t launch_copy_rows(const float* src, const int* srows, float* dst, cons
 
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
 template <int NT> hipError_t prepare_kernels();
-// kind 0 encode, 1 edge_hop, 2 hop, 3 pool, 4 hop chain (last: 0/1, loop = M), 5 pool edge tiles
+// kind 0 encode, 1 edge_hop, 2 hop, 3 pool, 4 hop chain (last: 0/1, loop = M), 5 pool edge
+// tiles, 6 row epilogue
 template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop);
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hopm(const HopMArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_epi(const EpiArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);
 
 }  // namespace msw

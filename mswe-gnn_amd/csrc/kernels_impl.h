@@ -1178,6 +1178,72 @@ __global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- row epilogue
+// engine.h EpiArgs: what follows a layer's last hop, on dense node tiles -- tile t = rows
+// n0 + 16t .. n0 + 16t + 15, lane (row j, group g) -- instead of on the hop's edge tiles.
+// Same operations in the same order as the hop's own epilogue (bit-identical results).
+// LOOP: weights staged once per workgroup, the next tile's rows in flight while a tile
+// computes.
+template <int NT, int ACT, bool LOOP>
+__global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_epi(EpiArgs a) {
+#pragma clang fp contract(off)
+  constexpr int WV = waves_of<NT, LOOP>();
+  constexpr int F = 16 * NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int stride = gridDim.x * WV;
+  int tile = blockIdx.x * WV + w;
+  Common c = a.c;
+  MSW_MARK(c, 0);
+  struct Rows {
+    f32x4 res[NT];
+    EpiPre<NT> pre;
+    int n;
+    bool nv;
+  };
+  auto load = [&](Rows& r, int t, int j, int g) {
+    const int i = 16 * t + j;
+    r.nv = i < a.ns;
+    r.n = a.n0 + (r.nv ? i : 0);
+    load_row<NT>(r.res, a.in + (size_t)r.n * F, g);
+    epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, (size_t)r.n, g);
+  };
+  if constexpr (!LOOP) {
+    Rows r0;
+    load(r0, tile < a.ntiles ? tile : 0, j, g);
+    MSW_MARK(c, 1);
+    if constexpr (kStaged<NT>) {
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      c.W = smem;
+    }
+    MSW_MARK(c, 2);
+    if (tile < a.ntiles) node_epilogue<NT, ACT>(r0.res, a.epi, c, r0.pre, a.out, r0.n, r0.nv, lane, g);
+  } else {
+    if constexpr (kStaged<NT>) {
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      c.W = smem;
+    }
+    if (tile < a.ntiles) {
+      Rows q;
+      load(q, tile, j, g);
+      for (;;) {
+        const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+        const int t1 = tile + stride;
+        const bool more = t1 < a.ntiles;
+        Rows qn;
+        if (more) load(qn, t1, jj, gg);
+        node_epilogue<NT, ACT>(q.res, a.epi, c, q.pre, a.out, q.n, q.nv, ln, gg);
+        if (!more) break;
+        q = qn;
+        tile = t1;
+      }
+    }
+  }
+  MSW_MARK(c, 9);
+}
+
 // ---------------------------------------------------------------------------- plan time
 // MODE 0: edge encoder chain (raw <= 16 features -> F -> ... -> F);
 // MODE 1: edge part of a SWEGNN layer's first layer, Pe = W1[:, 4F:] e + b1 (F -> 2F).
@@ -1240,7 +1306,9 @@ hipError_t prepare_kernels() {
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
       {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
-      {(const void*)k_pool_edge<NT>, kWaves}};
+      {(const void*)k_pool_edge<NT>, kWaves},
+      {(const void*)k_epi<NT, 1, false>, kWaves}, {(const void*)k_epi<NT, -1, false>, kWaves},
+      {(const void*)k_epi<NT, 1, true>, WL}, {(const void*)k_epi<NT, -1, true>, WL}};
   for (const auto& f : fns) {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
@@ -1341,6 +1409,21 @@ hipError_t launch_hopm(const HopMArgs& a, hipStream_t st) {
                          hopm_lds<NT>(a), st);
 }
 template <int NT>
+hipError_t launch_epi(const EpiArgs& a, hipStream_t st) {
+  if (a.ntiles <= 0) return hipSuccess;
+  const bool loop = tile_loop(a);
+  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  const size_t sh = lds_bytes<NT>(a.reg.len);
+  if (a.c.prelu) {
+    if (loop) hipLaunchKernelGGL((k_epi<NT, 1, true>), grid, block, sh, st, a);
+    else hipLaunchKernelGGL((k_epi<NT, 1, false>), grid, block, sh, st, a);
+  } else {
+    if (loop) hipLaunchKernelGGL((k_epi<NT, -1, true>), grid, block, sh, st, a);
+    else hipLaunchKernelGGL((k_epi<NT, -1, false>), grid, block, sh, st, a);
+  }
+  return hipGetLastError();
+}
+template <int NT>
 hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
   if (a.R <= 0) return hipSuccess;
   if (a.mode == 1)
@@ -1361,6 +1444,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
                    : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
     case 3: return (const void*)k_pool<NT, LOOP>;
     case 5: return (const void*)k_pool_edge<NT>;
+    case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }
@@ -1370,7 +1454,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
-  const int block = kind == 4 ? 64 * chain_waves<NT>() : 64 * (loop && kind >= 1 && kind <= 3 ? waves_of<NT, true>() : kWaves);
+  const int block = kind == 4 ? 64 * chain_waves<NT>() : 64 * (loop && ((kind >= 1 && kind <= 3) || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1386,6 +1470,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
   template hipError_t launch_hopm<NT>(const HopMArgs&, hipStream_t);              \
+  template hipError_t launch_epi<NT>(const EpiArgs&, hipStream_t);                \
   template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);
 
 }  // namespace msw

@@ -266,7 +266,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOPM, L_EXCHANGE };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOPM, L_EXCHANGE, L_EPI };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -288,6 +288,7 @@ struct Launch {
     PoolArgs pool;
     HopMArgs hopm;
     ExchangeArgs xch;
+    EpiArgs ep;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
   Common& common() {
@@ -297,6 +298,7 @@ struct Launch {
       case L_HOP: return hop.c;
       case L_HOPM: return hopm.c;
       case L_EXCHANGE: return xch.c;
+      case L_EPI: return ep.c;
       default: return pool.c;
     }
   }
@@ -344,6 +346,10 @@ struct msw_plan {
   // turns chains of up to m hops on.
   int hop_pairs = 0;
   int chain_max = kChainMax;
+  // A layer's last hop on a scale with at least this many edge tiles runs as a middle hop
+  // + a row epilogue launch (engine.h EpiArgs); MSW_EPI_SPLIT_TILES overrides (0: never).
+  // Measured on MI355X (profiles/r01_v7/ab_epi_split.txt).
+  int epi_split_tiles = 8192;
   // partitioned mesh (msw_plan_create_part): per scale, the halo rows received from / the
   // owned rows sent to each peer (internal rows, concatenated in peer order)
   struct XchPeer { int peer, roff, rcount, soff, scount; };
@@ -595,15 +601,35 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
       h.last = last;
       h.epi = epi;
     } else {
+      // the last hop of a large scale: a middle hop into the free ping-pong buffer, then
+      // the epilogue on dense node tiles (not on parts: their schedules must stay equal)
+      // (only an epilogue with MFMA work gains: a bare store of the layer's output costs a
+      // whole extra pass over the rows)
+      const bool mfma_epi = epi.np.a_u >= 0 || epi.np.a_v >= 0 || epi.np.a_o >= 0 || epi.uu_a >= 0 || epi.dec.on;
+      const bool split = last && mfma_epi && P->part_rank < 0 && P->epi_split_tiles > 0 &&
+                         g.ntiles >= P->epi_split_tiles;
       L.kind = L_HOP;
       HopArgs& h = L.hop;
       h.c = c;
       h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
       h.s = P->s; h.xs = P->xs;
-      h.in = cur; h.out = nxt; h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
+      h.in = cur; h.out = split ? (cur == P->T[0] ? P->T[1] : P->T[0]) : nxt;
+      h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
       h.grad = pr.with_gradient; h.upwind = pr.upwind;
-      h.last = last;
+      h.last = last && !split;
       h.epi = epi;
+      if (split) {
+        q.push_back(L);
+        Launch LE;
+        LE.kind = L_EPI;
+        LE.scale = pr.scale;
+        EpiArgs& ea = LE.ep;
+        ea.c = c;
+        ea.n0 = g.n0; ea.ns = g.ns; ea.ntiles = (g.ns + kRowsPerWave - 1) / kRowsPerWave;
+        ea.in = h.out; ea.xs = P->xs; ea.out = nxt;
+        ea.epi = epi;
+        L = LE;
+      }
     }
     q.push_back(L);
     cur = nxt;
@@ -793,6 +819,12 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       reg = &a.reg;
     } else if (L.kind == L_EXCHANGE) {
       continue;  // no LDS weight region
+    } else if (L.kind == L_EPI) {
+      EpiArgs& a = L.ep;
+      RegionBuilder R(P->blob, 0);
+      rl.epi(R, a.epi);
+      a.reg = R.done();
+      reg = &a.reg;
     } else if (L.kind == L_HOPM) {
       HopMArgs& a = L.hopm;  // filters stay blob offsets (loaded into registers)
       if (!a.last) continue;
@@ -850,6 +882,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     }
     case L_EXCHANGE: break;
+    case L_EPI: caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len); break;
     default: {
       // edge tiles while they all fit on the chip at once (latency-bound launch), else rows
       PoolArgs& a = L.pool;
@@ -870,6 +903,7 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_HOP: return launch_hop<NT>(L.hop, st);
     case L_HOPM: return launch_hopm<NT>(L.hopm, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
+    case L_EPI: return launch_epi<NT>(L.ep, st);
     default: return hipErrorInvalidValue;  // exchanges are run by run_schedule / the group driver
   }
 }
@@ -936,7 +970,8 @@ int schedule_dispatch(msw_plan* P, const std::vector<Launch>& q, hipStream_t st)
 void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
   for (Launch& L : q) {
     if (L.kind == L_ENCODE) L.enc.x = x;
-    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi : L.kind == L_HOPM ? &L.hopm.epi : nullptr;
+    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi : L.kind == L_HOPM ? &L.hopm.epi
+                 : L.kind == L_EPI ? &L.ep.epi : nullptr;
     if (e && e->dec.on) {
       e->dec.X = x;
       e->dec.y = y;
@@ -1316,6 +1351,7 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     return fail(MSW_ERR_INVALID, "MSGNN needs S-1 intra-scale layers");
   if (m->model_type == 1 && m->num_processors < 1) return fail(MSW_ERR_INVALID, "GNN needs >= 1 layer");
 
+  if (const char* es = getenv("MSW_EPI_SPLIT_TILES")) P->epi_split_tiles = atoi(es);
   if (const char* cm = getenv("MSW_HOP_CHAINS")) {  // a chain's halo is m-1 rings deep: not on parts
     P->chain_max = std::max(2, std::min(kChainMax, atoi(cm)));
     P->hop_pairs = xch ? 0 : 1;

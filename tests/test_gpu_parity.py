@@ -99,6 +99,40 @@ def test_hop_chains_match_single_hops(cuda, chain, monkeypatch):
     assert per_step_rel(r, r0) <= 1e-6
 
 
+@pytest.mark.parametrize("model", ["msgnn_K4_F32", "msgnn_K2_F16", "gnn"])
+def test_row_epilogue_split_matches_fused(cuda, model, monkeypatch):
+    """Last hop + row epilogue launch (engine.h EpiArgs; forced on every scale with
+    MSW_EPI_SPLIT_TILES=1) == the hop's fused epilogue, bit for bit, forward and rollout,
+    and against the reference fixtures."""
+    def build():
+        if model == "gnn":
+            return _hip(build_gnn(state=weights("gnn_F32_seed42")), cuda)
+        ck, K, F = {"msgnn_K4_F32": ("K4_F32", 4, 32), "msgnn_K2_F16": ("K2_F16", 2, 16)}[model]
+        return _hip(build_msgnn(4, F, K, state=weights(ck)), cuda)
+    if model == "gnn":
+        fx = golden("fx_gnn_small_rollout10")
+        g = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=10), seed=2).to(cuda)
+        T = 10
+    else:
+        fx = golden(f"fx_small_{model[6:]}_rollout48")
+        g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+        T = 48
+    base = build()
+    with torch.no_grad():
+        y0 = base(g).cpu()
+    r0 = base.rollout(g, T).cpu()
+    n0 = _stats(base, g)["kernels_per_step"]
+    monkeypatch.setenv("MSW_EPI_SPLIT_TILES", "1")
+    m = build()
+    with torch.no_grad():
+        y = m(g).cpu()
+    r = m.rollout(g, T).cpu()
+    assert _stats(m, g)["kernels_per_step"] > n0  # the row epilogues were scheduled
+    assert torch.equal(y, y0)
+    assert torch.equal(r, r0)
+    assert per_step_rel(r, torch.from_numpy(fx["rollout"])) <= REL_TOL
+
+
 def test_rollout_zenodo_size_vs_reference(cuda):
     fx = golden("fx_zenodo4_K4_F32_rollout48")
     g = make_multiscale_mesh(**mesh_config("zenodo4"), T=48).to(cuda)
