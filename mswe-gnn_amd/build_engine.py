@@ -27,7 +27,8 @@ def _newer(a, b):
 def build(force=False, verbose=True, variant=""):
     """variant "trace": diagnostic library lib/libmswegnn_trace.so (-DMSW_TRACE)."""
     odir = os.path.join(HERE, "_obj" + (f"_{variant}" if variant else ""))
-    extra = {"trace": ["-DMSW_TRACE"], "w8": ["-DMSW_WAVES=8"], "w2": ["-DMSW_WAVES=2"]}.get(variant, [])
+    extra = {"trace": ["-DMSW_TRACE"], "w8": ["-DMSW_WAVES=8"], "w2": ["-DMSW_WAVES=2"],
+             "ew8": ["-DMSW_EDGE_WAVES=8"], "ew4": ["-DMSW_EDGE_WAVES=4"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     objs, cmds = [], []
@@ -57,4 +58,5 @@ def build(force=False, verbose=True, variant=""):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, variant="trace" if "--trace" in sys.argv else "")
+    var = [a[len("--variant="):] for a in sys.argv if a.startswith("--variant=")]
+    build(force="--force" in sys.argv, variant="trace" if "--trace" in sys.argv else (var[0] if var else ""))

@@ -155,7 +155,8 @@ struct EdgeHopArgs {
   const float* in;                 // out_0 rows [Npad][F]
   int own_zero;                    // destination rows read as zero (intra_scale_gnn)
   int grad, upwind;
-  int filt_a;                      // packed filter W_1, -1 = none
+  int filt_a;                      // packed filter W_1, -1 = none (blob offset)
+  int filt_l;                      // the same operand in the launch's LDS region (grid-stride variant)
   const float* skip;               // + skip rows (unpool), or null
   float* out;                      // out_1 rows, or null
   int last;                        // last hop of the layer: run the epilogue

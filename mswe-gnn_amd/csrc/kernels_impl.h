@@ -30,6 +30,14 @@ constexpr int kBlock = 64 * kWaves;
 // staging traffic of a large mesh and the LDS the copies take.
 template <int NT, bool LOOP>
 constexpr int waves_of() { return LOOP && NT <= 2 ? 8 : kWaves; }
+// the fused edge MLP + hop keeps one tile per wave in flight in its grid-stride loop:
+// a software-pipelined loop (next tile's gathers during the MLP) needs > 256 registers,
+// i.e. one wave per SIMD, and measured 24 % slower on the 1M-node mesh
+#ifndef MSW_EDGE_WAVES
+#define MSW_EDGE_WAVES 12
+#endif
+template <int NT, bool LOOP>
+constexpr int edge_waves() { return LOOP && NT <= 2 ? MSW_EDGE_WAVES : kWaves; }
 
 #define MSW_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
@@ -577,10 +585,19 @@ struct EdgeHopRows {  // everything one tile reads from HBM
   f32x4 Us[2 * NT], Ps[2 * NT], Vn[2 * NT], os[NT], inn[NT], sk[NT];
   EpiPre<NT> pre;  // a.last only
 };
+// NODE = false leaves the rows needed only after the MLP (skip, epilogue inputs) to
+// edge_hop_node (the pipelined loop issues them when the tile starts computing).
 template <int NT>
-__device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
+__device__ __forceinline__ void edge_hop_node(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int g) {
+  constexpr int F = 16 * NT;
+  load_row<NT>(r.sk, a.skip ? a.skip + r.L.n * F : a.c.zrow, g);
+  if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, r.L.n, g);
+}
+template <int NT, bool NODE = true>
+__device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHopArgs& a, const LaneRec& rec,
+                                                int tile, int j, int g) {
   constexpr int F = 16 * NT, T2 = 2 * NT;
-  r.L = lanes_of(load_rec(a.recs, tile, j), tile, j, a.n0);
+  r.L = lanes_of(rec, tile, j, a.n0);
   const Lanes& L = r.L;
   const int hs = 16 * a.h1t;
   const float* z = a.c.zrow;
@@ -597,10 +614,13 @@ __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopA
   }
   load_row<NT>(r.os, a.in + L.sr * F, g);
   load_row<NT>(r.inn, a.own_zero ? z : a.in + L.n * F, g);
-  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
-  if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
+  if constexpr (NODE) edge_hop_node<NT>(r, a, g);
 }
-template <int NT, int ACT, int XS>
+template <int NT>
+__device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
+  edge_hop_gather<NT>(r, a, load_rec(a.recs, tile, j), tile, j, g);
+}
+template <int NT, int ACT, int XS, bool FREG = true>
 __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
                                               const f32x4 (&wf)[NT][NT], float* slab, int j, int lane, int g,
                                               f32x4 (&res_out)[NT]) {
@@ -654,7 +674,10 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
   MSW_MARK(c, 7);
 #pragma unroll
   for (int t = 0; t < NT; ++t) res[t] = r.inn[t];
-  apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+  if constexpr (FREG)
+    apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+  else  // filter operand in the staged LDS region (fewer live registers in the loop)
+    apply_filter<NT>(res, agg, a.filt_l, c.W, lane);
   MSW_MARK(c, 8);
   if (a.skip) {
 #pragma unroll
@@ -675,8 +698,8 @@ __device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const EdgeHopR
   }
 }
 template <int NT, int ACT, bool LOOP>
-__global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_edge_hop(EdgeHopArgs a) {
-  constexpr int WV = waves_of<NT, LOOP>();
+__global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgpu_waves_per_eu(LOOP && MSW_EDGE_WAVES % 3 == 0 ? 3 : 1))) void k_edge_hop(EdgeHopArgs a) {
+  constexpr int WV = edge_waves<NT, LOOP>();
   // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
   constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
   __shared__ __attribute__((aligned(16))) float slab[WV][kRowsPerWave][XS];
@@ -687,7 +710,8 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_edge_hop(EdgeHo
   Common c = a.c;
   MSW_MARK(c, 0);
   f32x4 wf[NT][NT];
-  load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
+  if constexpr (!LOOP || !kStaged<NT>)
+    load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
   if constexpr (!LOOP) {
     const bool live = tile < a.ntiles;
     EdgeHopRows<NT> r;
@@ -718,7 +742,7 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_edge_hop(EdgeHo
       EdgeHopRows<NT> q;
       edge_hop_load<NT>(q, a, tile, jj, gg);
       f32x4 res[NT];
-      edge_hop_core<NT, ACT, XS>(q, a, c, wf, &slab[w][0][0], jj, ln, gg, res);
+      edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, wf, &slab[w][0][0], jj, ln, gg, res);
       edge_hop_finish<NT, ACT>(res, q, a, c, ln, gg);
     }
   }
@@ -1302,7 +1326,8 @@ hipError_t prepare_kernels() {
   const std::pair<const void*, int> fns[] = {
       {(const void*)k_encode<NT, 1>, kWaves}, {(const void*)k_encode<NT, -1>, kWaves},
       {(const void*)k_edge_hop<NT, 1, false>, kWaves}, {(const void*)k_edge_hop<NT, -1, false>, kWaves},
-      {(const void*)k_edge_hop<NT, 1, true>, WL}, {(const void*)k_edge_hop<NT, -1, true>, WL},
+      {(const void*)k_edge_hop<NT, 1, true>, edge_waves<NT, true>()},
+      {(const void*)k_edge_hop<NT, -1, true>, edge_waves<NT, true>()},
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
       {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
@@ -1352,7 +1377,7 @@ template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  const dim3 grid(tile_grid(a)), block(64 * (loop ? edge_waves<NT, true>() : kWaves));
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (a.c.prelu) {
     if (loop) hipLaunchKernelGGL((k_edge_hop<NT, 1, true>), grid, block, sh, st, a);
@@ -1454,7 +1479,9 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
-  const int block = kind == 4 ? 64 * chain_waves<NT>() : 64 * (loop && ((kind >= 1 && kind <= 3) || kind == 6) ? waves_of<NT, true>() : kWaves);
+  const int block = kind == 4 ? 64 * chain_waves<NT>()
+                    : kind == 1 ? 64 * (loop ? edge_waves<NT, true>() : kWaves)
+                    : 64 * (loop && (kind == 2 || kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

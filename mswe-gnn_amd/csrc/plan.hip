@@ -812,7 +812,10 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       EdgeHopArgs& a = L.eh;
       RegionBuilder R(P->blob, 0);
       a.b1_off = R.put(a.b1_off, 16 * a.h1t);
-      rl.mlp(R, a.rest);  // filt_a stays a blob offset: k_edge_hop loads it into registers
+      rl.mlp(R, a.rest);
+      // filt_a stays a blob offset (the one-tile-per-wave variant loads it into registers);
+      // the grid-stride variant reads the region's copy from LDS
+      a.filt_l = R.put(a.filt_a, P->NT * P->NT * 256);
       const int split = R.pos();  // operands after this one stream in behind the MLP
       if (a.last) rl.epi(R, a.epi);
       a.reg = R.done(split);
@@ -868,13 +871,25 @@ void caps(msw_plan* P, A& a, int kind, int prelu, int last, int floats) {
   a.max_blocks = resident_of(P->NT, kind, prelu, last, (size_t)floats * 4, 1);
   a.fit_blocks = resident_of(P->NT, kind, prelu, last, (size_t)floats * 4, 0);
 }
+// A/B measurements: MSW_NO_LOOP=eh,hop,epi,all keeps those launches one tile per wave at
+// any size (no grid-stride loop).
+bool no_loop(const char* kind) {
+  const char* e = getenv("MSW_NO_LOOP");
+  return e && (strstr(e, kind) || strstr(e, "all"));
+}
 void set_grid_cap(msw_plan* P, Launch& L) {
   switch (L.kind) {
     case L_ENCODE:
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
       break;
-    case L_EDGE_HOP: caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len); break;
-    case L_HOP: caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len); break;
+    case L_EDGE_HOP:
+      caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len);
+      if (no_loop("eh")) L.eh.max_blocks = 0;
+      break;
+    case L_HOP:
+      caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
+      if (no_loop("hop")) L.hop.max_blocks = 0;
+      break;
     case L_HOPM: {
       HopMArgs& a = L.hopm;
       const size_t dyn = ((size_t)a.wfloats + (size_t)(a.m == 3 ? 2 : 1) * a.bmax * (16 * P->NT + 4)) * 4;
@@ -882,7 +897,10 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     }
     case L_EXCHANGE: break;
-    case L_EPI: caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len); break;
+    case L_EPI:
+      caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len);
+      if (no_loop("epi")) L.ep.max_blocks = 0;
+      break;
     default: {
       // edge tiles while they all fit on the chip at once (latency-bound launch), else rows
       PoolArgs& a = L.pool;
