@@ -888,7 +888,10 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     case L_HOP:
       caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
-      if (no_loop("hop")) L.hop.max_blocks = 0;
+      // one tile per wave at any size unless MSW_HOP_LOOP=1: the grid-stride variant
+      // measured equal on the 1M-node mesh and 1.3-1.6 % slower on the batch of 8
+      // (profiles/r01_v7/ab_edge_waves.txt)
+      if (no_loop("hop") || !getenv("MSW_HOP_LOOP")) L.hop.max_blocks = 0;
       break;
     case L_HOPM: {
       HopMArgs& a = L.hopm;
