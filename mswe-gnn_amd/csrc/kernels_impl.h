@@ -410,9 +410,11 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
         stage_glds(smem, a.c.W, a.sreg[s], 0, a.sreg[s].len);
         __syncthreads();
         staged = s;
-        c.W = smem;
       }
     }
+    // weight reads straight from the LDS pointer (not through c.W, which the compiler cannot
+    // prove to be LDS across the loop: it emitted flat loads, which wait on vmcnt too)
+    const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
     MSW_MARK(c, 2);
     f32x4 xs[NT];
     {
@@ -420,20 +422,20 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = (c.with_wl && 4 * g + r == nstat) ? wlv : raw[r];
       const f32x4 in[1] = {v};
-      run_mlp<1, NT, NT, ACT>(in, xs, a.stat, c.W, lane, g);
+      run_mlp<1, NT, NT, ACT>(in, xs, a.stat, Wl, lane, g);
       if (valid) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
     }
     MSW_MARK(c, 5);
     if (s == 0) {
       f32x4 xd[NT];
       const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
-      run_mlp<1, NT, NT, ACT>(in, xd, a.dynm, c.W, lane, g);
+      run_mlp<1, NT, NT, ACT>(in, xd, a.dynm, Wl, lane, g);
       if (valid && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
       MSW_MARK(c, 6);
-      np_project<NT>(xs, xd, a.np0, c.W, n, valid, lane, g);
+      np_project<NT>(xs, xd, a.np0, Wl, n, valid, lane, g);
     }
     MSW_MARK(c, 8);
-    if (a.vu_a[s] >= 0) side_proj<NT, NT>(xs, a.vu_h1t, c.W + a.vu_a[s], a.Vu, n, valid, lane, g);
+    if (a.vu_a[s] >= 0) side_proj<NT, NT>(xs, a.vu_h1t, Wl + a.vu_a[s], a.Vu, n, valid, lane, g);
   }
   MSW_MARK(c, 9);
 }
