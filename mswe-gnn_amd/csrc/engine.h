@@ -138,7 +138,9 @@ struct Epilogue {
 // (+ epilogue when the layer has K = 1; intra-scale unpooling is such a layer).
 struct EdgeHopArgs {
   Common c;
-  WReg reg;
+  WReg reg;                        // [MLP | epilogue operands | filter W_1]
+  int reg_nf;                      // floats without the trailing filter copy (one-tile-per-wave
+                                   // variant, which keeps the filter in registers)
   int max_blocks;                  // grid cap of the grid-stride variant (resident workgroups)
   int fit_blocks;                  // workgroups of the one-tile-per-wave variant the chip holds
   int n0;                          // first internal row of the destination scale

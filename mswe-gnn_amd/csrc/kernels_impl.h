@@ -721,12 +721,12 @@ __global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgp
     MSW_MARK(c, 1);
     // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
     // stream into LDS behind the MLP and are waited for at the epilogue barrier
-    const bool split = kStaged<NT> && a.reg.split < a.reg.len;
+    const bool split = kStaged<NT> && a.reg.split < a.reg_nf;
     if constexpr (kStaged<NT>) {
       stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.split);
       __syncthreads();
       c.W = smem;
-      if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg.len);
+      if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
     }
     MSW_MARK(c, 2);
     f32x4 res[NT];
@@ -1380,7 +1380,7 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const bool loop = tile_loop(a);
   const dim3 grid(tile_grid(a)), block(64 * (loop ? edge_waves<NT, true>() : kWaves));
-  const size_t sh = lds_bytes<NT>(a.reg.len);
+  const size_t sh = lds_bytes<NT>(loop ? a.reg.len : a.reg_nf);
   if (a.c.prelu) {
     if (loop) hipLaunchKernelGGL((k_edge_hop<NT, 1, true>), grid, block, sh, st, a);
     else hipLaunchKernelGGL((k_edge_hop<NT, 1, false>), grid, block, sh, st, a);

@@ -813,11 +813,12 @@ int relocate(msw_plan* P, std::vector<Launch>& q) {
       RegionBuilder R(P->blob, 0);
       a.b1_off = R.put(a.b1_off, 16 * a.h1t);
       rl.mlp(R, a.rest);
-      // filt_a stays a blob offset (the one-tile-per-wave variant loads it into registers);
-      // the grid-stride variant reads the region's copy from LDS
-      a.filt_l = R.put(a.filt_a, P->NT * P->NT * 256);
       const int split = R.pos();  // operands after this one stream in behind the MLP
       if (a.last) rl.epi(R, a.epi);
+      // filt_a stays a blob offset (the one-tile-per-wave variant loads it into registers and
+      // stages the region without it); the grid-stride variant reads this trailing copy
+      a.reg_nf = R.pos();
+      a.filt_l = R.put(a.filt_a, P->NT * P->NT * 256);
       a.reg = R.done(split);
       reg = &a.reg;
     } else if (L.kind == L_EXCHANGE) {
@@ -873,6 +874,7 @@ void caps(msw_plan* P, A& a, int kind, int prelu, int last, int floats) {
 }
 // A/B measurements: MSW_NO_LOOP=eh,hop,epi,all keeps those launches one tile per wave at
 // any size (no grid-stride loop).
+constexpr int kHopLoopTiles = 65536;
 bool no_loop(const char* kind) {
   const char* e = getenv("MSW_NO_LOOP");
   return e && (strstr(e, kind) || strstr(e, "all"));
@@ -884,14 +886,16 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     case L_EDGE_HOP:
       caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len);
+      L.eh.fit_blocks = resident_of(P->NT, 1, L.eh.c.prelu, 0, (size_t)L.eh.reg_nf * 4, 0);
       if (no_loop("eh")) L.eh.max_blocks = 0;
       break;
     case L_HOP:
       caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
-      // one tile per wave at any size unless MSW_HOP_LOOP=1: the grid-stride variant
-      // measured equal on the 1M-node mesh and 1.3-1.6 % slower on the batch of 8
+      // one tile per wave below kHopLoopTiles (MSW_HOP_LOOP=1: loop whenever the grid does
+      // not fit): the grid-stride variant measured 1.1-1.6 % slower on the batch of 8 and
+      // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
       // (profiles/r01_v7/ab_edge_waves.txt)
-      if (no_loop("hop") || !getenv("MSW_HOP_LOOP")) L.hop.max_blocks = 0;
+      if (no_loop("hop") || (!getenv("MSW_HOP_LOOP") && L.hop.ntiles < kHopLoopTiles)) L.hop.max_blocks = 0;
       break;
     case L_HOPM: {
       HopMArgs& a = L.hopm;

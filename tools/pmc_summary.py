@@ -47,9 +47,11 @@ def main():
     if hops:
         k, v = max(hops, key=lambda kv: kv[1]["dispatches"])
         res["k_hop"] = dict(v, kernel=k)
-        # bench.py's large-mesh roofline (config 5): the middle hop with the largest grid
-        mids = [(kk, vv) for kk, vv in hops if "false," in kk or kk.count("false") >= 1]
-        kl, vl = max(mids or hops, key=lambda kv: int(kv[0].split("grid=")[1]))
+        # bench.py's large-mesh roofline (config 5): the middle hop (LAST = false, the third
+        # template argument) moving the most bytes per launch (grid-stride launches have
+        # capped grids, so the grid size does not identify it)
+        mids = [(kk, vv) for kk, vv in hops if kk.split("<")[1].split(",")[2].strip() == "false"]
+        kl, vl = max(mids or hops, key=lambda kv: kv[1]["hbm_bytes_per_launch"] or 0)
         res["k_hop_large"] = dict(vl, kernel=kl)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res.get("k_hop"), indent=1))
