@@ -587,15 +587,7 @@ struct EdgeHopRows {  // everything one tile reads from HBM
   f32x4 Us[2 * NT], Ps[2 * NT], Vn[2 * NT], os[NT], inn[NT], sk[NT];
   EpiPre<NT> pre;  // a.last only
 };
-// NODE = false leaves the rows needed only after the MLP (skip, epilogue inputs) to
-// edge_hop_node (the pipelined loop issues them when the tile starts computing).
 template <int NT>
-__device__ __forceinline__ void edge_hop_node(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int g) {
-  constexpr int F = 16 * NT;
-  load_row<NT>(r.sk, a.skip ? a.skip + r.L.n * F : a.c.zrow, g);
-  if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, r.L.n, g);
-}
-template <int NT, bool NODE = true>
 __device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHopArgs& a, const LaneRec& rec,
                                                 int tile, int j, int g) {
   constexpr int F = 16 * NT, T2 = 2 * NT;
@@ -616,7 +608,8 @@ __device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHo
   }
   load_row<NT>(r.os, a.in + L.sr * F, g);
   load_row<NT>(r.inn, a.own_zero ? z : a.in + L.n * F, g);
-  if constexpr (NODE) edge_hop_node<NT>(r, a, g);
+  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
+  if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
 }
 template <int NT>
 __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
@@ -700,7 +693,7 @@ __device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const EdgeHopR
   }
 }
 template <int NT, int ACT, bool LOOP>
-__global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgpu_waves_per_eu(LOOP && MSW_EDGE_WAVES % 3 == 0 ? 3 : 1))) void k_edge_hop(EdgeHopArgs a) {
+__global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgpu_waves_per_eu(LOOP && NT <= 2 && MSW_EDGE_WAVES % 3 == 0 ? 3 : 1))) void k_edge_hop(EdgeHopArgs a) {
   constexpr int WV = edge_waves<NT, LOOP>();
   // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
   constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
