@@ -28,7 +28,8 @@ def build(force=False, verbose=True, variant=""):
     """variant "trace": diagnostic library lib/libmswegnn_trace.so (-DMSW_TRACE)."""
     odir = os.path.join(HERE, "_obj" + (f"_{variant}" if variant else ""))
     extra = {"trace": ["-DMSW_TRACE"], "w8": ["-DMSW_WAVES=8"], "w2": ["-DMSW_WAVES=2"],
-             "ew8": ["-DMSW_EDGE_WAVES=8"], "ew4": ["-DMSW_EDGE_WAVES=4"]}.get(variant, [])
+             "ew8": ["-DMSW_EDGE_WAVES=8"], "ew4": ["-DMSW_EDGE_WAVES=4"],
+             "e0w12": ["-DMSW_EDGE_WAVES0=12"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     objs, cmds = [], []

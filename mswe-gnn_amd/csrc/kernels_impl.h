@@ -34,10 +34,17 @@ constexpr int waves_of() { return LOOP && NT <= 2 ? 8 : kWaves; }
 // a software-pipelined loop (next tile's gathers during the MLP) needs > 256 registers,
 // i.e. one wave per SIMD, and measured 24 % slower on the 1M-node mesh
 #ifndef MSW_EDGE_WAVES
-#define MSW_EDGE_WAVES 12
+#define MSW_EDGE_WAVES 12   // grid-stride, with epilogue (LST = 1): 3 waves per SIMD
 #endif
-template <int NT, bool LOOP>
-constexpr int edge_waves() { return LOOP && NT <= 2 ? MSW_EDGE_WAVES : kWaves; }
+#ifndef MSW_EDGE_WAVES0
+#define MSW_EDGE_WAVES0 16  // grid-stride, no epilogue (LST = 0): 4 waves per SIMD
+#endif
+// Workgroup of the grid-stride edge MLP + hop: as many waves as the register budget allows
+// per SIMD, times 4 -- one workgroup per CU, so one staged weight copy serves all of them.
+template <int NT, bool LOOP, int LST = 1>
+constexpr int edge_waves() { return LOOP && NT <= 2 ? (LST ? MSW_EDGE_WAVES : MSW_EDGE_WAVES0) : kWaves; }
+template <int NT, bool LOOP, int LST>
+constexpr int edge_eu() { return LOOP && NT <= 2 ? edge_waves<NT, LOOP, LST>() / 4 : 1; }
 
 #define MSW_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
@@ -587,7 +594,9 @@ struct EdgeHopRows {  // everything one tile reads from HBM
   f32x4 Us[2 * NT], Ps[2 * NT], Vn[2 * NT], os[NT], inn[NT], sk[NT];
   EpiPre<NT> pre;  // a.last only
 };
-template <int NT>
+// LST = 0: the launch never runs an epilogue (compiled out: fewer live scalars, no SGPR
+// spills into VGPR lanes in the grid-stride loop); LST = 1: a.last decides.
+template <int NT, int LST>
 __device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHopArgs& a, const LaneRec& rec,
                                                 int tile, int j, int g) {
   constexpr int F = 16 * NT, T2 = 2 * NT;
@@ -609,11 +618,11 @@ __device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHo
   load_row<NT>(r.os, a.in + L.sr * F, g);
   load_row<NT>(r.inn, a.own_zero ? z : a.in + L.n * F, g);
   load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
-  if (a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
+  if (LST && a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
 }
-template <int NT>
+template <int NT, int LST>
 __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
-  edge_hop_gather<NT>(r, a, load_rec(a.recs, tile, j), tile, j, g);
+  edge_hop_gather<NT, LST>(r, a, load_rec(a.recs, tile, j), tile, j, g);
 }
 template <int NT, int ACT, int XS, bool FREG = true>
 __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
@@ -681,20 +690,21 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
 #pragma unroll
   for (int t = 0; t < NT; ++t) res_out[t] = res[t];
 }
-template <int NT, int ACT>
+template <int NT, int ACT, int LST>
 __device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const EdgeHopRows<NT>& r, const EdgeHopArgs& a,
                                                 const Common& c, int lane, int g) {
   constexpr int F = 16 * NT;
   const Lanes& L = r.L;
-  if (a.last) {
+  if (LST && a.last) {
     node_epilogue<NT, ACT>(res, a.epi, c, r.pre, a.out, L.n, L.nv, lane, g);
   } else if (L.nv && a.out) {
     store_row<NT>(a.out + L.n * F, res, NT, g);
   }
 }
-template <int NT, int ACT, bool LOOP>
-__global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgpu_waves_per_eu(LOOP && NT <= 2 && MSW_EDGE_WAVES % 3 == 0 ? 3 : 1))) void k_edge_hop(EdgeHopArgs a) {
-  constexpr int WV = edge_waves<NT, LOOP>();
+template <int NT, int ACT, bool LOOP, int LST>
+__global__ __launch_bounds__((64 * edge_waves<NT, LOOP, LST>())) __attribute__((amdgpu_waves_per_eu(edge_eu<NT, LOOP, LST>())))
+void k_edge_hop(EdgeHopArgs a) {
+  constexpr int WV = edge_waves<NT, LOOP, LST>();
   // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
   constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
   __shared__ __attribute__((aligned(16))) float slab[WV][kRowsPerWave][XS];
@@ -710,7 +720,7 @@ __global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgp
   if constexpr (!LOOP) {
     const bool live = tile < a.ntiles;
     EdgeHopRows<NT> r;
-    edge_hop_load<NT>(r, a, live ? tile : 0, j, g);  // idle waves stay in bounds
+    edge_hop_load<NT, LST>(r, a, live ? tile : 0, j, g);  // idle waves stay in bounds
     MSW_MARK(c, 1);
     // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
     // stream into LDS behind the MLP and are waited for at the epilogue barrier
@@ -725,7 +735,7 @@ __global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgp
     f32x4 res[NT];
     if (live) edge_hop_core<NT, ACT, XS>(r, a, c, wf, &slab[w][0][0], j, lane, g, res);
     if (split) __syncthreads();  // every wave: the epilogue operands have landed
-    if (live) edge_hop_finish<NT, ACT>(res, r, a, c, lane, g);
+    if (live) edge_hop_finish<NT, ACT, LST>(res, r, a, c, lane, g);
   } else {
     if constexpr (kStaged<NT>) {
       stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
@@ -735,10 +745,10 @@ __global__ __launch_bounds__((64 * edge_waves<NT, LOOP>())) __attribute__((amdgp
     for (; tile < a.ntiles; tile += stride) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       EdgeHopRows<NT> q;
-      edge_hop_load<NT>(q, a, tile, jj, gg);
+      edge_hop_load<NT, LST>(q, a, tile, jj, gg);
       f32x4 res[NT];
       edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, wf, &slab[w][0][0], jj, ln, gg, res);
-      edge_hop_finish<NT, ACT>(res, q, a, c, ln, gg);
+      edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
     }
   }
   MSW_MARK(c, 9);
@@ -1320,9 +1330,12 @@ hipError_t prepare_kernels() {
   constexpr int WL = waves_of<NT, true>();
   const std::pair<const void*, int> fns[] = {
       {(const void*)k_encode<NT, 1>, kWaves}, {(const void*)k_encode<NT, -1>, kWaves},
-      {(const void*)k_edge_hop<NT, 1, false>, kWaves}, {(const void*)k_edge_hop<NT, -1, false>, kWaves},
-      {(const void*)k_edge_hop<NT, 1, true>, edge_waves<NT, true>()},
-      {(const void*)k_edge_hop<NT, -1, true>, edge_waves<NT, true>()},
+      {(const void*)k_edge_hop<NT, 1, false, 0>, kWaves}, {(const void*)k_edge_hop<NT, -1, false, 0>, kWaves},
+      {(const void*)k_edge_hop<NT, 1, false, 1>, kWaves}, {(const void*)k_edge_hop<NT, -1, false, 1>, kWaves},
+      {(const void*)k_edge_hop<NT, 1, true, 0>, edge_waves<NT, true, 0>()},
+      {(const void*)k_edge_hop<NT, -1, true, 0>, edge_waves<NT, true, 0>()},
+      {(const void*)k_edge_hop<NT, 1, true, 1>, edge_waves<NT, true, 1>()},
+      {(const void*)k_edge_hop<NT, -1, true, 1>, edge_waves<NT, true, 1>()},
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
       {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
@@ -1369,19 +1382,23 @@ static inline int tile_grid(const A& a) {
 }
 
 template <int NT>
+static const void* edge_hop_kernel(int prelu, bool loop, int last) {
+  if (loop) {
+    if (last) return prelu ? (const void*)k_edge_hop<NT, 1, true, 1> : (const void*)k_edge_hop<NT, -1, true, 1>;
+    return prelu ? (const void*)k_edge_hop<NT, 1, true, 0> : (const void*)k_edge_hop<NT, -1, true, 0>;
+  }
+  if (last) return prelu ? (const void*)k_edge_hop<NT, 1, false, 1> : (const void*)k_edge_hop<NT, -1, false, 1>;
+  return prelu ? (const void*)k_edge_hop<NT, 1, false, 0> : (const void*)k_edge_hop<NT, -1, false, 0>;
+}
+template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)), block(64 * (loop ? edge_waves<NT, true>() : kWaves));
+  const dim3 grid(tile_grid(a)),
+      block(64 * (loop ? (a.last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves));
   const size_t sh = lds_bytes<NT>(loop ? a.reg.len : a.reg_nf);
-  if (a.c.prelu) {
-    if (loop) hipLaunchKernelGGL((k_edge_hop<NT, 1, true>), grid, block, sh, st, a);
-    else hipLaunchKernelGGL((k_edge_hop<NT, 1, false>), grid, block, sh, st, a);
-  } else {
-    if (loop) hipLaunchKernelGGL((k_edge_hop<NT, -1, true>), grid, block, sh, st, a);
-    else hipLaunchKernelGGL((k_edge_hop<NT, -1, false>), grid, block, sh, st, a);
-  }
-  return hipGetLastError();
+  void* args[] = {const_cast<EdgeHopArgs*>(&a)};
+  return hipLaunchKernel(edge_hop_kernel<NT>(a.c.prelu, loop, a.last), grid, block, args, sh, st);
 }
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
@@ -1458,7 +1475,7 @@ template <int NT, bool LOOP>
 static const void* kernel_of(int kind, int prelu, int last) {
   switch (kind) {
     case 0: return prelu ? (const void*)k_encode<NT, 1> : (const void*)k_encode<NT, -1>;
-    case 1: return prelu ? (const void*)k_edge_hop<NT, 1, LOOP> : (const void*)k_edge_hop<NT, -1, LOOP>;
+    case 1: return edge_hop_kernel<NT>(prelu, LOOP, last);
     case 2:
       return !last ? (const void*)k_hop<NT, 1, false, LOOP>
                    : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
@@ -1475,7 +1492,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   int per_cu = 0, dev = 0, cus = 0;
   const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
-                    : kind == 1 ? 64 * (loop ? edge_waves<NT, true>() : kWaves)
+                    : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : 64 * (loop && (kind == 2 || kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
     return 0;

@@ -885,8 +885,8 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
       break;
     case L_EDGE_HOP:
-      caps(P, L.eh, 1, L.eh.c.prelu, 0, L.eh.reg.len);
-      L.eh.fit_blocks = resident_of(P->NT, 1, L.eh.c.prelu, 0, (size_t)L.eh.reg_nf * 4, 0);
+      caps(P, L.eh, 1, L.eh.c.prelu, L.eh.last, L.eh.reg.len);
+      L.eh.fit_blocks = resident_of(P->NT, 1, L.eh.c.prelu, L.eh.last, (size_t)L.eh.reg_nf * 4, 0);
       if (no_loop("eh")) L.eh.max_blocks = 0;
       break;
     case L_HOP:
