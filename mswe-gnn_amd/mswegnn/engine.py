@@ -251,7 +251,7 @@ class EnginePlan:
                                          self._stream()))
         return dst
 
-    KERNELS = {"hop": 0, "edge_hop": 1, "pool": 2, "encode": 3, "unpool": 4, "hop2": 5}  # plan.hip bench_kernel
+    KERNELS = {"hop": 0, "edge_hop": 1, "pool": 2, "encode": 3, "unpool": 4, "hopm": 5}  # plan.hip bench_kernel (hopm: opt-in hop chains)
 
     def bench_kernel(self, kernel, scale, iters):
         """Enqueue `iters` launches of one kernel on the current stream -> units (rows, edges)
