@@ -624,10 +624,12 @@ template <int NT, int LST>
 __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
   edge_hop_gather<NT, LST>(r, a, load_rec(a.recs, tile, j), tile, j, g);
 }
+// Wm: the MLP operands (b1, layers 2..L) -- the staged region; c.W: everything else (the
+// same region for F <= 32, the blob for F = 64, whose epilogue operands do not fit in LDS).
 template <int NT, int ACT, int XS, bool FREG = true>
 __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
-                                              const f32x4 (&wf)[NT][NT], float* slab, int j, int lane, int g,
-                                              f32x4 (&res_out)[NT]) {
+                                              const float* Wm, const f32x4 (&wf)[NT][NT], float* slab, int j,
+                                              int lane, int g, f32x4 (&res_out)[NT]) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT, T2 = 2 * NT;
   const Lanes& L = r.L;
@@ -641,7 +643,7 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
     const int off = 16 * t + 4 * g;
-    const f32x4 p = a.Pe ? r.Ps[t] : ld4(c.W + a.b1_off + off);
+    const f32x4 p = a.Pe ? r.Ps[t] : ld4(Wm + a.b1_off + off);
     H[t] = (t < a.h1t) ? (r.Us[t] + ld4(dr + off)) + p : zero4();
   }
   load_row<NT>(od, dr + 16 * T2, g);
@@ -649,7 +651,7 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
   act_tiles<ACT, T2>(H, a.act1, a.slope1);
   f32x4 sv[NT];
   if (a.rest.n > 0) {
-    run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, c.W, lane, g);
+    run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, lane, g);
   } else {
 #pragma unroll
     for (int t = 0; t < NT; ++t) sv[t] = H[t];
@@ -725,29 +727,41 @@ void k_edge_hop(EdgeHopArgs a) {
     // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
     // stream into LDS behind the MLP and are waited for at the epilogue barrier
     const bool split = kStaged<NT> && a.reg.split < a.reg_nf;
+    const float* Wm = c.W;
     if constexpr (kStaged<NT>) {
       stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.split);
       __syncthreads();
       c.W = smem;
+      Wm = smem;
       if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
+    } else if (a.reg.len > 0) {  // F = 64: the MLP region alone (plan.hip relocate)
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      Wm = smem;
     }
     MSW_MARK(c, 2);
     f32x4 res[NT];
-    if (live) edge_hop_core<NT, ACT, XS>(r, a, c, wf, &slab[w][0][0], j, lane, g, res);
+    if (live) edge_hop_core<NT, ACT, XS>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
     if (split) __syncthreads();  // every wave: the epilogue operands have landed
     if (live) edge_hop_finish<NT, ACT, LST>(res, r, a, c, lane, g);
   } else {
+    const float* Wm = c.W;
     if constexpr (kStaged<NT>) {
       stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
       __syncthreads();
       c.W = smem;
+      Wm = smem;
+    } else if (a.reg.len > 0) {  // F = 64: the MLP region alone
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      Wm = smem;
     }
     for (; tile < a.ntiles; tile += stride) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       EdgeHopRows<NT> q;
       edge_hop_load<NT, LST>(q, a, tile, jj, gg);
       f32x4 res[NT];
-      edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, wf, &slab[w][0][0], jj, ln, gg, res);
+      edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, Wm, wf, &slab[w][0][0], jj, ln, gg, res);
       edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
     }
   }
@@ -1307,6 +1321,10 @@ __global__ __launch_bounds__(kBlock) void k_rowmlp(RowMlpArgs a) {
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // dynamic LDS of a launch: its weight region rounded up to whole 1-KB LDS-DMA chunks
+// the edge hop stages its MLP region at every width
+constexpr size_t eh_lds_bytes(int floats) {
+  return (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float);
+}
 template <int NT>
 constexpr size_t lds_bytes(int floats) {
   return kStaged<NT> ? (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float) : 0;
@@ -1396,7 +1414,7 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   const bool loop = tile_loop(a);
   const dim3 grid(tile_grid(a)),
       block(64 * (loop ? (a.last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves));
-  const size_t sh = lds_bytes<NT>(loop ? a.reg.len : a.reg_nf);
+  const size_t sh = eh_lds_bytes(loop ? a.reg.len : a.reg_nf);
   void* args[] = {const_cast<EdgeHopArgs*>(&a)};
   return hipLaunchKernel(edge_hop_kernel<NT>(a.c.prelu, loop, a.last), grid, block, args, sh, st);
 }
@@ -1490,7 +1508,8 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const void* f = kind == 4 ? hopm_kernel<NT>(loop, last, prelu)
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
-  const size_t dyn = kind == 4 ? dyn_bytes : lds_bytes<NT>((int)(dyn_bytes / 4));
+  const size_t dyn = kind == 4 ? dyn_bytes : kind == 1 ? eh_lds_bytes((int)(dyn_bytes / 4))
+                                                     : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : 64 * (loop && (kind == 2 || kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);

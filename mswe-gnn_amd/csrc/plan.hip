@@ -781,11 +781,31 @@ struct Relocator {
 
 constexpr int kMaxRegionFloats = (160 * 1024) / 4 - kWaves * kRowsPerWave * (3 * 32 + 4);  // minus the F=32 slab
 
-int relocate(msw_plan* P, std::vector<Launch>& q) {
+// mlp_only (F = 64): only the edge hops' MLP operands (b1, layers 2..L) get a region -- when
+// it fits beside the edge slab; every other operand stays a blob offset.
+int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
   Relocator rl{P->NT, P->p};
   for (Launch& L : q) {
     WReg* reg = nullptr;
     int tot = 0;
+    if (mlp_only) {
+      if (L.kind != L_EDGE_HOP) continue;
+      EdgeHopArgs& a = L.eh;
+      const int len = 16 * a.h1t + [&] {
+        int n = 0;
+        for (int i = 0; i < a.rest.n; ++i) n += a.rest.l[i].tout * a.rest.l[i].tin * 256 + 16 * a.rest.l[i].tout;
+        return n;
+      }();
+      const int slab = kWaves * kRowsPerWave * (48 * P->NT + 4) * (int)sizeof(float);
+      if ((len + 255) / 256 * 256 * (int)sizeof(float) + slab > 160 * 1024) continue;  // stays in the blob
+      RegionBuilder R(P->blob, 0);
+      a.b1_off = R.put(a.b1_off, 16 * a.h1t);
+      rl.mlp(R, a.rest);
+      a.reg = R.done();
+      a.reg_nf = a.reg.len;
+      a.filt_l = -1;
+      continue;
+    }
     if (L.kind == L_ENCODE) {
       // one contiguous region per scale (one LDS-DMA copy per workgroup): the static
       // encoder first -- identical relative offsets in every scale's region -- then the
@@ -1467,8 +1487,10 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
   // ---- launch schedules (forward / rollout), per-launch weight regions, weight upload
   sched_step(P.get(), P->sched_fwd, false);
   sched_step(P.get(), P->sched_roll, true);
-  if (P->NT <= 2) {
-    if ((rc = relocate(P.get(), P->sched_fwd)) || (rc = relocate(P.get(), P->sched_roll))) return rc;
+  {
+    const bool mlp_only = P->NT > 2;  // F = 64: only the edge-MLP operands fit in LDS
+    if ((rc = relocate(P.get(), P->sched_fwd, mlp_only)) || (rc = relocate(P.get(), P->sched_roll, mlp_only)))
+      return rc;
   }
   P->blob.alloc(256);  // slack: LDS-DMA chunks may read up to 255 floats past a region
   if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
