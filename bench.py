@@ -50,6 +50,8 @@ def build_workload(name, seed, T):
         "zenodo4": dict(mesh="zenodo4", S=4, F=32, K=4, weights="K4_F32"),
         # config 2, "3-scale" wording: same N0, 3 scales, seeded init (no 3-scale checkpoint)
         "zenodo3": dict(mesh="zenodo3", S=3, F=32, K=4, weights=None),
+        # config 2 with the other shipped 4-scale checkpoint (hid_features 16, K 2)
+        "zenodo4_k2f16": dict(mesh="zenodo4", S=4, F=16, K=2, weights="K2_F16"),
         # config 2 at the reference's default config.yaml width (hid_features 64, K 4; no
         # F = 64 checkpoint is shipped -> seeded init)
         "zenodo4_f64": dict(mesh="zenodo4", S=4, F=64, K=4, weights=None),
