@@ -235,6 +235,27 @@ def main():
                         "peak_tflops": FP32_MFMA_PEAK_TFS},
                     "k_pool<32> (mean pool + projection), scale 1": {
                         "avg_launch_us": t_pool * 1e6, "rows": r_pool}}}
+        # ---------------- the launch floor the zenodo-size hop is bound by: one dependent
+        # gather of the previous launch's rows (torch.index_select, same rows x F) per launch
+        # of a captured 35-launch graph (tools/launch_floor.py)
+        if world == 1:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import launch_floor as lf
+            small = torch.ones(1024, device=dev)
+            perm = torch.randperm(rows, device=dev)
+            bufs = [torch.randn(rows, F, device=dev), torch.empty(rows, F, device=dev)]
+            flip = {"i": 0}
+
+            def _gather():
+                i = flip["i"]
+                torch.index_select(bufs[i], 0, perm, out=bufs[1 - i])
+                flip["i"] = 1 - i
+            roof["launch_floor"] = {
+                "trivial_us": lf.per_launch_us(lambda: small.mul_(1.0), 35),
+                "dependent_row_gather_us": lf.per_launch_us(_gather, 35),
+                "note": "per launch, 35 dependent launches in one graph; the gather reads the "
+                        "previous launch's rows (same rows x F as the roofline hop)"}
+            del small, perm, bufs
         # ---------------- the same hop kernel where HBM, not latency, bounds it: the ~1M-node
         # mesh of config 5 (fully wet; one rollout step to populate the buffers)
         if world == 1 and not args.no_roofline_large and args.workload != "hbm1m":
