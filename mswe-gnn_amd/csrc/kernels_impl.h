@@ -640,11 +640,20 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
   wave_lds_sync();
   const float* dr = slab + L.dl * XS;
   f32x4 H[T2], od[NT];
+  // unconditional LDS reads + selects: reads under the run-time h1t / Pe flags compiled to
+  // a branch and an lgkmcnt(0) wait per tile
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  f32x4 vr[T2], br[T2];
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
     const int off = 16 * t + 4 * g;
-    const f32x4 p = a.Pe ? r.Ps[t] : ld4(Wm + a.b1_off + off);
-    H[t] = (t < a.h1t) ? (r.Us[t] + ld4(dr + off)) + p : zero4();
+    vr[t] = ld4(dr + off);
+    br[t] = ld4(Wm + b1 + off);
+  }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const f32x4 p = a.Pe ? r.Ps[t] : br[t];
+    H[t] = (t < a.h1t) ? (r.Us[t] + vr[t]) + p : zero4();
   }
   load_row<NT>(od, dr + 16 * T2, g);
   MSW_MARK(c, 4);
