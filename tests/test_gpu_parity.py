@@ -143,11 +143,13 @@ def test_rollout_zenodo_size_vs_reference(cuda):
 
 
 def test_fused_rollout_matches_step_loop_and_graph_capture(cuda):
-    """Fused msw_rollout (captured hipGraph) == msw_rollout without graph == the
-    reference-style Python loop over the HIP forward (training/train.py semantics)."""
+    """Fused msw_rollout (captured hipGraphs: one 16-step graph + single-step remainder at
+    T = 20) == msw_rollout without graph == the reference-style Python loop over the HIP
+    forward (training/train.py semantics)."""
     from mswegnn.engine import plan_for
     from utils.dataset import apply_boundary_condition, use_prediction
-    g = make_multiscale_mesh(**mesh_config("small"), T=12).to(cuda)
+    T = 20
+    g = make_multiscale_mesh(**mesh_config("small"), T=T).to(cuda)
     m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
     plan = plan_for(m, g)
     plan.set_graph_capture(True)
@@ -159,7 +161,7 @@ def test_fused_rollout_matches_step_loop_and_graph_capture(cuda):
     temp = g.clone()
     preds = []
     with torch.no_grad():
-        for t in range(12):
+        for t in range(T):
             temp.x[:, -6:] = apply_boundary_condition(temp.x[:, -6:], temp.BC[:, :, t], temp.node_BC, 2)
             p = m(temp)
             temp.x = use_prediction(temp.x, p, 3)
