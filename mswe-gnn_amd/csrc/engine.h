@@ -163,6 +163,8 @@ struct EdgeHopArgs {
   float* out;                      // out_1 rows, or null
   int last;                        // last hop of the layer: run the epilogue
   Epilogue epi;
+  int coop;                        // waves per tile (k_edge_coop: MFMA output tiles split
+                                   // across them), 0/1 = one wave per tile
 };
 
 // Hops 2..K over the same edge tiles as the fused first hop.

@@ -777,6 +777,235 @@ void k_edge_hop(EdgeHopArgs a) {
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- cooperative edge hop
+// The fused edge MLP + hop with P waves per tile, for scales whose tiles are far fewer than
+// the chip's SIMDs (the MLP chain of one wave is then the launch's critical path): every
+// wave of a tile group loads the tile and does the (cheap) VALU / LDS work itself; the MFMA
+// work -- each MLP layer, the filter, the epilogue projections -- is split by output tile,
+// rank r computing tiles [r T/P, (r+1) T/P), the parts exchanged through LDS.  Same
+// operations on the same operands as k_edge_hop (every output element is one MFMA chain
+// in k order either way): bit-identical results.
+// a[k TS + t] for the rank's k, with compile-time register indices (a run-time index into a
+// register array would move it to scratch)
+template <int N, int TS>
+__device__ __forceinline__ f32x4 pick(const f32x4 (&a)[N], int r, int t) {
+  f32x4 v = a[t];
+#pragma unroll
+  for (int k = 1; k < N / TS; ++k) v = (r == k) ? a[k * TS + t] : v;
+  return v;
+}
+template <int T, int P>
+__device__ __forceinline__ void coop_exchange(const f32x4* sub, f32x4 (&full)[T], float* buf, int xw, int r,
+                                              int j, int g) {
+  constexpr int TS = T / P;
+#pragma unroll
+  for (int t = 0; t < TS; ++t) st4(buf + j * xw + 16 * (r * TS + t) + 4 * g, sub[t]);
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < T; ++t) full[t] = ld4(buf + j * xw + 16 * t + 4 * g);
+}
+// nn.Linear + bias + activation on output tiles [to0, to0 + TS) of a TIN -> T layer
+template <int TIN, int TS, int ACT>
+__device__ __forceinline__ void mfma_layer_sub(const f32x4 (&in)[TIN], f32x4 (&out)[TS], const LayerDev& L,
+                                               const float* __restrict__ W, int to0, int lane, int g) {
+  f32x4 acc[TS];
+  proj<TIN, TS>(in, acc, W + L.a_off + (size_t)to0 * TIN * 256, lane);
+#pragma unroll
+  for (int to = 0; to < TS; ++to) acc[to] = acc[to] + ld4(W + L.b_off + 16 * (to0 + to) + 4 * g);
+  act_tiles<ACT, TS>(acc, L.act, L.slope);
+#pragma unroll
+  for (int to = 0; to < TS; ++to) out[to] = acc[to];
+}
+// run_mlp with each layer's output tiles split over the P ranks; buffers alternate per layer
+template <int IN0, int T, int TL, int ACT, int P>
+__device__ __forceinline__ void coop_run_mlp(const f32x4 (&in)[IN0], f32x4 (&out)[TL], const MlpDev& m,
+                                             const float* __restrict__ W, int lane, int g, int j, int r,
+                                             float* buf0, float* buf1, int xw) {
+  if (m.n == 1) {
+    f32x4 o[TL / P];
+    mfma_layer_sub<IN0, TL / P, ACT>(in, o, m.l[0], W, r * (TL / P), lane, g);
+    coop_exchange<TL, P>(o, out, buf0, xw, r, j, g);
+    return;
+  }
+  f32x4 h[T];
+  {
+    f32x4 o[T / P];
+    mfma_layer_sub<IN0, T / P, ACT>(in, o, m.l[0], W, r * (T / P), lane, g);
+    coop_exchange<T, P>(o, h, buf0, xw, r, j, g);
+  }
+  for (int li = 1; li + 1 < m.n; ++li) {
+    f32x4 o[T / P];
+    mfma_layer_sub<T, T / P, ACT>(h, o, m.l[li], W, r * (T / P), lane, g);
+    coop_exchange<T, P>(o, h, (li & 1) ? buf1 : buf0, xw, r, j, g);
+  }
+  f32x4 o[TL / P];
+  mfma_layer_sub<T, TL / P, ACT>(h, o, m.l[m.n - 1], W, r * (TL / P), lane, g);
+  coop_exchange<TL, P>(o, out, ((m.n - 1) & 1) ? buf1 : buf0, xw, r, j, g);
+}
+// np_project with the output tiles of U, V and O split over the ranks (each stores its part)
+template <int TIN, int TS>
+__device__ __forceinline__ void proj_store_part(const f32x4 (&in)[TIN], const float* A, int r, float* dst, size_t n,
+                                                int ntl, bool valid, int lane, int g) {
+  f32x4 acc[TS];
+  proj<TIN, TS>(in, acc, A + (size_t)r * TS * TIN * 256, lane);
+  if (valid) {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) st4(dst + n * (16 * ntl) + 16 * (r * TS + t) + 4 * g, acc[t]);
+  }
+}
+template <int NT, int H1T, int P>
+__device__ __forceinline__ void np_project_coop(const f32x4 (&xs)[NT], const f32x4 (&xin)[NT], const NpDesc& d,
+                                                const float* W, size_t n, bool valid, int r, int lane, int g) {
+  constexpr int T2 = 2 * NT;
+  f32x4 in[T2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    in[t] = xs[t];
+    in[NT + t] = xin[t];
+  }
+  if (d.a_u >= 0) proj_store_part<T2, H1T / P>(in, W + d.a_u, r, d.U, n, H1T, valid, lane, g);
+  if (d.a_v >= 0) proj_store_part<T2, H1T / P>(in, W + d.a_v, r, d.V, n, H1T, valid, lane, g);
+  if (d.a_o >= 0) proj_store_part<NT, NT / P>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
+}
+
+template <int NT, int ACT, int LST, int P>
+__global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  constexpr int XS = 16 * 2 * NT + 16 * NT + 4;  // per-wave slab row, as k_edge_hop
+  constexpr int XW = 16 * T2 + 4;                // exchange buffer row
+  constexpr int G = kWaves / P;                  // tile groups per workgroup
+  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float xbuf[G][2][kRowsPerWave][XW];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int grp = w / P, r = w % P;
+  const int tile = blockIdx.x * G + grp;
+  const bool live = tile < a.ntiles;
+  Common c = a.c;
+  f32x4 wf[NT][NT];
+  load_filter<NT>(wf, a.c.W, a.filt_a, lane);
+  EdgeHopRows<NT> q;
+  edge_hop_load<NT, LST>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
+  const bool split = a.reg.split < a.reg_nf;
+  stage_glds<kWaves>(smem, a.c.W, a.reg, 0, a.reg.split);
+  __syncthreads();
+  c.W = smem;
+  if (split) stage_glds<kWaves>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
+  float* slab = &slab_all[w][0][0];
+  float* b0 = &xbuf[grp][0][0][0];
+  float* b1p = &xbuf[grp][1][0][0];
+  const Lanes& L = q.L;
+  // ---- as edge_hop_core up to the MLP (every rank)
+  float* my = slab + j * XS;
+  store_row<T2>(my, q.Vn, T2, g);
+  store_row<NT>(my + 16 * T2, q.inn, NT, g);
+  wave_lds_sync();
+  const float* dr = slab + L.dl * XS;
+  f32x4 H[T2], od[NT];
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  f32x4 vr[T2], br[T2];
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    vr[t] = ld4(dr + off);
+    br[t] = ld4(c.W + b1 + off);
+  }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const f32x4 p = a.Pe ? q.Ps[t] : br[t];
+    H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
+  }
+  load_row<NT>(od, dr + 16 * T2, g);
+  act_tiles<ACT, T2>(H, a.act1, a.slope1);
+  f32x4 sv[NT];
+  if (a.rest.n > 0) {
+    coop_run_mlp<T2, T2, NT, ACT, P>(H, sv, a.rest, c.W, lane, g, j, r, b0, b1p, XW);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sv[t] = H[t];
+  }
+  if (a.normalize) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+    const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 v = sv[t] / nrm;
+      v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
+      v.y = (v.y == v.y) ? v.y : 0.f;
+      v.z = (v.z == v.z) ? v.z : 0.f;
+      v.w = (v.w == v.w) ? v.w : 0.f;
+      sv[t] = v;
+    }
+  }
+  if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
+  put_message<NT>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
+  f32x4 agg[NT];
+  gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
+  // ---- filter on this rank's output tiles, + skip, exchanged into the full row
+  constexpr int TS = NT / P;
+  f32x4 rs[TS];
+#pragma unroll
+  for (int t = 0; t < TS; ++t) rs[t] = pick<NT, TS>(q.inn, r, t);
+  if (a.filt_a >= 0) {
+    f32x4 wr[TS][NT];  // this rank's filter rows, selected with compile-time indices
+#pragma unroll
+    for (int to = 0; to < TS; ++to)
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti) {
+        f32x4 v = wf[to][ti];
+#pragma unroll
+        for (int k = 1; k < P; ++k) v = (r == k) ? wf[k * TS + to][ti] : v;
+        wr[to][ti] = v;
+      }
+    f32x4 acc[TS];
+#pragma unroll
+    for (int to = 0; to < TS; ++to) acc[to] = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int to = 0; to < TS; ++to) acc[to] = MSW_MFMA(wr[to][ti][rr], agg[ti][rr], acc[to]);
+#pragma unroll
+    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + pick<NT, TS>(agg, r, t);
+  }
+  if (a.skip) {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + pick<NT, TS>(q.sk, r, t);
+  }
+  f32x4 res[NT];
+  // the buffer the MLP's last exchange did not use (its readers may still be reading that one)
+  coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? b1p : b0, XW, r, j, g);
+  if (split) __syncthreads();  // every wave: the epilogue operands have landed
+  // ---- finish: store, or the epilogue (projections split over the ranks)
+  if (LST && a.last) {
+    const Epilogue& e = a.epi;
+    if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
+    if (live && r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
+    if (e.np.h1t == T2)
+      np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, live && L.nv, r, lane, g);
+    else
+      np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, live && L.nv, r, lane, g);
+  } else if (live && r == 0 && L.nv && a.out) {
+    store_row<NT>(a.out + L.n * F, res, NT, g);
+  }
+}
+
+template <int NT>
+static const void* edge_coop_kernel(int prelu, int last) {
+  if constexpr (NT == 2) {  // F = 32: each MLP layer's output tiles halve (F = 16 has one)
+    if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
+    return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
+  }
+  return nullptr;
+}
+
 // ---------------------------------------------------------------------------- hop
 // Hops 2..K (gnn.py:406-443) over the same tiles:
 //   active(e) = rowsum(out[src]) != 0 || rowsum(out[dst]) != 0          (gnn.py:408-411)
@@ -1373,6 +1602,15 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
+  if constexpr (NT == 2) {  // cooperative edge hops: 160 KB minus slabs and exchange buffers
+    const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
+    for (int prelu = 0; prelu < 2; ++prelu)
+      for (int last = 0; last < 2; ++last) {
+        hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024 - st);
+        if (e != hipSuccess) return e;
+      }
+  }
   // hop chains: 160 KB minus their own (narrower) static slabs
   constexpr int WC = chain_waves<NT>();
   for (int m = 2; m <= kChainMax; ++m)
@@ -1420,6 +1658,13 @@ static const void* edge_hop_kernel(int prelu, bool loop, int last) {
 template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
+  if (a.coop == 2) {
+    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last);
+    if (!f) return hipErrorInvalidValue;
+    void* args[] = {const_cast<EdgeHopArgs*>(&a)};
+    return hipLaunchKernel(f, dim3(cdiv((long)a.ntiles * 2, kWaves)), dim3(kBlock), args,
+                           eh_lds_bytes(a.reg_nf), st);
+  }
   const bool loop = tile_loop(a);
   const dim3 grid(tile_grid(a)),
       block(64 * (loop ? (a.last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves));
@@ -1509,6 +1754,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 3: return (const void*)k_pool<NT, LOOP>;
     case 5: return (const void*)k_pool_edge<NT>;
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
+    case 7: return edge_coop_kernel<NT>(prelu, last);
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }
@@ -1517,7 +1763,8 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const void* f = kind == 4 ? hopm_kernel<NT>(loop, last, prelu)
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
-  const size_t dyn = kind == 4 ? dyn_bytes : kind == 1 ? eh_lds_bytes((int)(dyn_bytes / 4))
+  if (!f) return 0;
+  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)

@@ -370,6 +370,9 @@ struct msw_plan {
   // device (measured, rocprofv3 step breakdown), inside a graph the steps run back to back.
   // MSW_GRAPH_STEPS overrides (1: one graph launch per step).
   int graph_steps = 16;
+  // Fused edge MLP + hop with two waves per tile (k_edge_coop) when 2 x tiles <= coop_waves
+  // (MSW_COOP_WAVES; 0: never).
+  int coop_waves = 2048;
   std::vector<void*> owned;
   void drop_graphs() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
@@ -914,11 +917,22 @@ void set_grid_cap(msw_plan* P, Launch& L) {
     case L_ENCODE:
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
       break;
-    case L_EDGE_HOP:
-      caps(P, L.eh, 1, L.eh.c.prelu, L.eh.last, L.eh.reg.len);
-      L.eh.fit_blocks = resident_of(P->NT, 1, L.eh.c.prelu, L.eh.last, (size_t)L.eh.reg_nf * 4, 0);
-      if (no_loop("eh")) L.eh.max_blocks = 0;
+    case L_EDGE_HOP: {
+      EdgeHopArgs& a = L.eh;
+      caps(P, a, 1, a.c.prelu, a.last, a.reg.len);
+      a.fit_blocks = resident_of(P->NT, 1, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0);
+      if (no_loop("eh")) a.max_blocks = 0;
+      // two waves per tile (k_edge_coop) while the tiles leave most SIMDs idle: one tile
+      // per wave at most, no grid-stride loop, an epilogue of projections only
+      const bool loop = a.fit_blocks > 0 && a.max_blocks > 0 && (a.ntiles + kWaves - 1) / kWaves > a.fit_blocks;
+      const bool epi_ok = !a.last || (!a.epi.dec.on && a.epi.uu_a < 0);
+      // ... and its grid resident at once (a second round of workgroups costs more than the
+      // halved MLP chain saves: measured +4.7 us on the finest unpooling of zenodo4)
+      const int coop_fit = P->NT == 2 ? resident_of(P->NT, 7, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0) : 0;
+      a.coop = (P->NT == 2 && !loop && epi_ok && P->coop_waves > 0 && 2L * a.ntiles <= P->coop_waves &&
+                (2 * a.ntiles + kWaves - 1) / kWaves <= coop_fit) ? 2 : 0;
       break;
+    }
     case L_HOP:
       caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
       // one tile per wave below kHopLoopTiles (MSW_HOP_LOOP=1: loop whenever the grid does
@@ -1408,6 +1422,7 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
 
   if (const char* es = getenv("MSW_EPI_SPLIT_TILES")) P->epi_split_tiles = atoi(es);
   if (const char* gs = getenv("MSW_GRAPH_STEPS")) P->graph_steps = std::max(1, atoi(gs));
+  if (const char* cw = getenv("MSW_COOP_WAVES")) P->coop_waves = std::max(0, atoi(cw));
   if (const char* cm = getenv("MSW_HOP_CHAINS")) {  // a chain's halo is m-1 rings deep: not on parts
     P->chain_max = std::max(2, std::min(kChainMax, atoi(cm)));
     P->hop_pairs = xch ? 0 : 1;

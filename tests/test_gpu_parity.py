@@ -133,6 +133,26 @@ def test_row_epilogue_split_matches_fused(cuda, model, monkeypatch):
     assert per_step_rel(r, torch.from_numpy(fx["rollout"])) <= REL_TOL
 
 
+def test_coop_edge_hop_matches_single_wave(cuda, monkeypatch):
+    """Two waves per tile in the fused edge MLP + hop (k_edge_coop, on by default while the
+    tiles leave SIMDs idle) == one wave per tile (MSW_COOP_WAVES=0), bit for bit, incl. the
+    unpooling layers' projection epilogue; and against the reference fixture."""
+    fx = golden("fx_small_K4_F32_rollout48")
+    g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+    m1 = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    with torch.no_grad():
+        y1 = m1(g).cpu()
+    r1 = m1.rollout(g).cpu()
+    monkeypatch.setenv("MSW_COOP_WAVES", "0")
+    m0 = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    with torch.no_grad():
+        y0 = m0(g).cpu()
+    r0 = m0.rollout(g).cpu()
+    assert torch.equal(y1, y0)
+    assert torch.equal(r1, r0)
+    assert per_step_rel(r1, torch.from_numpy(fx["rollout"])) <= REL_TOL
+
+
 def test_rollout_zenodo_size_vs_reference(cuda):
     fx = golden("fx_zenodo4_K4_F32_rollout48")
     g = make_multiscale_mesh(**mesh_config("zenodo4"), T=48).to(cuda)
