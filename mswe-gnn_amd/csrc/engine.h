@@ -255,6 +255,7 @@ struct PoolArgs {
   const float* in;         // x_down
   const float* xs;
   NpDesc np;
+  int coop;                // edge tiles: 2 = two waves per tile (projection split), else one
 };
 
 // Epilogue of a layer's last hop on dense 16-row node tiles (large scales, plan.hip

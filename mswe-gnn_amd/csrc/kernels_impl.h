@@ -1414,7 +1414,9 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_pool(PoolArgs a
 // children in all, lane j loads child j, the coarse lanes sum through LDS -- four times
 // the waves of the row layout, each with a shorter load chain (measured faster while the
 // launch is latency-bound).
-template <int NT>
+// P = 2: two waves per tile, both summing the children, the projection's output tiles split
+// between them (as k_edge_coop; bit-identical).
+template <int NT, int P = 1>
 __global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
@@ -1422,7 +1424,8 @@ __global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
   __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  int tile = blockIdx.x * kWaves + w;
+  int tile = blockIdx.x * (kWaves / P) + w / P;
+  const int rk = w % P;
   Common c = a.c;
   MSW_MARK(c, 0);
   struct Rows {
@@ -1444,7 +1447,14 @@ __global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
     const float cnt = (float)(L.q1 - L.q0 > 0 ? L.q1 - L.q0 : 1);
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = acc[t] / cnt;
-    np_project<NT>(r.xs, acc, a.np, c.W, L.n, L.nv, lane, g);
+    if constexpr (P == 1) {
+      np_project<NT>(r.xs, acc, a.np, c.W, L.n, L.nv, lane, g);
+    } else {
+      if (a.np.h1t == 2 * NT)
+        np_project_coop<NT, 2 * NT, P>(r.xs, acc, a.np, c.W, L.n, L.nv, rk, lane, g);
+      else
+        np_project_coop<NT, NT, P>(r.xs, acc, a.np, c.W, L.n, L.nv, rk, lane, g);
+    }
   };
   Rows r0;
   load(r0, tile < a.ntiles ? tile : 0, j, g);
@@ -1595,7 +1605,7 @@ hipError_t prepare_kernels() {
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
       {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
-      {(const void*)k_pool_edge<NT>, kWaves},
+      {(const void*)k_pool_edge<NT>, kWaves}, {(const void*)k_pool_edge<NT, NT == 2 ? 2 : 1>, kWaves},
       {(const void*)k_epi<NT, 1, false>, kWaves}, {(const void*)k_epi<NT, -1, false>, kWaves},
       {(const void*)k_epi<NT, 1, true>, WL}, {(const void*)k_epi<NT, -1, true>, WL}};
   for (const auto& f : fns) {
@@ -1697,6 +1707,12 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (!a.rows) {
+    if constexpr (NT == 2) {
+      if (a.coop == 2) {
+        hipLaunchKernelGGL((k_pool_edge<NT, 2>), dim3(cdiv((long)a.ntiles * 2, kWaves)), dim3(kBlock), sh, st, a);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((k_pool_edge<NT>), dim3(cdiv(a.ntiles, kWaves)), dim3(kBlock), sh, st, a);
     return hipGetLastError();
   }

@@ -372,7 +372,7 @@ struct msw_plan {
   int graph_steps = 16;
   // Fused edge MLP + hop with two waves per tile (k_edge_coop) when 2 x tiles <= coop_waves
   // (MSW_COOP_WAVES; 0: never).
-  int coop_waves = 2048;
+  int coop_waves = 1024;
   std::vector<void*> owned;
   void drop_graphs() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
@@ -959,6 +959,9 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       a.rows = !(fe > 0 && (a.etiles + kWaves - 1) / kWaves <= fe) || getenv("MSW_POOL_ROWS") != nullptr;
       a.ntiles = a.rows ? a.rtiles : a.etiles;
       caps(P, a, 3, 0, 0, a.reg.len);
+      // two waves per edge tile (projection split) while that grid too is resident at once
+      a.coop = (!a.rows && P->NT == 2 && P->coop_waves > 0 && 2L * a.etiles <= P->coop_waves &&
+                (2 * a.etiles + kWaves - 1) / kWaves <= fe) ? 2 : 0;
       break;
     }
   }

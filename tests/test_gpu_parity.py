@@ -134,9 +134,10 @@ def test_row_epilogue_split_matches_fused(cuda, model, monkeypatch):
 
 
 def test_coop_edge_hop_matches_single_wave(cuda, monkeypatch):
-    """Two waves per tile in the fused edge MLP + hop (k_edge_coop, on by default while the
-    tiles leave SIMDs idle) == one wave per tile (MSW_COOP_WAVES=0), bit for bit, incl. the
-    unpooling layers' projection epilogue; and against the reference fixture."""
+    """Two waves per tile in the fused edge MLP + hop (k_edge_coop) and in the edge-tile
+    pooling (k_pool_edge<.., 2>), on by default while the tiles leave SIMDs idle, == one wave
+    per tile (MSW_COOP_WAVES=0), bit for bit, incl. the unpooling layers' projection
+    epilogue; and against the reference fixture."""
     fx = golden("fx_small_K4_F32_rollout48")
     g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
     m1 = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
