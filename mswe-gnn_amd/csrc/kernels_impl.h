@@ -997,11 +997,126 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   }
 }
 
+// F = 64 (NT = 4): the whole workgroup (4 waves) on one tile, one slab shared by the four
+// ranks (rank 0 writes the node rows and the messages) so that the 96 KB edge-MLP region
+// still fits beside it; the epilogue's operands stay in the blob (F = 64 relocation).
+template <int ACT, int LST>
+__global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int NT = 4, P = 4, F = 16 * NT, T2 = 2 * NT;
+  constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
+  constexpr int XW = 16 * T2 + 4;
+  __shared__ __attribute__((aligned(16))) float slab[kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float xbuf[2][kRowsPerWave][XW];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, r = wave_id();
+  const int tile = blockIdx.x;
+  Common c = a.c;  // c.W stays the blob: the epilogue reads it there
+  // this rank's filter row (out tile r): wr[ti] = W_1 block (r, ti)
+  f32x4 wr[NT];
+  {
+    const int fa = a.filt_a >= 0 ? a.filt_a : 0;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) wr[ti] = ld4(c.W + fa + ((size_t)(r * NT + ti) * 64 + lane) * 4);
+  }
+  EdgeHopRows<NT> q;
+  edge_hop_load<NT, LST>(q, a, tile, j, g);
+  const Lanes& L = q.L;
+  if (a.reg.len > 0) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
+  const float* Wm = a.reg.len > 0 ? (const float*)smem : c.W;
+  float* my = &slab[j][0];
+  if (r == 0) {
+    store_row<T2>(my, q.Vn, T2, g);
+    store_row<NT>(my + 16 * T2, q.inn, NT, g);
+  }
+  __syncthreads();  // node rows and the MLP region have landed
+  const float* dr = &slab[L.dl][0];
+  f32x4 H[T2], od[NT];
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  f32x4 vr[T2], br[T2];
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    vr[t] = ld4(dr + off);
+    br[t] = ld4(Wm + b1 + off);
+  }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const f32x4 p = a.Pe ? q.Ps[t] : br[t];
+    H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
+  }
+  load_row<NT>(od, dr + 16 * T2, g);
+  act_tiles<ACT, T2>(H, a.act1, a.slope1);
+  f32x4 sv[NT];
+  if (a.rest.n > 0) {
+    coop_run_mlp<T2, T2, NT, ACT, P>(H, sv, a.rest, Wm, lane, g, j, r, &xbuf[0][0][0], &xbuf[1][0][0], XW);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sv[t] = H[t];
+  }
+  if (a.normalize) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+    const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 v = sv[t] / nrm;
+      v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
+      v.y = (v.y == v.y) ? v.y : 0.f;
+      v.z = (v.z == v.z) ? v.z : 0.f;
+      v.w = (v.w == v.w) ? v.w : 0.f;
+      sv[t] = v;
+    }
+  }
+  if (r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
+  // every rank has read the slab's node rows before the first MLP exchange barrier: rank 0
+  // may overwrite them with the messages (a.rest.n == 0 has no barrier: add one)
+  if (a.rest.n == 0) __syncthreads();
+  if (r == 0) put_message<NT>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
+  __syncthreads();
+  f32x4 agg[NT];
+  gather_messages<NT, XS>(agg, &slab[0][0], L.q0, L.q1, g);
+  // this rank's tile of inn / agg / skip by address (a 4-way select over a register array
+  // was turned back into a scratch-indexed load): inn sits past the messages in the slab row
+  f32x4 rs[1];
+  rs[0] = ld4(&slab[j][16 * T2 + 16 * r + 4 * g]);
+  if (a.filt_a >= 0) {
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc = MSW_MFMA(wr[ti][rr], agg[ti][rr], acc);
+    rs[0] = rs[0] + acc;
+  } else {
+    f32x4 ag = zero4();
+    for (int qq = L.q0; qq < L.q1; ++qq) ag = ag + ld4(&slab[qq][16 * r + 4 * g]);
+    rs[0] = rs[0] + ag;
+  }
+  if (a.skip) rs[0] = rs[0] + ld4(a.skip + L.n * F + 16 * r + 4 * g);
+  f32x4 res[NT];
+  coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? &xbuf[1][0][0] : &xbuf[0][0][0], XW, r, j, g);
+  if (LST && a.last) {
+    const Epilogue& e = a.epi;
+    if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
+    if (r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
+    if (e.np.h1t == T2)
+      np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv, r, lane, g);
+    else
+      np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv, r, lane, g);
+  } else if (r == 0 && L.nv && a.out) {
+    store_row<NT>(a.out + L.n * F, res, NT, g);
+  }
+}
+
 template <int NT>
 static const void* edge_coop_kernel(int prelu, int last) {
   if constexpr (NT == 2) {  // F = 32: each MLP layer's output tiles halve (F = 16 has one)
     if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
     return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
+  } else if constexpr (NT == 4) {  // F = 64: four waves per tile
+    if (last) return prelu ? (const void*)k_edge_coop4<1, 1> : (const void*)k_edge_coop4<-1, 1>;
+    return prelu ? (const void*)k_edge_coop4<1, 0> : (const void*)k_edge_coop4<-1, 0>;
   }
   return nullptr;
 }
@@ -1605,12 +1720,21 @@ hipError_t prepare_kernels() {
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
       {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
-      {(const void*)k_pool_edge<NT>, kWaves}, {(const void*)k_pool_edge<NT, NT == 2 ? 2 : 1>, kWaves},
+      {(const void*)k_pool_edge<NT>, kWaves}, {(const void*)k_pool_edge<NT, NT >= 2 ? NT : 1>, kWaves},
       {(const void*)k_epi<NT, 1, false>, kWaves}, {(const void*)k_epi<NT, -1, false>, kWaves},
       {(const void*)k_epi<NT, 1, true>, WL}, {(const void*)k_epi<NT, -1, true>, WL}};
   for (const auto& f : fns) {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
+  }
+  if constexpr (NT == 4) {  // F = 64 cooperative edge hops: one shared slab + exchange buffers
+    const int st = kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4;
+    for (int prelu = 0; prelu < 2; ++prelu)
+      for (int last = 0; last < 2; ++last) {
+        hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024 - st);
+        if (e != hipSuccess) return e;
+      }
   }
   if constexpr (NT == 2) {  // cooperative edge hops: 160 KB minus slabs and exchange buffers
     const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
@@ -1668,11 +1792,11 @@ static const void* edge_hop_kernel(int prelu, bool loop, int last) {
 template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  if (a.coop == 2) {
+  if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
     const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last);
     if (!f) return hipErrorInvalidValue;
     void* args[] = {const_cast<EdgeHopArgs*>(&a)};
-    return hipLaunchKernel(f, dim3(cdiv((long)a.ntiles * 2, kWaves)), dim3(kBlock), args,
+    return hipLaunchKernel(f, dim3(cdiv((long)a.ntiles * a.coop, kWaves)), dim3(kBlock), args,
                            eh_lds_bytes(a.reg_nf), st);
   }
   const bool loop = tile_loop(a);
@@ -1707,9 +1831,9 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (!a.rows) {
-    if constexpr (NT == 2) {
-      if (a.coop == 2) {
-        hipLaunchKernelGGL((k_pool_edge<NT, 2>), dim3(cdiv((long)a.ntiles * 2, kWaves)), dim3(kBlock), sh, st, a);
+    if constexpr (NT >= 2) {  // waves per tile: 2 (F = 32), 4 (F = 64)
+      if (a.coop == NT) {
+        hipLaunchKernelGGL((k_pool_edge<NT, NT>), dim3(cdiv((long)a.ntiles * NT, kWaves)), dim3(kBlock), sh, st, a);
         return hipGetLastError();
       }
     }

@@ -928,9 +928,11 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       const bool epi_ok = !a.last || (!a.epi.dec.on && a.epi.uu_a < 0);
       // ... and its grid resident at once (a second round of workgroups costs more than the
       // halved MLP chain saves: measured +4.7 us on the finest unpooling of zenodo4)
-      const int coop_fit = P->NT == 2 ? resident_of(P->NT, 7, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0) : 0;
-      a.coop = (P->NT == 2 && !loop && epi_ok && P->coop_waves > 0 && 2L * a.ntiles <= P->coop_waves &&
-                (2 * a.ntiles + kWaves - 1) / kWaves <= coop_fit) ? 2 : 0;
+      // (F = 32: two waves per tile; F = 64: four, one tile per workgroup)
+      const int pw = P->NT == 2 ? 2 : P->NT == 4 ? 4 : 0;
+      const int coop_fit = pw ? resident_of(P->NT, 7, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0) : 0;
+      a.coop = (pw && !loop && epi_ok && P->coop_waves > 0 && (long)pw * a.ntiles <= P->coop_waves &&
+                (pw * a.ntiles + kWaves - 1) / kWaves <= coop_fit) ? pw : 0;
       break;
     }
     case L_HOP:
@@ -960,8 +962,10 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       a.ntiles = a.rows ? a.rtiles : a.etiles;
       caps(P, a, 3, 0, 0, a.reg.len);
       // two waves per edge tile (projection split) while that grid too is resident at once
-      a.coop = (!a.rows && P->NT == 2 && P->coop_waves > 0 && 2L * a.etiles <= P->coop_waves &&
-                (2 * a.etiles + kWaves - 1) / kWaves <= fe) ? 2 : 0;
+      // (F = 32: two waves per tile, F = 64: four)
+      const int pw = P->NT >= 2 ? P->NT : 0;
+      a.coop = (!a.rows && pw && P->coop_waves > 0 && (long)pw * a.etiles <= P->coop_waves &&
+                (pw * a.etiles + kWaves - 1) / kWaves <= fe) ? pw : 0;
       break;
     }
   }

@@ -133,25 +133,30 @@ def test_row_epilogue_split_matches_fused(cuda, model, monkeypatch):
     assert per_step_rel(r, torch.from_numpy(fx["rollout"])) <= REL_TOL
 
 
-def test_coop_edge_hop_matches_single_wave(cuda, monkeypatch):
+@pytest.mark.parametrize("F", [32, 64])
+def test_coop_edge_hop_matches_single_wave(cuda, monkeypatch, F):
     """Two waves per tile in the fused edge MLP + hop (k_edge_coop) and in the edge-tile
     pooling (k_pool_edge<.., 2>), on by default while the tiles leave SIMDs idle, == one wave
     per tile (MSW_COOP_WAVES=0), bit for bit, incl. the unpooling layers' projection
     epilogue; and against the reference fixture."""
     fx = golden("fx_small_K4_F32_rollout48")
     g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
-    m1 = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    if F == 64:  # seeded init (no F = 64 checkpoint), wet start so that every scale is active
+        g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=12), seed=5).to(cuda)
+    build = lambda: _hip(build_msgnn(4, F, 4, state=weights("K4_F32") if F == 32 else None), cuda)
+    m1 = build()
     with torch.no_grad():
         y1 = m1(g).cpu()
     r1 = m1.rollout(g).cpu()
     monkeypatch.setenv("MSW_COOP_WAVES", "0")
-    m0 = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    m0 = build()
     with torch.no_grad():
         y0 = m0(g).cpu()
     r0 = m0.rollout(g).cpu()
     assert torch.equal(y1, y0)
     assert torch.equal(r1, r0)
-    assert per_step_rel(r1, torch.from_numpy(fx["rollout"])) <= REL_TOL
+    if F == 32:
+        assert per_step_rel(r1, torch.from_numpy(fx["rollout"])) <= REL_TOL
 
 
 def test_rollout_zenodo_size_vs_reference(cuda):
