@@ -252,6 +252,35 @@ def test_variants_vs_oracle(cuda):
     assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL
 
 
+def test_max_in_degree_and_unsupported_degree(cuda):
+    """Limits of the edge tiles: a node with 16 in-edges (a whole tile of
+    its own) matches the oracle; 17 in-edges is refused at plan creation with an error,
+    never a fault."""
+    def star(extra):
+        gs = wet_state(make_single_scale_mesh(n_coarse=3, refinements=2, T=3), seed=9)
+        ei = gs.edge_index
+        have = set(ei[0, ei[1] == 0].tolist()) | {0}
+        add = [u for u in range(1, gs.x.shape[0]) if u not in have][:extra]
+        new = torch.tensor([add, [0] * len(add)], dtype=ei.dtype)
+        gs.edge_index = torch.cat([ei, new], 1)
+        gen = torch.Generator().manual_seed(3)
+        gs.edge_attr = torch.cat([gs.edge_attr, torch.rand(len(add), gs.edge_attr.shape[1], generator=gen)], 0)
+        return gs
+    base = int((make_single_scale_mesh(n_coarse=3, refinements=2, T=3).edge_index[1] == 0).sum())
+    g16 = star(16 - base)
+    assert int((g16.edge_index[1] == 0).sum()) == 16
+    m = build_gnn(hid=32, K=2, n_layers=2, mlp_layers=2)
+    cfg = orc.gnn_config(hid_features=32, K=2, n_GNN_layers=2, mlp_layers=2)
+    ref = orc.rollout(state_dict_of(m), cfg, g16)
+    mh = _hip(m, cuda)
+    assert per_step_rel(mh.rollout(g16.to(cuda)).cpu(), ref) <= REL_TOL
+    g17 = star(17 - base)
+    m2 = _hip(build_gnn(hid=32, K=2, n_layers=2, mlp_layers=2), cuda)
+    with pytest.raises(RuntimeError, match="16 in-edges"):
+        with torch.no_grad():
+            m2(g17.to(cuda))
+
+
 def test_batched_graphs_match_individual(cuda):
     """Two simulations as one disjoint-union batch (update_batch_multiscale layout,
     training/train.py:31-65) give the same rollouts as each alone."""
