@@ -183,6 +183,7 @@ struct HopArgs {
   int grad, upwind;
   int last;
   Epilogue epi;
+  int coop;          // last hop: waves per tile (k_hop_coop), 0 = one
 };
 
 // Hop chain: M = 2 or 3 consecutive hops (k .. k+M-1) in one launch, the last of them

@@ -261,6 +261,10 @@ __device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, c
 // tanh(x_up) -> node_decoder -> + learned residual -> ReLU -> small-depth mask
 // (gnn.py:335-348, models.py:50-91); rollout mode: use_prediction + BC of the next step
 // (dataset.py:486-529) and the rollout write (train.py:88-95).
+// decode_tail: what follows the decoder MLP (o = its output tile: h, |q| in lane group 0)
+template <int NT>
+__device__ __forceinline__ void decode_tail(const f32x4 (&o)[1], const DecDesc& d, const Common& c,
+                                            const EpiPre<NT>& pre, int n, bool valid, int g);
 template <int NT, int ACT>
 __device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDesc& d, const Common& c,
                                             const EpiPre<NT>& pre, int n, bool valid, int lane, int g) {
@@ -270,6 +274,12 @@ __device__ __forceinline__ void decode_rows(const f32x4 (&xup)[NT], const DecDes
   for (int t = 0; t < NT; ++t) x0[t] = xup[t];
   act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
   run_mlp<NT, NT, 1, ACT>(x0, o, d.dec, c.W, lane, g);
+  decode_tail<NT>(o, d, c, pre, n, valid, g);
+}
+template <int NT>
+__device__ __forceinline__ void decode_tail(const f32x4 (&o)[1], const DecDesc& d, const Common& c,
+                                            const EpiPre<NT>& pre, int n, bool valid, int g) {
+#pragma clang fp contract(off)
   if (!valid || g) return;  // lane group 0 holds output features 0 (h) and 1 (|q|)
   const int ext = pre.ext;
   if (ext < 0) return;
@@ -1249,6 +1259,138 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_hop(HopArgs a) 
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- cooperative last hop
+// A layer's last hop + its epilogue with P waves per tile (small scales, as k_edge_coop):
+// every rank does the hop's VALU / LDS work; the filter, the projections (next layer U/V/O,
+// unpool U) and the decoder's hidden layers are split by output tile and exchanged through
+// LDS; the decoder's 2-wide output layer runs on every rank, its tail on rank 0.
+template <int NT, int ACT, int P>
+__device__ __forceinline__ void node_epilogue_coop(f32x4 (&res)[NT], const Epilogue& e, const Common& c,
+                                                   const EpiPre<NT>& pre, float* out, int n, bool valid,
+                                                   int r, int lane, int g, int j, float* b0, float* b1, int xw) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
+  if (out && valid && r == 0) store_row<NT>(out + (size_t)n * F, res, NT, g);
+  if (e.np.a_u >= 0 || e.np.a_v >= 0 || e.np.a_o >= 0) {
+    if (e.np.h1t == T2)
+      np_project_coop<NT, T2, P>(pre.xs, res, e.np, c.W, (size_t)n, valid, r, lane, g);
+    else
+      np_project_coop<NT, NT, P>(pre.xs, res, e.np, c.W, (size_t)n, valid, r, lane, g);
+  }
+  if (e.uu_a >= 0) {
+    f32x4 in[T2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      in[t] = pre.xs[t];
+      in[NT + t] = res[t];
+    }
+    if (e.uu_h1t == T2)
+      proj_store_part<T2, T2 / P>(in, c.W + e.uu_a, r, e.Uu, (size_t)n, T2, valid, lane, g);
+    else
+      proj_store_part<T2, NT / P>(in, c.W + e.uu_a, r, e.Uu, (size_t)n, NT, valid, lane, g);
+  }
+  if (e.dec.on) {
+    const DecDesc& d = e.dec;
+    f32x4 x0[NT], o[1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) x0[t] = res[t];
+    act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
+    const MlpDev& m = d.dec;
+    if (m.n == 1) {
+      mfma_layer<NT, 1, ACT>(x0, o, m.l[0], c.W, lane, g);
+    } else {  // hidden layers split (exchanges alternate b1, b0, ...: b0 held the result row)
+      f32x4 h[NT];
+      {
+        f32x4 p[NT / P];
+        mfma_layer_sub<NT, NT / P, ACT>(x0, p, m.l[0], c.W, r * (NT / P), lane, g);
+        coop_exchange<NT, P>(p, h, b1, xw, r, j, g);
+      }
+      for (int li = 1; li + 1 < m.n; ++li) {
+        f32x4 p[NT / P];
+        mfma_layer_sub<NT, NT / P, ACT>(h, p, m.l[li], c.W, r * (NT / P), lane, g);
+        coop_exchange<NT, P>(p, h, (li & 1) ? b0 : b1, xw, r, j, g);
+      }
+      mfma_layer<NT, 1, ACT>(h, o, m.l[m.n - 1], c.W, lane, g);
+    }
+    if (r == 0) decode_tail<NT>(o, d, c, pre, n, valid, g);
+  }
+}
+
+template <int NT, int ACT, int P>
+__global__ __launch_bounds__(kBlock) void k_hop_coop(HopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, TS = NT / P;
+  constexpr int XS = F + 4;
+  constexpr int XW = 16 * NT + 4;
+  constexpr int G = kWaves / P;
+  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float xbuf[G][2][kRowsPerWave][XW];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int grp = w / P, r = w % P;
+  const int tile = blockIdx.x * G + grp;
+  const bool live = tile < a.ntiles;
+  Common c = a.c;
+  // this rank's filter rows (out tiles r TS .. r TS + TS - 1), by address
+  f32x4 wr[TS][NT];
+  {
+    const int fa = a.filt_a >= 0 ? a.filt_a : 0;
+#pragma unroll
+    for (int to = 0; to < TS; ++to)
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti) wr[to][ti] = ld4(c.W + fa + ((size_t)((r * TS + to) * NT + ti) * 64 + lane) * 4);
+  }
+  HopRows<NT> q;
+  hop_load<NT, true>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
+  if constexpr (kStaged<NT>) stage_glds<kWaves>(smem, a.c.W, a.reg, 0, a.reg.len);  // epilogue operands
+  const Lanes& L = q.L;
+  float* slab = &slab_all[w][0][0];
+  float* my = slab + j * XS;
+  store_row<NT>(my, q.inn, NT, g);
+  wave_lds_sync();
+  f32x4 od[NT];
+  load_row<NT>(od, slab + L.dl * XS, g);
+  put_message<NT>(my, q.os, od, q.sv, L.ev, a.grad, a.upwind, g);
+  f32x4 agg[NT];
+  gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
+  f32x4 rs[TS];
+#pragma unroll
+  for (int t = 0; t < TS; ++t) rs[t] = ld4(a.in + L.n * F + 16 * (r * TS + t) + 4 * g);  // inn, by address
+  if (a.filt_a >= 0) {
+    f32x4 acc[TS];
+#pragma unroll
+    for (int to = 0; to < TS; ++to) acc[to] = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int to = 0; to < TS; ++to) acc[to] = MSW_MFMA(wr[to][ti][rr], agg[ti][rr], acc[to]);
+#pragma unroll
+    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+      f32x4 ag = zero4();
+      for (int qq = L.q0; qq < L.q1; ++qq) ag = ag + ld4(slab + qq * XS + 16 * (r * TS + t) + 4 * g);
+      rs[t] = rs[t] + ag;
+    }
+  }
+  f32x4 res[NT];
+  float* b0 = &xbuf[grp][0][0][0];
+  float* b1 = &xbuf[grp][1][0][0];
+  coop_exchange<NT, P>(rs, res, b0, XW, r, j, g);  // its barrier also lands the staged operands
+  if constexpr (kStaged<NT>) c.W = smem;
+  node_epilogue_coop<NT, ACT, P>(res, a.epi, c, q.pre, a.out, (int)L.n, live && L.nv, r, lane, g, j, b0, b1, XW);
+}
+
+template <int NT>
+static const void* hop_coop_kernel(int prelu) {
+  if constexpr (NT >= 2) return prelu ? (const void*)k_hop_coop<NT, 1, NT> : (const void*)k_hop_coop<NT, -1, NT>;
+  return nullptr;
+}
+
 // ---------------------------------------------------------------------------- hop chain
 // Hops k .. k+M-1 in one launch (engine.h HopMArgs).  Grid-stride over workgroup blocks;
 // every wave of a workgroup walks the same blocks and levels, so the barriers are uniform.
@@ -1727,6 +1869,12 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
+  if constexpr (NT >= 2) {  // cooperative last hops (F = 32, 64)
+    for (int prelu = 0; prelu < 2; ++prelu) {
+      hipError_t e = hipFuncSetAttribute(hop_coop_kernel<NT>(prelu), hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
+      if (e != hipSuccess) return e;
+    }
+  }
   if constexpr (NT == 4) {  // F = 64 cooperative edge hops: one shared slab + exchange buffers
     const int st = kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4;
     for (int prelu = 0; prelu < 2; ++prelu)
@@ -1809,6 +1957,13 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
+  if (a.coop > 1 && a.last) {  // waves per tile = NT (2 for F = 32, 4 for F = 64)
+    const void* f = hop_coop_kernel<NT>(a.c.prelu);
+    if (!f) return hipErrorInvalidValue;
+    void* args[] = {const_cast<HopArgs*>(&a)};
+    return hipLaunchKernel(f, dim3(cdiv((long)a.ntiles * a.coop, kWaves)), dim3(kBlock), args,
+                           lds_bytes<NT>(a.reg.len), st);
+  }
   const bool loop = tile_loop(a);
   const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
   if (!a.last) {
@@ -1895,6 +2050,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 5: return (const void*)k_pool_edge<NT>;
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     case 7: return edge_coop_kernel<NT>(prelu, last);
+    case 9: return hop_coop_kernel<NT>(prelu);
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }

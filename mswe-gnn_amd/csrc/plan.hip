@@ -942,6 +942,15 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
       // (profiles/r01_v7/ab_edge_waves.txt)
       if (no_loop("hop") || (!getenv("MSW_HOP_LOOP") && L.hop.ntiles < kHopLoopTiles)) L.hop.max_blocks = 0;
+      {  // a last hop with an epilogue on few tiles: P = F / 16 waves per tile (k_hop_coop)
+        HopArgs& h = L.hop;
+        const bool loop = h.fit_blocks > 0 && h.max_blocks > 0 && (h.ntiles + kWaves - 1) / kWaves > h.fit_blocks;
+        const int pw = P->NT >= 2 ? P->NT : 0;
+        h.coop = 0;
+        if (h.last && pw && !loop && P->coop_waves > 0 && (long)pw * h.ntiles <= P->coop_waves &&
+            (pw * h.ntiles + kWaves - 1) / kWaves <= resident_of(P->NT, 9, h.c.prelu, 1, (size_t)h.reg.len * 4, 0))
+          h.coop = pw;
+      }
       break;
     case L_HOPM: {
       HopMArgs& a = L.hopm;
