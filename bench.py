@@ -238,97 +238,109 @@ def main():
         # ---------------- the launch floor the zenodo-size hop is bound by: one dependent
         # gather of the previous launch's rows (torch.index_select, same rows x F) per launch
         # of a captured 35-launch graph (tools/launch_floor.py)
-        if world == 1:
-            sys.path.insert(0, os.path.join(ROOT, "tools"))
-            import launch_floor as lf
-            small = torch.ones(1024, device=dev)
-            perm = torch.randperm(rows, device=dev)
-            bufs = [torch.randn(rows, F, device=dev), torch.empty(rows, F, device=dev)]
-            flip = {"i": 0}
+        try:  # optional: a failure here is recorded, never drops the result line
+            if world == 1:
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                import launch_floor as lf
+                small = torch.ones(1024, device=dev)
+                perm = torch.randperm(rows, device=dev)
+                bufs = [torch.randn(rows, F, device=dev), torch.empty(rows, F, device=dev)]
+                flip = {"i": 0}
 
-            def _gather():
-                i = flip["i"]
-                torch.index_select(bufs[i], 0, perm, out=bufs[1 - i])
-                flip["i"] = 1 - i
-            roof["launch_floor"] = {
-                "trivial_us": lf.per_launch_us(lambda: small.mul_(1.0), 35),
-                "dependent_row_gather_us": lf.per_launch_us(_gather, 35),
-                "note": "per launch, 35 dependent launches in one graph; the gather reads the "
-                        "previous launch's rows (same rows x F as the roofline hop)"}
-            del small, perm, bufs
+                def _gather():
+                    i = flip["i"]
+                    torch.index_select(bufs[i], 0, perm, out=bufs[1 - i])
+                    flip["i"] = 1 - i
+                roof["launch_floor"] = {
+                    "trivial_us": lf.per_launch_us(lambda: small.mul_(1.0), 35),
+                    "dependent_row_gather_us": lf.per_launch_us(_gather, 35),
+                    "note": "per launch, 35 dependent launches in one graph; the gather reads the "
+                            "previous launch's rows (same rows x F as the roofline hop)"}
+                del small, perm, bufs
+        except Exception as e:  # noqa: BLE001
+            roof["launch_floor"] = {"error": repr(e)}
         # ---------------- the same hop kernel where HBM, not latency, bounds it: the ~1M-node
         # mesh of config 5 (fully wet; one rollout step to populate the buffers)
-        if world == 1 and not args.no_roofline_large and args.workload != "hbm1m":
-            gl, ml, _, dl = build_workload("hbm1m", seed=0, T=1)
-            gl = gl.to(dev)
-            ml = ml.to(dev)
-            ml.engine = "hip"
-            pl = plan_for(ml, gl)
-            pl.rollout(gl.x, gl.BC, gl.node_BC, gl.type_BC, 1)
-            tl, (rl, el) = time_kernel(pl, "hop", 0, iters=50)
-            bl = el * (4 * F + 4) + rl * (12 * F + 4)
-            # the MFMA-bound kernel on the same mesh: fused edge MLP + hop 1, finest scale
-            tle, (_, ele) = time_kernel(pl, "edge_hop", 0, iters=20)
-            fle = ele * 2 * (2 * F * 2 * F + 2 * F * F)  # edge-MLP layers 2-3 (MFMA fp32)
-            roof["large_mesh"] = {
-                "workload": "hbm1m", "fine_nodes": dl["fine_nodes"], "rows": rl, "edges": el,
-                "algorithmic_bytes_per_launch": bl, "avg_launch_us": tl * 1e6,
-                "achieved": bl / tl / 1e9, "frac": bl / tl / 1e9 / HBM_PEAK_GBS,
-                "traffic": read_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_hop_large"),
-                "edge_mlp": {"kernel": "k_edge_hop<32> (edge MLP + hop 1), finest scale", "bound": "mfma",
-                             "edges": ele, "flops_per_launch": fle, "avg_launch_us": tle * 1e6,
-                             "achieved": fle / tle / 1e12, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                             "frac": fle / tle / 1e12 / FP32_MFMA_PEAK_TFS}}
-            del pl, ml, gl
-            torch.cuda.empty_cache()
+        try:  # optional: a failure here is recorded, never drops the result line
+            if world == 1 and not args.no_roofline_large and args.workload != "hbm1m":
+                gl, ml, _, dl = build_workload("hbm1m", seed=0, T=1)
+                gl = gl.to(dev)
+                ml = ml.to(dev)
+                ml.engine = "hip"
+                pl = plan_for(ml, gl)
+                pl.rollout(gl.x, gl.BC, gl.node_BC, gl.type_BC, 1)
+                tl, (rl, el) = time_kernel(pl, "hop", 0, iters=50)
+                bl = el * (4 * F + 4) + rl * (12 * F + 4)
+                # the MFMA-bound kernel on the same mesh: fused edge MLP + hop 1, finest scale
+                tle, (_, ele) = time_kernel(pl, "edge_hop", 0, iters=20)
+                fle = ele * 2 * (2 * F * 2 * F + 2 * F * F)  # edge-MLP layers 2-3 (MFMA fp32)
+                roof["large_mesh"] = {
+                    "workload": "hbm1m", "fine_nodes": dl["fine_nodes"], "rows": rl, "edges": el,
+                    "algorithmic_bytes_per_launch": bl, "avg_launch_us": tl * 1e6,
+                    "achieved": bl / tl / 1e9, "frac": bl / tl / 1e9 / HBM_PEAK_GBS,
+                    "traffic": read_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_hop_large"),
+                    "edge_mlp": {"kernel": "k_edge_hop<32> (edge MLP + hop 1), finest scale", "bound": "mfma",
+                                 "edges": ele, "flops_per_launch": fle, "avg_launch_us": tle * 1e6,
+                                 "achieved": fle / tle / 1e12, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                 "frac": fle / tle / 1e12 / FP32_MFMA_PEAK_TFS}}
+                del pl, ml, gl
+                torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001
+            roof["large_mesh"] = {"error": repr(e)}
         # ---------------- parity vs the reference fixture (zenodo4 only; CPU reference run)
         parity = {}
         r_gpu = plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
-        if args.workload == "zenodo4" and rank == 0 and T == 48 and B == 1:
-            fx = np.load(os.path.join(ROOT, "tests", "golden", "fx_zenodo4_K4_F32_rollout48.npz"))
-            ref = torch.from_numpy(fx["rollout_sel"])
-            sel = r_gpu[..., fx["steps"]]
-            parity["vs_reference_fixture"] = {
-                "steps": fx["steps"].tolist(), "max_abs_err": float((sel - ref).abs().max()),
-                "max_rel_err": float(max((sel[..., i] - ref[..., i]).abs().max() / ref[..., i].abs().max()
-                                         for i in range(ref.shape[-1])))}
-        # ---------------- CPU baseline (reference algorithm on the host cores)
+        try:  # optional: a failure here is recorded, never drops the result line
+            if args.workload == "zenodo4" and rank == 0 and T == 48 and B == 1:
+                fx = np.load(os.path.join(ROOT, "tests", "golden", "fx_zenodo4_K4_F32_rollout48.npz"))
+                ref = torch.from_numpy(fx["rollout_sel"])
+                sel = r_gpu[..., fx["steps"]]
+                parity["vs_reference_fixture"] = {
+                    "steps": fx["steps"].tolist(), "max_abs_err": float((sel - ref).abs().max()),
+                    "max_rel_err": float(max((sel[..., i] - ref[..., i]).abs().max() / ref[..., i].abs().max()
+                                             for i in range(ref.shape[-1])))}
+            # ---------------- CPU baseline (reference algorithm on the host cores)
+        except Exception as e:  # noqa: BLE001
+            parity["vs_reference_fixture"] = {"error": repr(e)}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import msgnn_torch as orc  # test/baseline infrastructure only
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            threads = min(threads, 16)
-            torch.set_num_threads(threads)
-            P = {k: v.detach().cpu() for k, v in model_cpu.state_dict().items()}
-            cfg = orc.msgnn_config(num_scales=desc["num_scales"], hid_features=F, K=desc["K"])
-            # bounded sample: one step first, then as many rollout steps of simulation 0 as
-            # fit ~cpu_seconds (whole rollouts repeated for small meshes, up to 4)
-            c0 = time.perf_counter()
-            orc.rollout(P, cfg, g_cpu, 1)
-            t1 = time.perf_counter() - c0
-            Tc = int(min(T, max(1, args.cpu_seconds / max(t1, 1e-6))))
-            reps, t_cpu, r_cpu = 0, 0.0, None
-            while reps < 4 and (reps == 0 or t_cpu < args.cpu_seconds):
+        try:  # optional: a failure here is recorded, never drops the result line
+            if world == 1 and not args.no_cpu_baseline:
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                import msgnn_torch as orc  # test/baseline infrastructure only
+                threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+                threads = min(threads, 16)
+                torch.set_num_threads(threads)
+                P = {k: v.detach().cpu() for k, v in model_cpu.state_dict().items()}
+                cfg = orc.msgnn_config(num_scales=desc["num_scales"], hid_features=F, K=desc["K"])
+                # bounded sample: one step first, then as many rollout steps of simulation 0 as
+                # fit ~cpu_seconds (whole rollouts repeated for small meshes, up to 4)
                 c0 = time.perf_counter()
-                r = orc.rollout(P, cfg, g_cpu, Tc)
-                t_cpu += time.perf_counter() - c0
-                reps += 1
-                r_cpu = r if r_cpu is None else r_cpu
-                if Tc < T:
-                    break
-            cpu = {"value": n0 * Tc * reps / t_cpu, "unit": "fine-node-steps/s", "cores": threads,
-                   "kind": "port",
-                   "sample": f"{reps} x {Tc}-step rollout of one simulation of the workload "
-                             f"(N0={n0}), reference algorithm in oracle/msgnn_torch.py (same ATen "
-                             f"CPU ops, bit-identical to the reference), torch {torch.__version__}, "
-                             f"{threads} threads, {t_cpu:.1f} s"}
-            r0 = r_gpu[:g_cpu.num_nodes, :, :Tc]  # simulation 0 = the batch's first graph
-            d = (r0 - r_cpu).abs()
-            parity["vs_cpu_reference"] = {
-                "steps": Tc, "max_abs_err": float(d.max()),
-                "max_rel_err": float(max(d[..., t].max() / max(r_cpu[..., t].abs().max(), 1e-30)
-                                         for t in range(Tc)))}
+                orc.rollout(P, cfg, g_cpu, 1)
+                t1 = time.perf_counter() - c0
+                Tc = int(min(T, max(1, args.cpu_seconds / max(t1, 1e-6))))
+                reps, t_cpu, r_cpu = 0, 0.0, None
+                while reps < 4 and (reps == 0 or t_cpu < args.cpu_seconds):
+                    c0 = time.perf_counter()
+                    r = orc.rollout(P, cfg, g_cpu, Tc)
+                    t_cpu += time.perf_counter() - c0
+                    reps += 1
+                    r_cpu = r if r_cpu is None else r_cpu
+                    if Tc < T:
+                        break
+                cpu = {"value": n0 * Tc * reps / t_cpu, "unit": "fine-node-steps/s", "cores": threads,
+                       "kind": "port",
+                       "sample": f"{reps} x {Tc}-step rollout of one simulation of the workload "
+                                 f"(N0={n0}), reference algorithm in oracle/msgnn_torch.py (same ATen "
+                                 f"CPU ops, bit-identical to the reference), torch {torch.__version__}, "
+                                 f"{threads} threads, {t_cpu:.1f} s"}
+                r0 = r_gpu[:g_cpu.num_nodes, :, :Tc]  # simulation 0 = the batch's first graph
+                d = (r0 - r_cpu).abs()
+                parity["vs_cpu_reference"] = {
+                    "steps": Tc, "max_abs_err": float(d.max()),
+                    "max_rel_err": float(max(d[..., t].max() / max(r_cpu[..., t].abs().max(), 1e-30)
+                                             for t in range(Tc)))}
+        except Exception as e:  # noqa: BLE001
+            cpu = {"error": repr(e)}
         result = {
             "metric": "mesh-nodes x rollout-steps / sec (fine-scale nodes); fp32 max-abs err vs CPU ref",
             "value": value, "unit": "fine-node-steps/s", "n_gpus": world, "steps": args.steps,
