@@ -371,8 +371,10 @@ struct msw_plan {
   // MSW_GRAPH_STEPS overrides (1: one graph launch per step).
   int graph_steps = 16;
   // Fused edge MLP + hop with two waves per tile (k_edge_coop) when 2 x tiles <= coop_waves
-  // (MSW_COOP_WAVES; 0: never).
+  // (MSW_COOP_WAVES; 0: never).  Per launch kind: coop_w[0] edge hop, [1] last hop,
+  // [2] pooling (MSW_COOP_WAVES_EH / _HOP / _POOL override the shared value).
   int coop_waves = 1024;
+  int coop_w[3] = {1024, 1024, 1024};
   std::vector<void*> owned;
   void drop_graphs() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
@@ -931,7 +933,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // (F = 32: two waves per tile; F = 64: four, one tile per workgroup)
       const int pw = P->NT == 2 ? 2 : P->NT == 4 ? 4 : 0;
       const int coop_fit = pw ? resident_of(P->NT, 7, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0) : 0;
-      a.coop = (pw && !loop && epi_ok && P->coop_waves > 0 && (long)pw * a.ntiles <= P->coop_waves &&
+      a.coop = (pw && !loop && epi_ok && P->coop_w[0] > 0 && (long)pw * a.ntiles <= P->coop_w[0] &&
                 (pw * a.ntiles + kWaves - 1) / kWaves <= coop_fit) ? pw : 0;
       break;
     }
@@ -947,7 +949,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         const bool loop = h.fit_blocks > 0 && h.max_blocks > 0 && (h.ntiles + kWaves - 1) / kWaves > h.fit_blocks;
         const int pw = P->NT >= 2 ? P->NT : 0;
         h.coop = 0;
-        if (h.last && pw && !loop && P->coop_waves > 0 && (long)pw * h.ntiles <= P->coop_waves &&
+        if (h.last && pw && !loop && P->coop_w[1] > 0 && (long)pw * h.ntiles <= P->coop_w[1] &&
             (pw * h.ntiles + kWaves - 1) / kWaves <= resident_of(P->NT, 9, h.c.prelu, 1, (size_t)h.reg.len * 4, 0))
           h.coop = pw;
       }
@@ -973,7 +975,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // two waves per edge tile (projection split) while that grid too is resident at once
       // (F = 32: two waves per tile, F = 64: four)
       const int pw = P->NT >= 2 ? P->NT : 0;
-      a.coop = (!a.rows && pw && P->coop_waves > 0 && (long)pw * a.etiles <= P->coop_waves &&
+      a.coop = (!a.rows && pw && P->coop_w[2] > 0 && (long)pw * a.etiles <= P->coop_w[2] &&
                 (pw * a.etiles + kWaves - 1) / kWaves <= fe) ? pw : 0;
       break;
     }
@@ -1439,6 +1441,13 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
   if (const char* es = getenv("MSW_EPI_SPLIT_TILES")) P->epi_split_tiles = atoi(es);
   if (const char* gs = getenv("MSW_GRAPH_STEPS")) P->graph_steps = std::max(1, atoi(gs));
   if (const char* cw = getenv("MSW_COOP_WAVES")) P->coop_waves = std::max(0, atoi(cw));
+  {
+    const char* kinds[3] = {"MSW_COOP_WAVES_EH", "MSW_COOP_WAVES_HOP", "MSW_COOP_WAVES_POOL"};
+    for (int k = 0; k < 3; ++k) {
+      const char* v = getenv(kinds[k]);
+      P->coop_w[k] = v ? std::max(0, atoi(v)) : P->coop_waves;
+    }
+  }
   if (const char* cm = getenv("MSW_HOP_CHAINS")) {  // a chain's halo is m-1 rings deep: not on parts
     P->chain_max = std::max(2, std::min(kChainMax, atoi(cm)));
     P->hop_pairs = xch ? 0 : 1;
