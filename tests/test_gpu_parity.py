@@ -311,6 +311,20 @@ def test_edge_cases(cuda):
     assert per_step_rel(m.rollout(g2).cpu(), ref) <= REL_TOL
 
 
+def test_water_depth_boundary_condition(cuda):
+    """type_BC = 1: the BC series drives the ghost cell's water-depth columns instead of the
+    discharge ones (apply_boundary_condition, utils/dataset.py:486-497), vs the oracle."""
+    g = make_multiscale_mesh(**mesh_config("tiny"), T=6)
+    g.type_BC = torch.tensor(1, dtype=torch.int)
+    g.BC = g.BC * 0.25  # a depth series of plausible size
+    cfg = manifest()["weights_K4_F32_cfg"]
+    ref = orc.rollout(weights("K4_F32"), cfg, g)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    r = m.rollout(g.to(cuda)).cpu()
+    assert per_step_rel(r, ref) <= REL_TOL
+    assert ref.abs().max() > 0  # the depth BC wets the mesh: a non-trivial comparison
+
+
 def test_rollout_metrics_kernel_vs_reference(cuda):
     """the on-device metrics kernel against the reference's own evaluation
     functions (fx_metrics.npz): losses within fp32 rounding of the reference's fp32
