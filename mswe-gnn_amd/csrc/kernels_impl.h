@@ -243,6 +243,7 @@ struct EpiPre {
   f32x4 xs[NT];
   float xd[kMaxDyn];  // X[row, nstat : nnf] (lane group 0 uses it)
   int ext, step;
+  int bc;             // the row's BC slot (rollout mode), -1 = none
 };
 template <int NT>
 __device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, const Common& c,
@@ -252,6 +253,7 @@ __device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, c
   if (e.dec.on) {
     p.ext = c.perm ? c.perm[n] : (int)n;
     p.step = e.dec.io ? e.dec.io->step : 0;
+    p.bc = e.dec.bc_slot ? e.dec.bc_slot[n] : -1;  // here, not after the decoder chain
     const size_t row = e.dec.x_internal ? n : (size_t)(p.ext > 0 ? p.ext : 0);
     const float* xr = e.dec.X + row * c.nnf + (c.nnf - c.dyn);
 #pragma unroll
@@ -318,7 +320,7 @@ __device__ __forceinline__ void decode_tail(const f32x4 (&o)[1], const DecDesc& 
     if (k + 2 < c.dyn) xw[k] = pre.xd[k + 2];
   xw[c.dyn - 2] = hm;
   xw[c.dyn - 1] = vm;
-  const int b = d.bc_slot ? d.bc_slot[n] : -1;
+  const int b = pre.bc;
   if (b >= 0 && t + 1 < io->bc_tstride) {
     for (int tau = 0; tau < c.p; ++tau)
       xw[(io->type_bc - 1) + 2 * tau] = io->bc[((size_t)b * c.p + tau) * io->bc_tstride + t + 1];

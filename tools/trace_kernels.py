@@ -64,6 +64,21 @@ def main():
         for k, cyc, ns in marks[1:]:
             print(f"    {PHASES[k]:16s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
             prev = ns
+    # the finest scale's last hop + decoder epilogue: the last launch of a rollout step, so a
+    # one-step rollout leaves its marks in the buffer (marks it does not set are skipped)
+    buf.zero_()
+    plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, 1)
+    torch.cuda.synchronize()
+    t = buf.cpu().tolist()
+    clk0, rt0 = t[0], t[1]
+    marks = sorted([(k, t[2 * k] - clk0, (t[2 * k + 1] - rt0) * 10.0) for k in (0, 1, 2, 4, 6, 7, 8, 9)
+                    if t[2 * k] != 0], key=lambda mk: mk[2])  # time order (the staging wait is late)
+    if len(marks) >= 2:
+        print(f"last hop + decoder, scale 0 (last launch of a rollout step): {marks[-1][2] / 1e3:6.2f} us on wave 0")
+        prev = 0.0
+        for k, cyc, ns in marks[1:]:
+            print(f"    {PHASES[k]:16s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
+            prev = ns
     L.check(L.lib().msw_set_trace(plan._h, None))
 
 
