@@ -354,3 +354,42 @@ def test_partition_halo_exchange_two_ranks_gloo():
         p.join(60)
         assert p.exitcode == 0
     assert err <= 1e-12, err
+
+
+def test_pmc_summary_attribution(tmp_path):
+    """tools/pmc_summary.py (the `traffic` figures bench.py reports): gfx950 FETCH_SIZE
+    correction (x2), per-launch averages, and the selection of the roofline kernels -- the
+    middle hop moving the most bytes, and only the finest-scale dispatches of the grid-stride
+    edge MLP (its launches of every scale share one grid)."""
+    import csv
+    import json
+    import subprocess
+    cols = ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Counter_Name", "Counter_Value"]
+
+    def write(d, counter, rows):
+        d.mkdir()
+        with open(d / "run_counter_collection.csv", "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=cols)
+            w.writeheader()
+            for i, (name, grid, val) in enumerate(rows):
+                w.writerow(dict(Dispatch_Id=i, Kernel_Name=name, Grid_Size=grid, Counter_Name=counter,
+                                Counter_Value=val))
+    eh = "void msw::k_edge_hop<2, 1, true, 0>(msw::EdgeHopArgs)"
+    mid = "void msw::k_hop<2, 1, false, true>(msw::HopArgs)"
+    small = "void msw::k_hop<2, 1, false, false>(msw::HopArgs)"
+    fetch = [(eh, 262144, 1000.0), (eh, 262144, 250.0), (eh, 262144, 1000.0), (mid, 262144, 400.0),
+             (small, 2048, 10.0), (small, 2048, 10.0), (small, 2048, 10.0)]
+    write_rows = [(n, g, v / 2) for n, g, v in fetch]
+    write(tmp_path / "f", "FETCH_SIZE", fetch)
+    write(tmp_path / "w", "WRITE_SIZE", write_rows)
+    out = tmp_path / "s.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(out),
+                    str(tmp_path / "f"), str(tmp_path / "w")], check=True, capture_output=True)
+    s = json.load(open(out))
+    big = s["k_edge_hop_large"]
+    assert big["dispatches"] == 2  # the 250-KB (coarser-scale) launch is left out
+    assert big["read_bytes_per_launch"] == 2 * 1024 * 1000.0
+    assert big["write_bytes_per_launch"] == 1024 * 500.0
+    assert s["k_hop_large"]["kernel"].startswith("k_hop<2, 1, false, true>")
+    assert s["k_hop"]["kernel"].startswith("k_hop<2, 1, false, false>")  # most dispatches
+    assert s["k_hop"]["hbm_bytes_per_launch"] == 2 * 1024 * 10.0 + 1024 * 5.0
