@@ -41,29 +41,43 @@ def load_weights(name):
     return {k: torch.from_numpy(z[k]) for k in z.files}
 
 
+WORKLOADS = {
+    # config 2: Zenodo-like mesh, 4 scales, shipped K4_F32 checkpoint
+    "zenodo4": dict(mesh="zenodo4", S=4, F=32, K=4, weights="K4_F32"),
+    # config 2, "3-scale" wording: same N0, 3 scales, seeded init (no 3-scale checkpoint)
+    "zenodo3": dict(mesh="zenodo3", S=3, F=32, K=4, weights=None),
+    # config 2 with the other shipped 4-scale checkpoint (hid_features 16, K 2)
+    "zenodo4_k2f16": dict(mesh="zenodo4", S=4, F=16, K=2, weights="K2_F16"),
+    # config 2 at the reference's default config.yaml width (hid_features 64, K 4; no
+    # F = 64 checkpoint is shipped -> seeded init)
+    "zenodo4_f64": dict(mesh="zenodo4", S=4, F=64, K=4, weights=None),
+    # config 3: Zenodo-like test meshes of 8,193-12,801 fine nodes (member i: size cycled,
+    # seed i; mswegnn.mesh.config3_members), 3 scales seeded init / 4 scales K4_F32
+    "config3": dict(mesh="config3", S=3, F=32, K=4, weights=None),
+    "config3_k4": dict(mesh="config3", S=4, F=32, K=4, weights="K4_F32"),
+    # config 4: dk15-like mesh (fine-tune checkpoint not shipped -> K4_F32 weights)
+    "dk15": dict(mesh="dk15", S=4, F=32, K=4, weights="K4_F32"),
+    # config 5: ~1M fine nodes, 3 scales, fully wet (every edge active)
+    "hbm1m": dict(mesh="hbm1m", S=3, F=32, K=4, weights=None),
+    # plumbing size for the CPU (gloo) tests of the multi-rank path
+    "tiny": dict(mesh="tiny", S=4, F=32, K=4, weights="K4_F32"),
+    # two sizes alternating by seed (CPU gloo test of the all-gather's padding path)
+    "tiny_mixed": dict(mesh="tiny_mixed", S=4, F=32, K=4, weights="K4_F32"),
+}
+
+
 def build_workload(name, seed, T):
-    """-> (graph, model, cfg-dict for the oracle, description)."""
+    """Simulation `seed` of a workload -> (graph, model, workload row, description)."""
     from models.gnn import MSGNN
-    from mswegnn.mesh import make_multiscale_mesh, mesh_config
-    table = {
-        # config 2 (SURVEY §8(d)): Zenodo-like mesh, 4 scales, shipped K4_F32 checkpoint
-        "zenodo4": dict(mesh="zenodo4", S=4, F=32, K=4, weights="K4_F32"),
-        # config 2, "3-scale" wording: same N0, 3 scales, seeded init (no 3-scale checkpoint)
-        "zenodo3": dict(mesh="zenodo3", S=3, F=32, K=4, weights=None),
-        # config 2 with the other shipped 4-scale checkpoint (hid_features 16, K 2)
-        "zenodo4_k2f16": dict(mesh="zenodo4", S=4, F=16, K=2, weights="K2_F16"),
-        # config 2 at the reference's default config.yaml width (hid_features 64, K 4; no
-        # F = 64 checkpoint is shipped -> seeded init)
-        "zenodo4_f64": dict(mesh="zenodo4", S=4, F=64, K=4, weights=None),
-        # config 4: dk15-like mesh (fine-tune checkpoint not shipped -> K4_F32 weights)
-        "dk15": dict(mesh="dk15", S=4, F=32, K=4, weights="K4_F32"),
-        # config 5: ~1M fine nodes, 3 scales, fully wet (every edge active)
-        "hbm1m": dict(mesh="hbm1m", S=3, F=32, K=4, weights=None),
-        # plumbing size for the CPU (gloo) tests of the multi-rank path
-        "tiny": dict(mesh="tiny", S=4, F=32, K=4, weights="K4_F32"),
-    }
-    w = table[name]
-    g = make_multiscale_mesh(**mesh_config(w["mesh"]), seed=seed, T=T)
+    from mswegnn.mesh import make_multiscale_mesh, mesh_config, config3_members
+    w = WORKLOADS[name]
+    if w["mesh"] == "config3":
+        kw = config3_members(w["S"], count=seed + 1)[seed]
+    elif w["mesh"] == "tiny_mixed":
+        kw = dict(n_coarse=2 + seed % 2, num_scales=4, seed=seed)
+    else:
+        kw = dict(mesh_config(w["mesh"]), seed=seed)
+    g = make_multiscale_mesh(**kw, T=T)
     if name == "hbm1m":
         from mswegnn.mesh import wet_state
         g = wet_state(g, seed=seed, all_wet=True)
@@ -129,12 +143,48 @@ def read_traffic(path, kernel_prefix):
         return None
 
 
+def simulations_of_rank(args, rank, world):
+    """Simulation ids this rank runs.  --global-batch G: a FIXED set of G simulations split
+    round-robin over the ranks, {i : i mod W = r} (strong scaling).  Otherwise
+    --batch B per rank, ids r*B .. r*B+B-1 (weak scaling)."""
+    if args.global_batch:
+        if args.global_batch < world:
+            raise SystemExit(f"--global-batch {args.global_batch} < {world} ranks")
+        return [i for i in range(args.global_batch) if i % world == rank], "strong"
+    B = max(1, args.batch)
+    return [rank * B + i for i in range(B)], "weak"
+
+
+def rank_batch(workload, ids, T):
+    """This rank's simulations as ONE graph: the single simulation, or a disjoint-union batch
+    in the reference's layout (PyG collation + adapt_batch_training / update_batch_multiscale,
+    train.py:14-65).  -> (sims, graph, fine_rows or None, fine nodes per rollout)."""
+    sims = [build_workload(workload, seed=i, T=T) for i in ids]
+    fine = sum(s[3]["fine_nodes"] for s in sims)
+    if len(sims) == 1:
+        return sims, sims[0][0], None, fine
+    from mswegnn.batch import collate
+    from mswegnn.rollout import adapt_batch_training
+    gb = adapt_batch_training(collate([s[0] for s in sims]))
+    npt = gb.node_ptr
+    rows = torch.cat([torch.arange(int(npt[i, 0]), int(npt[i, 1])) for i in range(len(sims))])
+    return sims, gb, rows, fine
+
+
+def _built_from_sources():
+    try:
+        import build_engine
+        return build_engine.library_matches_sources()
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="zenodo4")
+    ap.add_argument("--workload", default="zenodo4", choices=sorted(WORKLOADS))
     ap.add_argument("--T", type=int, default=48)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -142,6 +192,12 @@ def main():
                     help="skip the hop-kernel roofline on the ~1M-node mesh (config 5)")
     ap.add_argument("--batch", type=int, default=1,
                     help="simulations per GPU, run as one disjoint-union batch (SURVEY §8 f1)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="a fixed set of G simulations split round-robin over the ranks "
+                         "(strong scaling; each rank runs its share as one batch)")
+    ap.add_argument("--caller", default="fused", choices=["fused", "reference-loop"],
+                    help="fused: rollout_test as ONE msw_rollout; reference-loop: the reference's "
+                         "own rollout_test loop (train.py:87-95), one HIP msw_forward per step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,34 +212,50 @@ def main():
     torch.cuda.set_device(dev)
 
     T = args.T
-    B = max(1, args.batch)
-    # rank r simulates seeds r*B .. r*B+B-1 (independent simulations, weak scaling)
-    sims = [build_workload(args.workload, seed=rank * B + i, T=T) for i in range(B)]
+    ids, scaling = simulations_of_rank(args, rank, world)
+    B = len(ids)
+    sims, gb, fine_rows, fine_rank = rank_batch(args.workload, ids, T)
     g_cpu, model_cpu, w, desc = sims[0]
-    n0 = desc["fine_nodes"]
-    if B == 1:
-        gb = g_cpu
-        fine_rows = None
-    else:  # the reference's batch layout (update_batch_multiscale, train.py:31-65)
-        from mswegnn.batch import collate
-        from training.train import adapt_batch_training
-        gb = adapt_batch_training(collate([s[0] for s in sims]))
-        npt = gb.node_ptr
-        fine_rows = torch.cat([torch.arange(int(npt[i, 0]), int(npt[i, 1])) for i in range(B)]).to(dev)
-        desc = dict(desc, batch=B, batch_nodes=int(gb.x.shape[0]))
+    n0_list = [s[3]["fine_nodes"] for s in sims]
+    n0 = n0_list[0]
+    if B > 1:
+        desc = dict(desc, batch=B, batch_nodes=int(gb.x.shape[0]), batch_fine_nodes=fine_rank,
+                    member_fine_nodes=n0_list)
+        fine_rows = fine_rows.to(dev)
     g = gb.to(dev)
     model = model_cpu.to(dev)
     model.engine = "hip"
 
     from mswegnn.engine import plan_for
+    from mswegnn import _lib
     plan = plan_for(model, g)
     out = torch.empty(g.num_nodes, 2, T, device=dev)
-    gather = make_gatherer(dist, world, n0 * B, T, dev)
+    gather = make_gatherer(dist, world, fine_rank, T, dev)
+
+    if args.caller == "fused":
+        def rollout():
+            plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T, out=out)
+            return out
+    else:
+        from mswegnn.rollout import apply_boundary_condition, use_prediction
+        dyn = model.previous_t * model.NUM_WATER_VARS
+
+        def rollout():  # training/train.py:87-95 verbatim semantics, model(temp) -> msw_forward
+            temp = g.clone()
+            preds = []
+            with torch.no_grad():
+                for t in range(T):
+                    temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, t],
+                                                                temp.node_BC, type_BC=temp.type_BC)
+                    pred = model(temp)
+                    temp.x = use_prediction(temp.x, pred, model.previous_t)
+                    preds.append(pred)
+            return torch.stack(preds, -1)
 
     def one_step():
-        plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T, out=out)
+        r = rollout()
         if world > 1:
-            gather(out[:n0] if fine_rows is None else out.index_select(0, fine_rows))
+            gather(r[:n0] if fine_rows is None else r.index_select(0, fine_rows))
 
     for _ in range(args.warmup):
         one_step()
@@ -202,9 +274,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / max(args.steps, 1) * 1e3
-    nodes_all = B * n0  # fine nodes simulated per step, summed over ranks (meshes may differ)
+    nodes_all = fine_rank  # fine nodes simulated per step, summed over ranks (meshes may differ)
     if world > 1:
-        tn = torch.tensor([B * n0], device=dev, dtype=torch.float64)
+        tn = torch.tensor([fine_rank], device=dev, dtype=torch.float64)
         dist.all_reduce(tn, op=dist.ReduceOp.SUM)
         nodes_all = float(tn.item())
     value = nodes_all * T * args.steps / dt
@@ -355,11 +427,15 @@ def main():
             "metric": "mesh-nodes x rollout-steps / sec (fine-scale nodes); fp32 max-abs err vs CPU ref",
             "value": value, "unit": "fine-node-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (own multi-scale triangular mesh generator; dry start + hydrograph BC)",
-            "config": dict(desc, parallelism=f"sim-sharded x{world} ({B} sim/GPU, RCCL all-gather at end)"
+            "config": dict(desc, caller=args.caller, global_batch=args.global_batch or None,
+                           parallelism=f"sim-sharded x{world} ({B} sim on rank 0, RCCL all-gather at end)"
                            if world > 1 else ("single GPU" if B == 1 else f"single GPU, batch of {B} sims")),
-            "all_node_steps_per_s": value * desc["all_nodes"] / n0,
+            "timed_region": "whole rollouts (T steps each) incl. the per-rollout edge encoder + edge "
+                            "terms of every processor (msw_rollout prologue); inputs resident in HBM",
+            "library": dict(_lib.lib_info(), built_from_current_sources=_built_from_sources()),
+            "all_node_steps_per_s": value * desc.get("batch_nodes", desc["all_nodes"]) / fine_rank,
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "engine": {"kernels_per_step": st["kernels_per_step"], "graph_captured": st["graph_captured"],
                        "device_bytes": st["device_bytes"]},

@@ -3,8 +3,13 @@
     python mswe-gnn_amd/build_engine.py [--force]
 
 Objects go to mswe-gnn_amd/_obj/, the library to mswe-gnn_amd/lib/libmswegnn.so.
-Rebuilds an object only when its source or a header is newer.
+Rebuilds an object when its source or a header is newer, and everything when the sha256 of
+the sources + flags differs from the one recorded beside the library at its last build
+(lib/libmswegnn.so.srchash): a library copied in with fresh mtimes but built from other
+sources is rebuilt.  ``source_hash()`` / ``library_matches_sources()`` let the bench record
+which build it measured.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -20,6 +25,31 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
          "-I", os.path.join(ROOT, "include")]
 
 
+def source_hash(variant=""):
+    """sha256 over the engine sources, headers, compiler flags and variant."""
+    h = hashlib.sha256()
+    for f in SRC + HDR:
+        path = f if os.path.isabs(f) else os.path.join(HERE, f)
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS + [variant]).encode())
+    return h.hexdigest()
+
+
+def lib_path(variant=""):
+    return os.path.join(HERE, "lib", f"libmswegnn_{variant}.so" if variant else "libmswegnn.so")
+
+
+def library_matches_sources(variant=""):
+    """True when the library's recorded source hash equals the current sources' hash."""
+    try:
+        with open(lib_path(variant) + ".srchash") as f:
+            return f.read().strip() == source_hash(variant)
+    except OSError:
+        return False
+
+
 def _newer(a, b):
     return not os.path.exists(b) or os.path.getmtime(a) > os.path.getmtime(b)
 
@@ -32,6 +62,9 @@ def build(force=False, verbose=True, variant=""):
              "e0w12": ["-DMSW_EDGE_WAVES0=12"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
+    out = lib_path(variant)
+    if os.path.exists(out) and not library_matches_sources(variant):
+        force = True  # built from other sources (or unrecorded): rebuild everything
     objs, cmds = [], []
     hdr_t = max(os.path.getmtime(h if os.path.isabs(h) else os.path.join(HERE, h)) for h in HDR)
     for s in SRC:
@@ -49,12 +82,13 @@ def build(force=False, verbose=True, variant=""):
         for r in list(ex.map(lambda c: subprocess.run(c, check=False), cmds)):
             if r.returncode != 0:
                 raise subprocess.CalledProcessError(r.returncode, r.args)
-    out = os.path.join(HERE, "lib", f"libmswegnn_{variant}.so" if variant else "libmswegnn.so")
     if force or any(_newer(o, out) for o in objs):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+    with open(out + ".srchash", "w") as f:
+        f.write(source_hash(variant) + "\n")
     return out
 
 

@@ -129,11 +129,11 @@ int upload(T** p, const std::vector<T>& v, int64_t& counter) {
   return MSW_OK;
 }
 
-hipError_t rowmlp_dispatch(int NT, const RowMlpArgs& ra) {
+hipError_t rowmlp_dispatch(int NT, const RowMlpArgs& ra, hipStream_t st = nullptr) {
   switch (NT) {
-    case 1: return launch_rowmlp<1>(ra, nullptr);
-    case 2: return launch_rowmlp<2>(ra, nullptr);
-    default: return launch_rowmlp<4>(ra, nullptr);
+    case 1: return launch_rowmlp<1>(ra, st);
+    case 2: return launch_rowmlp<2>(ra, st);
+    default: return launch_rowmlp<4>(ra, st);
   }
 }
 
@@ -326,6 +326,10 @@ struct msw_plan {
   float* zrow_d = nullptr;
   std::vector<int> bc_rows_set;
   RolloutIO* io_d = nullptr;
+  // Edge terms of the processors' first edge-MLP layer (edge encoder, gnn.py:281-282, then
+  // Pe = W1[:, 4F:] . enc + b1 per processor): static for a graph, computed at plan creation
+  // for msw_forward and recomputed at the start of every msw_rollout (edge_jobs, in order).
+  std::vector<RowMlpArgs> edge_jobs;
   // O / U / V of consecutive SWEGNN layers alternate between two sets (Proc::par): the
   // last hop of layer j reads O[j&1] (K = 1: also U/V[j&1]) while its epilogue writes the
   // projection of layer j+1.  T[0] / T[1] carry the intermediate hops.
@@ -1569,17 +1573,16 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
             ea[(size_t)(sbase[s] + q) * ef_raw + f] = g->edge_attr[(size_t)P->sc[s].porig[q] * ef_raw + f];
     float* ea_d = nullptr;
     float* enc_d = nullptr;
-    int64_t tmp_bytes = 0;
-    if ((rc = upload(&ea_d, ea, tmp_bytes))) return rc;
+    if ((rc = pupload(P.get(), &ea_d, ea))) return rc;
     const float* feat = ea_d;
     int feat_stride = ef_raw, feat_dim = ef_raw;
     if (m->edge_mlp) {
-      if ((rc = dalloc(&enc_d, (size_t)E * F, tmp_bytes))) return rc;
+      if ((rc = palloc(P.get(), &enc_d, (size_t)E * F))) return rc;
       RowMlpArgs ra{};
       ra.mode = 0;
       ra.in = ea_d; ra.in_stride = ef_raw; ra.in_dim = ef_raw; ra.R = (int)E; ra.m = P->edge_enc;
       ra.W = P->dW; ra.out = enc_d; ra.out_stride = F; ra.out_tiles = P->NT;
-      HIP_TRY(rowmlp_dispatch(P->NT, ra));
+      P->edge_jobs.push_back(ra);
       feat = enc_d; feat_stride = F; feat_dim = F;
     }
     for (size_t j = 0; j < P->procs.size(); ++j) {
@@ -1597,20 +1600,16 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
       md.l[0].b_off = pack_bias(tb, L1.bias, H1, 2 * P->NT);
       md.l[0].act = 0;
       float* tw = nullptr;
-      if ((rc = upload(&tw, tb.h, tmp_bytes))) return rc;
+      if ((rc = pupload(P.get(), &tw, tb.h))) return rc;
       const ScaleCSR& c = P->sc[pr.scale];
       RowMlpArgs ra{};
       ra.mode = 1;
       ra.in = feat + (size_t)sbase[pr.scale] * feat_stride; ra.in_stride = feat_stride;
       ra.in_dim = feat_dim; ra.R = c.ntiles * kRowsPerWave; ra.m = md; ra.W = tw;
       ra.out = pr.Pe; ra.out_stride = 16 * pr.h1t; ra.out_tiles = pr.h1t;
-      HIP_TRY(rowmlp_dispatch(P->NT, ra));
-      HIP_TRY(hipDeviceSynchronize());
-      HIP_TRY(hipFree(tw));
+      P->edge_jobs.push_back(ra);
     }
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipFree(ea_d));
-    if (enc_d) HIP_TRY(hipFree(enc_d));
+    for (const RowMlpArgs& ra : P->edge_jobs) HIP_TRY(rowmlp_dispatch(P->NT, ra));
   }
   HIP_TRY(hipDeviceSynchronize());
   if (xch) P->use_graph = getenv("MSW_PART_GRAPH") ? 1 : 0;  // exchanges run eagerly by default
@@ -1650,6 +1649,7 @@ int rollout_prologue(msw_plan* P, const float* x0, const float* bc, int32_t bc_t
     }
     P->bc_rows_set = rows;
   }
+  for (const RowMlpArgs& ra : P->edge_jobs) HIP_TRY(rowmlp_dispatch(P->NT, ra, st));
   RolloutIO io{};
   io.bc = bc; io.out = out; io.bc_tstride = bc_tstride; io.type_bc = type_bc; io.T = T; io.step = -1;
   HIP_TRY(launch_set_io(P->io_d, io, st));

@@ -15,7 +15,10 @@ Execution paths of ``forward(graph)``:
   mathematics as composite torch ops, so the module stays trainable.  It is not the
   measured hot path.
 
-``engine`` ('auto' | 'hip' | 'torch') on a model instance forces a path.
+``engine`` ('auto' | 'hip' | 'torch') on a model instance forces a path.  In 'auto' a
+configuration the engine does not implement (e.g. learned_pooling=True, hid_features other
+than 16/32/64, layer_norm MLPs, a node with more than 16 in-edges) and a training-mode model
+with dropout take the torch path; 'hip' raises for them instead.
 
 Reference: GNN models/gnn.py:13-152, MSGNN :154-350, SWEGNN :352-450.
 """
@@ -26,10 +29,13 @@ import torch.nn as nn
 from torch import Tensor
 
 from models.models import BaseFloodModel, make_mlp, activation_functions
-from utils.dataset import create_scale_mask
+from mswegnn.rollout import create_scale_mask
+from mswegnn import hooks as _hooks
 
 
 def _engine_wanted(model, x: Tensor) -> bool:
+    if _hooks.PENDING:  # MSWEGNN_FUSED_ROLLOUT: a patch deferred by a half-imported module
+        _hooks.maybe_patch()
     mode = getattr(model, "engine", "auto")
     if mode == "torch":
         return False
@@ -37,9 +43,12 @@ def _engine_wanted(model, x: Tensor) -> bool:
         if not x.is_cuda:
             raise RuntimeError("engine='hip' needs the graph on a GPU")
         return True
-    needs_grad = torch.is_grad_enabled() and (
-        x.requires_grad or any(p.requires_grad for p in model.parameters()))
-    return x.is_cuda and not needs_grad
+    if not x.is_cuda:
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in model.parameters())):
+        return False
+    # the engine implements inference: no dropout
+    return not (model.training and any(isinstance(m, nn.Dropout) and m.p > 0 for m in model.modules()))
 
 
 class SWEGNN(nn.Module):
@@ -121,8 +130,10 @@ class _EngineMixin:
     engine = "auto"
 
     def _engine_for(self, graph):
+        """The cached plan for this graph, or None when engine='auto' and the engine does
+        not implement this model / graph (the caller then takes the torch path)."""
         from mswegnn.engine import plan_for
-        return plan_for(self, graph)
+        return plan_for(self, graph, unsupported_ok=getattr(self, "engine", "auto") == "auto")
 
     def rollout(self, graph, steps: Optional[int] = None):
         """Autoregressive rollout (rollout_test semantics, training/train.py:67-95) -> [N, 2, T].
@@ -131,11 +142,10 @@ class _EngineMixin:
         captured hipGraph.  CPU graph or engine='torch': the step-by-step torch path."""
         T = graph.y.shape[-1] if steps is None else steps
         with torch.no_grad():
-            if _engine_wanted(self, graph.x):
-                from mswegnn.engine import plan_for
-                return plan_for(self, graph).rollout(graph.x, graph.BC, graph.node_BC,
-                                                     graph.type_BC, T)
-            from utils.dataset import apply_boundary_condition, use_prediction
+            plan = self._engine_for(graph) if _engine_wanted(self, graph.x) else None
+            if plan is not None:
+                return plan.rollout(graph.x, graph.BC, graph.node_BC, graph.type_BC, T)
+            from mswegnn.rollout import apply_boundary_condition, use_prediction
             dyn = self.previous_t * self.NUM_WATER_VARS
             temp = graph.clone()
             preds = []
@@ -199,8 +209,9 @@ class GNN(_EngineMixin, BaseFloodModel):
         return x_s, x_d
 
     def forward(self, graph):
-        if _engine_wanted(self, graph.x):
-            return self._engine_for(graph).forward(graph.x)
+        plan = self._engine_for(graph) if _engine_wanted(self, graph.x) else None
+        if plan is not None:
+            return plan.forward(graph.x)
         x = graph.x.clone()
         edge_attr = self.edge_encoder(graph.edge_attr) if self.edge_mlp else graph.edge_attr
         x_s, x_d = self._split_inputs(x)
@@ -286,8 +297,9 @@ class MSGNN(_EngineMixin, BaseFloodModel):
         return out
 
     def forward(self, graph):
-        if _engine_wanted(self, graph.x):
-            return self._engine_for(graph).forward(graph.x)
+        plan = self._engine_for(graph) if _engine_wanted(self, graph.x) else None
+        if plan is not None:
+            return plan.forward(graph.x)
         S = self.num_scales
         x = graph.x.clone()
         ei, ep = graph.edge_index, graph.edge_ptr

@@ -133,8 +133,29 @@ def lib():
     return _lib
 
 
+def lib_info():
+    """Path, size, mtime and sha256 of the library this process loads (bench provenance)."""
+    import hashlib
+    with open(LIB_PATH, "rb") as f:
+        data = f.read()
+    st = os.stat(LIB_PATH)
+    return {"path": os.path.relpath(LIB_PATH, os.path.dirname(os.path.dirname(_HERE))),
+            "bytes": st.st_size, "mtime": st.st_mtime, "sha256": hashlib.sha256(data).hexdigest()}
+
+
+MSW_ERR_UNSUPPORTED = -3
+
+
+class EngineError(RuntimeError):
+    """A negative MSW_ERR_* return code; ``code`` holds it."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"mswegnn error {code}: {msg}")
+        self.code = code
+
+
 def check(rc):
     if rc != MSW_OK:
         msg = lib().msw_last_error().decode(errors="replace")
-        raise RuntimeError(f"mswegnn error {rc}: {msg}")
+        raise EngineError(rc, msg)
     return rc

@@ -182,6 +182,7 @@ class EnginePlan:
             raise RuntimeError("the HIP engine needs a GPU device")
         self.num_nodes = int(graph.x.shape[0])
         self.nnf = int(graph.x.shape[1])
+        self.previous_t = int(model.previous_t)
         md, k1 = describe_model(model)
         gd, k2 = describe_graph(model, graph)
         h = C.c_void_p()
@@ -234,9 +235,21 @@ class EnginePlan:
         bc = None
         tstride = 0
         if nbc.size:
-            bc = BC.to(self.device, torch.float32).contiguous()
+            if nbc.min() < 0 or nbc.max() >= self.num_nodes:
+                raise ValueError("node_BC holds a node index outside the graph")
+            bc = BC.to(self.device, torch.float32)
             if bc.dim() != 3 or bc.shape[0] != nbc.size:
                 raise ValueError("BC must be [n_BC, previous_t, T+1]")
+            if bc.shape[1] == 1 and self.previous_t > 1:
+                # x_d[node_BC, (type_BC-1)::2] = BC broadcasts a single column over the
+                # previous_t slots (utils/dataset.py:496); the kernels read [n_BC, p, T+1]
+                bc = bc.expand(-1, self.previous_t, -1)
+            if bc.shape[1] != self.previous_t:
+                raise ValueError(f"BC has {bc.shape[1]} time columns, the model expects previous_t="
+                                 f"{self.previous_t} (or 1, broadcast)")
+            if bc.shape[2] < T:
+                raise ValueError(f"BC holds {bc.shape[2]} time steps, the rollout needs {T}")
+            bc = bc.contiguous()
             tstride = int(bc.shape[-1])
         tb = int(torch.as_tensor(type_BC).reshape(-1)[0])
         L.check(L.lib().msw_rollout(self._h, C.c_void_p(x0.data_ptr()),
@@ -271,17 +284,26 @@ class EnginePlan:
 
 
 # ------------------------------------------------------------------ cache
-def _graph_key(model, graph):
-    names = ["x", "edge_index", "edge_attr"]
-    if model.type_model == "MSGNN":
-        names += ["node_ptr", "edge_ptr", "intra_mesh_edge_index", "intra_edge_ptr"]
-    key = []
-    for n in names:
-        t = getattr(graph, n)
-        key.append((n, t.data_ptr() if n != "x" else 0, tuple(t.shape), t.device.type,
-                    t._version if n != "x" else 0))
-    key.append(("dev", str(graph.x.device)))
-    return tuple(key)
+_TOPOLOGY = {"GNN": ("edge_index", "edge_attr"),
+             "MSGNN": ("edge_index", "edge_attr", "node_ptr", "edge_ptr", "intra_mesh_edge_index",
+                       "intra_edge_ptr")}
+
+
+class _GraphRef:
+    """The tensors a plan was built from, held by STRONG reference and compared by identity
+    plus in-place version: a freed tensor's address can be reused by a new same-shaped
+    tensor (caching allocator), so addresses alone cannot tell two graphs apart."""
+
+    def __init__(self, model, graph):
+        self.tensors = tuple(getattr(graph, n) for n in _TOPOLOGY[model.type_model])
+        self.versions = tuple(t._version for t in self.tensors)
+        self.shape = (tuple(graph.x.shape), str(graph.x.device))
+
+    def matches(self, model, graph):
+        ts = tuple(getattr(graph, n) for n in _TOPOLOGY[model.type_model])
+        return (self.shape == (tuple(graph.x.shape), str(graph.x.device))
+                and all(a is b for a, b in zip(ts, self.tensors))
+                and self.versions == tuple(t._version for t in ts))
 
 
 def _weights_key(model):
@@ -289,20 +311,37 @@ def _weights_key(model):
 
 
 _plans = weakref.WeakKeyDictionary()
+CACHE_PLANS = 4  # plans kept per model (most recently used first)
 
 
-def plan_for(model, graph):
-    """Cached EnginePlan for (model weights, graph topology)."""
-    per_model = _plans.setdefault(model, {})
-    gk, wk = _graph_key(model, graph), _weights_key(model)
-    ent = per_model.get(gk)
-    if ent is not None and ent[0] == wk:
-        return ent[1]
-    if ent is not None:
-        ent[1].close()
-    if len(per_model) >= 8:  # bound the cache
-        for k in list(per_model)[:4]:
-            per_model.pop(k)[1].close()
-    plan = EnginePlan(model, graph, graph.x.device)
-    per_model[gk] = (wk, plan)
+def plan_for(model, graph, unsupported_ok=False):
+    """Cached EnginePlan for (model weights, graph topology).
+
+    unsupported_ok: a model or graph the engine does not implement (MSW_ERR_UNSUPPORTED or
+    NotImplementedError while describing it) returns None instead of raising, and that
+    answer is cached like a plan (the caller takes its torch path)."""
+    entries = _plans.setdefault(model, [])
+    wk = _weights_key(model)
+    for i, (ref, w, plan) in enumerate(entries):
+        if ref.matches(model, graph):
+            if w == wk:
+                entries.insert(0, entries.pop(i))
+                if plan is None and not unsupported_ok:
+                    break  # rebuild to raise the engine's own error
+                return plan
+            entries.pop(i)
+            if plan is not None:
+                plan.close()
+            break
+    try:
+        plan = EnginePlan(model, graph, graph.x.device)
+    except (NotImplementedError, L.EngineError) as e:
+        if not unsupported_ok or (isinstance(e, L.EngineError) and e.code != L.MSW_ERR_UNSUPPORTED):
+            raise
+        plan = None
+    entries.insert(0, (_GraphRef(model, graph), wk, plan))
+    while len(entries) > CACHE_PLANS:
+        old = entries.pop()[2]
+        if old is not None:
+            old.close()
     return plan

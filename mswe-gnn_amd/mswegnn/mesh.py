@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 __all__ = ["Graph", "make_multiscale_mesh", "make_single_scale_mesh", "wet_state",
-           "mesh_config"]
+           "mesh_config", "config3_members"]
 
 
 class Graph:
@@ -303,6 +303,20 @@ def wet_state(graph, seed=0, depth=0.8, frac=0.35, previous_t=3, all_wet=False):
         x[:, 3 + 2 * tau] = q
     g.x = torch.from_numpy(x.astype(np.float32))
     return g
+
+
+def config3_members(num_scales=3, count=8):
+    """BASELINE config 3: a batch of Zenodo-like test meshes whose fine-cell counts span the
+    real test set's 8,191-12,989 (database/overview.csv:82-101): coarse sizes cycled so the
+    members hold 8,193-12,801 fine nodes (incl. the ghost), seeds 0..count-1.
+    Returns make_multiscale_mesh keyword dicts."""
+    if num_scales == 4:
+        sizes = [8, 9, 10]                    # 8,192 / 10,368 / 12,800 fine faces
+    elif num_scales == 3:
+        sizes = [16, 17, 18, 19, 20]          # 8,192 / 9,248 / 10,368 / 11,552 / 12,800
+    else:
+        raise ValueError("config 3 is defined for 3 or 4 scales")
+    return [dict(n_coarse=sizes[i % len(sizes)], num_scales=num_scales, seed=i) for i in range(count)]
 
 
 def mesh_config(name):

@@ -308,6 +308,14 @@ class PartitionedRollout:
             pl.close()
 
 
+def group_root(group=None):
+    """Global rank of `group`'s rank 0 (torch.distributed collectives take global ranks)."""
+    import torch.distributed as dist
+    if group is None:
+        return 0
+    return dist.get_global_rank(group, 0)
+
+
 class DistributedRollout:
     """One part per process (torch.distributed initialised, one GPU per rank): the rank's
     plan exchanges its halo over RCCL inside msw_rollout.  rollout() returns this rank's
@@ -331,7 +339,8 @@ class DistributedRollout:
         if self.rank == 0:
             L.check(L.lib().msw_comm_unique_id(uid))
         box = [bytes(uid.raw)]
-        dist.broadcast_object_list(box, src=0, group=group)
+        # src is a GLOBAL rank: the group's rank 0 (global rank 0 may not be in the group)
+        dist.broadcast_object_list(box, src=group_root(group), group=group)
         L.check(L.lib().msw_plan_set_comm(self.plan._h, box[0], self.world, self.rank))
 
     def rollout(self, x0, BC, node_BC, type_BC, T):

@@ -25,12 +25,17 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
-sys.path[:0] = [os.path.join(ROOT, "oracle", "refstubs"), REF, os.path.join(ROOT, "mswe-gnn_amd"),
-                os.path.join(ROOT, "oracle")]
+# Only the stand-ins and the reference on the path while the reference's modules import:
+# its models/ has no __init__.py (a namespace package), so the drop-in's regular ``models``
+# package would win from ANY position on sys.path.
+sys.path[:0] = [os.path.join(ROOT, "oracle", "refstubs"), REF]
 sys.dont_write_bytecode = True
 
 from models.gnn import MSGNN, GNN  # noqa: E402  (the reference's modules)
 from training.train import rollout_test  # noqa: E402
+import models.gnn as _refgnn  # noqa: E402
+assert _refgnn.__file__.startswith(REF), _refgnn.__file__
+sys.path += [os.path.join(ROOT, "mswe-gnn_amd"), os.path.join(ROOT, "oracle")]
 from mswegnn.mesh import make_multiscale_mesh, make_single_scale_mesh, wet_state, mesh_config  # noqa: E402
 import msgnn_torch as orc  # noqa: E402
 
@@ -145,10 +150,21 @@ def main():
     with torch.no_grad():
         r = rollout_test(model, g)
     print(f"  zenodo4 reference rollout48: {time.time() - t:.2f} s (8 threads)")
-    sel = np.array([0, 5, 11, 23, 35, 47])
+    sel = np.arange(48)  # every step (the bench times all of them)
     save("fx_zenodo4_K4_F32_rollout48", steps=sel, rollout_sel=r[..., sel].contiguous(),
          digest=np.frombuffer(bytes.fromhex(graph_digest(g)), np.uint8))
     manifest["zenodo4_ref_seconds_8thr"] = time.time() - t
+
+    # ------------------------------------------------------------ config 4: dk15-like, 200 steps
+    g = make_multiscale_mesh(**mesh_config("dk15"), T=200)
+    t = time.time()
+    with torch.no_grad():
+        r = rollout_test(model, g)
+    print(f"  dk15 reference rollout200: {time.time() - t:.2f} s (8 threads)")
+    sel = np.array(sorted(set(range(0, 200, 20)) | set(range(19, 200, 20))))
+    save("fx_dk15_K4_F32_rollout200", steps=sel, rollout_sel=r[..., sel].contiguous(),
+         digest=np.frombuffer(bytes.fromhex(graph_digest(g)), np.uint8))
+    manifest["dk15_ref_seconds_8thr"] = time.time() - t
 
     # ------------------------------------------------------------ 3-scale MSGNN, seeded init
     cfg = orc.msgnn_config(num_scales=3, hid_features=32, K=4)
@@ -178,10 +194,90 @@ def main():
     save("fx_gnn_small_rollout10", x=g.x, y=y, rollout=r,
          digest=np.frombuffer(bytes.fromhex(graph_digest(g)), np.uint8))
 
+    gen_batches()
+
+    manifest["cpu"] = cpu_model()
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, default=str)
     print(f"done in {time.time() - t0:.1f} s")
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# Batched rollouts: heterogeneous meshes collated as a PyG Batch
+# (oracle/refstubs/torch_geometric/data: PyG's collation restated) and run through the
+# reference's own rollout_test -> adapt_batch_training -> update_batch_multiscale
+# (training/train.py:14-95).  Each member is described by the arguments that regenerate it.
+BATCHES = {
+    # 4-scale, shipped K4_F32 checkpoint: three meshes of two sizes, one wet start
+    "fx_batch_K4_F32": dict(kind="msgnn", S=4, F=32, K=4, ckpt="K4_F32", T=12, members=[
+        dict(n_coarse=2, seed=11, wet=None), dict(n_coarse=3, seed=12, wet=5),
+        dict(n_coarse=2, seed=13, wet=None)]),
+    # 3-scale, seeded init (msgnn3 weights): two sizes, wet starts
+    "fx_batch_msgnn3": dict(kind="msgnn", S=3, F=32, K=4, ckpt=None, T=6, members=[
+        dict(n_coarse=5, seed=21, wet=6), dict(n_coarse=6, seed=22, wet=7)]),
+    # 1-scale GNN (config 1 model): the single-scale branch of adapt_batch_training
+    "fx_batch_gnn": dict(kind="gnn", T=5, members=[
+        dict(n_coarse=2, seed=31, wet=8), dict(n_coarse=3, seed=32, wet=9)]),
+}
+
+
+def batch_member(spec, m):
+    """The synthetic graph of one batch member (also used by tests/)."""
+    if spec["kind"] == "gnn":
+        g = make_single_scale_mesh(n_coarse=m["n_coarse"], refinements=3, seed=m["seed"], T=spec["T"])
+    else:
+        g = make_multiscale_mesh(n_coarse=m["n_coarse"], num_scales=spec["S"], seed=m["seed"], T=spec["T"])
+    return wet_state(g, seed=m["wet"]) if m["wet"] is not None else g
+
+
+def gen_batches():
+    from torch_geometric.data import Data, Batch
+    from training.train import adapt_batch_training
+    for name, spec in BATCHES.items():
+        if spec["kind"] == "gnn":
+            cfg = orc.gnn_config(hid_features=32, K=2, n_GNN_layers=2, mlp_layers=1)
+            model = ref_gnn(cfg)
+        else:
+            cfg = orc.msgnn_config(num_scales=spec["S"], hid_features=spec["F"], K=spec["K"])
+            model = ref_msgnn(cfg, load_ckpt(spec["ckpt"]) if spec["ckpt"] else None)
+        P = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        gs = [batch_member(spec, m) for m in spec["members"]]
+        batch = Batch.from_data_list([Data(**g.__dict__) for g in gs])
+        with torch.no_grad():
+            r = rollout_test(model, batch)
+        temp = adapt_batch_training(batch)
+        # the members one by one through the oracle (batching must not change a member)
+        ptr = batch.ptr
+        for i, g in enumerate(gs):
+            with torch.no_grad():
+                o = orc.rollout(P, cfg, g, spec["T"])
+            d = (r[ptr[i]:ptr[i + 1]] - o).abs().max().item()
+            print(f"  {name} member {i}: reference batch vs oracle single max|diff| = {d:.3e}")
+        arrays = dict(rollout=r, ptr=ptr, node_BC=temp.node_BC, node_BC_ptr=temp.node_BC_ptr,
+                      edge_index=temp.edge_index)
+        if spec["kind"] != "gnn":
+            arrays.update(node_ptr=temp.node_ptr, edge_ptr=temp.edge_ptr, intra_edge_ptr=temp.intra_edge_ptr,
+                          intra_mesh_edge_index=temp.intra_mesh_edge_index, edge_attr=temp.edge_attr)
+        arrays["digests"] = np.stack([np.frombuffer(bytes.fromhex(graph_digest(g)), np.uint8) for g in gs])
+        save(name, **arrays)
+        manifest[name + "_spec"] = spec
+
+
 if __name__ == "__main__":
-    main()
+    if "--batches-only" in sys.argv:  # add the batch fixtures to an existing manifest
+        with open(os.path.join(OUT, "manifest.json")) as f:
+            manifest.update(json.load(f))
+        gen_batches()
+        with open(os.path.join(OUT, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1, default=str)
+    else:
+        main()

@@ -1,1 +1,1 @@
-from . import callbacks  # noqa: F401
+from . import callbacks, loggers  # noqa: F401

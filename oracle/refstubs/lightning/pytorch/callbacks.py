@@ -5,3 +5,13 @@ class Callback:
 class BatchSizeFinder:
     def __init__(self, *a, **k):
         pass
+
+
+class EarlyStopping(Callback):  # import-only stand-in
+    def __init__(self, *a, **k):
+        pass
+
+
+class ModelCheckpoint(Callback):  # import-only stand-in
+    def __init__(self, *a, **k):
+        pass

@@ -90,3 +90,43 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def graph_digest(g):
+    """sha256 of a graph's input arrays (oracle/gen_golden.py graph_digest)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in ("x", "edge_index", "edge_attr", "edge_ptr", "node_ptr", "intra_mesh_edge_index",
+              "intra_edge_ptr", "BC", "node_BC"):
+        if k in g.keys():
+            h.update(np.ascontiguousarray(getattr(g, k).numpy()).tobytes())
+    return np.frombuffer(bytes.fromhex(h.hexdigest()), np.uint8)
+
+
+BATCH_FIXTURES = ["fx_batch_K4_F32", "fx_batch_msgnn3", "fx_batch_gnn"]
+
+
+def batch_fixture(name):
+    """-> (spec, member graphs, fixture arrays) of a batched-rollout fixture written by the
+    reference's rollout_test on a PyG Batch (oracle/gen_golden.py BATCHES)."""
+    from mswegnn.mesh import make_multiscale_mesh, make_single_scale_mesh, wet_state
+    spec = manifest()[name + "_spec"]
+    gs = []
+    for m in spec["members"]:
+        if spec["kind"] == "gnn":
+            g = make_single_scale_mesh(n_coarse=m["n_coarse"], refinements=3, seed=m["seed"], T=spec["T"])
+        else:
+            g = make_multiscale_mesh(n_coarse=m["n_coarse"], num_scales=spec["S"], seed=m["seed"], T=spec["T"])
+        gs.append(wet_state(g, seed=m["wet"]) if m["wet"] is not None else g)
+    return spec, gs, golden(name)
+
+
+def batch_model(spec):
+    """-> (model, oracle weights, oracle cfg) of a batch fixture."""
+    import msgnn_torch as orc
+    if spec["kind"] == "gnn":
+        P = weights("gnn_F32_seed42")
+        return build_gnn(state=P), P, orc.gnn_config(hid_features=32, K=2, n_GNN_layers=2, mlp_layers=1)
+    P = weights(spec["ckpt"] or "msgnn3_F32_seed666")
+    return (build_msgnn(num_scales=spec["S"], hid=spec["F"], K=spec["K"], state=P), P,
+            orc.msgnn_config(num_scales=spec["S"], hid_features=spec["F"], K=spec["K"]))

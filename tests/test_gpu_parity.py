@@ -173,7 +173,7 @@ def test_fused_rollout_matches_step_loop_and_graph_capture(cuda):
     T = 20) == msw_rollout without graph == the reference-style Python loop over the HIP
     forward (training/train.py semantics)."""
     from mswegnn.engine import plan_for
-    from utils.dataset import apply_boundary_condition, use_prediction
+    from mswegnn.rollout import apply_boundary_condition, use_prediction
     T = 20
     g = make_multiscale_mesh(**mesh_config("small"), T=T).to(cuda)
     m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
@@ -197,7 +197,7 @@ def test_fused_rollout_matches_step_loop_and_graph_capture(cuda):
 
 
 def test_rollout_test_dropin(cuda):
-    from training.train import rollout_test
+    from mswegnn.rollout import rollout_test
     fx = golden("fx_small_K4_F32_rollout48")
     g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
     m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
@@ -291,7 +291,7 @@ def test_batched_graphs_match_individual(cuda):
     ra = m.rollout(ga.to(cuda)).cpu()
     rb = m.rollout(gb.to(cuda)).cpu()
     bt = collate([ga, gb])
-    from training.train import rollout_test
+    from mswegnn.rollout import rollout_test
     r = rollout_test(m, bt.to(cuda)).cpu()
     na = ga.num_nodes
     assert per_step_rel(r[:na], ra) <= REL_TOL
@@ -379,3 +379,51 @@ def test_partitioned_rollout_matches_whole_mesh(cuda, parts):
     mg = _hip(build_gnn(state=weights("gnn_F32_seed42")), cuda)
     rg = PartitionedRollout(mg, gs, parts, cuda).rollout(gs.x, gs.BC, gs.node_BC, gs.type_BC, 10).cpu()
     assert per_step_rel(rg, torch.from_numpy(golden("fx_gnn_small_rollout10")["rollout"])) <= REL_TOL
+
+
+def test_plan_cache_same_shape_graphs_in_sequence(cuda):
+    """Two meshes of the same shape but different topology / edge_attr, one after the other,
+    each freshly moved to the GPU (the allocator may hand the second the first's freed
+    addresses): each rollout must match the oracle on its own graph, not a stale plan."""
+    P = weights("K4_F32")
+    cfg = orc.msgnn_config(num_scales=4, hid_features=32, K=4)
+    m = _hip(build_msgnn(4, 32, 4, state=P), cuda)
+    from mswegnn.rollout import rollout_test
+    for seed in (3, 4, 3):
+        g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), seed=seed, T=4), seed=seed)
+        gd = g.to(cuda)
+        r = rollout_test(m, gd).cpu()
+        del gd
+        assert per_step_rel(r, orc.rollout(P, cfg, g, 4)) <= REL_TOL, seed
+
+
+def test_auto_engine_falls_back_for_unsupported_models(cuda):
+    """engine='auto': a model the engine does not implement runs the torch path on the GPU
+    (and gives the same result as engine='torch'); engine='hip' raises instead."""
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=3), seed=1).to(cuda)
+    for kw in (dict(learned_pooling=True), dict(hid=24)):
+        m = build_msgnn(4, kw.pop("hid", 32), 4, **kw).to(cuda)
+        with torch.no_grad():
+            y = m(g)
+            m.engine = "torch"
+            y_t = m(g)
+        assert torch.equal(y, y_t)
+        m.engine = "hip"
+        with pytest.raises(RuntimeError):
+            with torch.no_grad():
+                m(g)
+
+
+def test_broadcast_bc_column(cuda):
+    """BC given as [n_BC, 1, T+1] broadcasts over the previous_t slots, as the reference's
+    x_d[node_BC, (type_BC-1)::2] = BC does (utils/dataset.py:496)."""
+    P = weights("K4_F32")
+    cfg = orc.msgnn_config(num_scales=4, hid_features=32, K=4)
+    g = make_multiscale_mesh(**mesh_config("tiny"), T=6)
+    g.BC = g.BC[:, 2:3, :].contiguous()
+    m = _hip(build_msgnn(4, 32, 4, state=P), cuda)
+    r = m.rollout(g.to(cuda), 6).cpu()
+    assert per_step_rel(r, orc.rollout(P, cfg, g, 6)) <= REL_TOL
+    g.BC = torch.zeros(1, 2, 7)
+    with pytest.raises(ValueError):
+        m.rollout(g.to(cuda), 6)

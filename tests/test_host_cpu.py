@@ -131,7 +131,7 @@ def test_collate_matches_individual_oracle():
     from mswegnn.batch import collate
     ga = make_multiscale_mesh(n_coarse=2, num_scales=4, seed=1, T=3)
     gb = make_multiscale_mesh(n_coarse=3, num_scales=4, seed=2, T=3)
-    from training.train import adapt_batch_training
+    from mswegnn.rollout import adapt_batch_training
     bt = adapt_batch_training(collate([ga, gb]))
     assert tuple(bt.node_ptr.shape) == (2, 5)
     cfg = manifest()["weights_K4_F32_cfg"]
@@ -149,46 +149,60 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, T, q):
-    import torch.distributed as dist
-    sys.path[:0] = [ROOT, PKG]
+def _rank_main(rank, world, port, T, q, workload, global_batch):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
     torch.set_num_threads(2)
+    import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import argparse
     import bench
-    g, m, w, desc = bench.build_workload("tiny", seed=rank, T=T)
+    args = argparse.Namespace(global_batch=global_batch, batch=1)
+    ids, scaling = bench.simulations_of_rank(args, rank, world)
+    sims, gb, rows, fine = bench.rank_batch(workload, ids, T)
+    m = sims[0][1]
     m.engine = "torch"
-    out = m.rollout(g, T)
-    gather = bench.make_gatherer(dist, world, desc["fine_nodes"], T, torch.device("cpu"))
-    parts = gather(out[:desc["fine_nodes"]].contiguous())
+    out = m.rollout(gb, T)
+    gather = bench.make_gatherer(dist, world, fine, T, torch.device("cpu"))
+    parts = gather((out[:fine] if rows is None else out.index_select(0, rows)).contiguous())
     if rank == 0:
-        q.put([p.clone().numpy() for p in parts])
+        q.put(([p.clone().numpy() for p in parts], scaling))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_sharding_and_allgather_gloo():
-    """bench.py's N>1 path on CPU: rank r simulates seed r, ONE all-gather at the end
-    delivers every rank's fine-scale rollout to every rank."""
+@pytest.mark.parametrize("workload,global_batch", [("tiny_mixed", 0), ("tiny_mixed", 3)])
+def test_two_rank_sharding_and_allgather_gloo(workload, global_batch):
+    """bench.py's N>1 path on CPU, world size 2.  Weak (global_batch 0): rank r simulates
+    seed r.  Strong (--global-batch 3): the fixed set {0, 1, 2} split round-robin, rank 0
+    runs {0, 2} as one batch, rank 1 runs {1}.  Ranks hold meshes of different sizes, so the
+    all-gather pads; ONE all-gather at the end delivers every rank's fine-scale rollouts."""
     T, world = 3, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, T, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, T, q, workload, global_batch))
+             for r in range(world)]
     for p in procs:
         p.start()
-    parts = q.get(timeout=600)
+    parts, scaling = q.get(timeout=600)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     sys.path.insert(0, ROOT)
     import bench
+    assert scaling == ("strong" if global_batch else "weak")
+    owners = [[i for i in range(global_batch) if i % world == r] if global_batch else [r] for r in range(world)]
+    assert parts[0].shape[0] != parts[1].shape[0], "ranks must hold different mesh sizes (padding path)"
     for r in range(world):
-        g, m, w, desc = bench.build_workload("tiny", seed=r, T=T)
-        m.engine = "torch"
-        ref = m.rollout(g, T)[:desc["fine_nodes"]]
-        assert np.array_equal(parts[r], ref.numpy()), f"rank {r} slot"
-    assert not np.array_equal(parts[0], parts[1]), "ranks must simulate different seeds"
+        refs = []
+        for i in owners[r]:
+            g, m, w, desc = bench.build_workload(workload, seed=i, T=T)
+            m.engine = "torch"
+            refs.append(m.rollout(g, T)[:desc["fine_nodes"]])
+        ref = torch.cat(refs).numpy()
+        assert parts[r].shape == ref.shape, (r, parts[r].shape, ref.shape)
+        assert np.abs(parts[r] - ref).max() <= 1e-5 * max(np.abs(ref).max(), 1e-30), f"rank {r} slot"
 
 
 def test_metrics_oracle_matches_reference_fixture():
@@ -393,3 +407,34 @@ def test_pmc_summary_attribution(tmp_path):
     assert s["k_hop_large"]["kernel"].startswith("k_hop<2, 1, false, true>")
     assert s["k_hop"]["kernel"].startswith("k_hop<2, 1, false, false>")  # most dispatches
     assert s["k_hop"]["hbm_bytes_per_launch"] == 2 * 1024 * 10.0 + 1024 * 5.0
+
+
+def _subgroup_main(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from mswegnn.partition import group_root
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sub = dist.new_group([1, 2])
+    if rank in (1, 2):
+        box = [f"uid-from-{rank}".encode()] if dist.get_rank(sub) == 0 else [None]
+        # DistributedRollout's unique-id broadcast within a group without global rank 0
+        dist.broadcast_object_list(box, src=group_root(sub), group=sub)
+        q.put((rank, group_root(sub), box[0]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_uid_broadcast_in_subgroup_gloo():
+    """The partitioned rollout's unique id is broadcast from the group's rank 0, named by
+    its GLOBAL rank (src=0 hangs for a group without global rank 0)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_main, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == [(1, 1, b"uid-from-1"), (2, 1, b"uid-from-1")]

@@ -1,9 +1,12 @@
 """The oracle (oracle/msgnn_torch.py) is pinned to outputs of the reference itself.
 
 The fixtures were produced by running sdat2/mSWE-GNN's own MSGNN / GNN modules and
-rollout_test on CPU (oracle/gen_golden.py); the oracle must reproduce them bit for bit
-(same ATen CPU ops in the same order).  The synthetic meshes must also regenerate
-identically (digest check), since fixtures store only the inputs that are not derivable.
+rollout_test on CPU (oracle/gen_golden.py, which also asserts oracle == reference bit for
+bit on the generating machine).  On a machine with the same CPU model (manifest "cpu") the
+oracle must reproduce them bit for bit (same ATen CPU ops in the same order); on another
+CPU the fp32 GEMM kernels round differently, so the bar there is 1e-5 relative per step.
+The synthetic meshes must also regenerate identically (digest check), since fixtures store
+only the inputs that are not derivable.
 """
 import hashlib
 
@@ -11,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, manifest, weights
+from conftest import golden, manifest, per_step_rel, weights
 import msgnn_torch as orc
 from mswegnn.mesh import make_multiscale_mesh, make_single_scale_mesh, wet_state, mesh_config
 
@@ -30,6 +33,30 @@ def _threads():
     torch.set_num_threads(min(8, torch.get_num_threads()))
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+SAME_CPU = manifest().get("cpu") == _cpu_model()
+
+
+def assert_pinned(ours, ref):
+    """Bit-exact on the fixture's CPU model, 1e-5 relative per step elsewhere."""
+    ref = torch.as_tensor(ref)
+    if SAME_CPU:
+        assert torch.equal(ours, ref), (ours - ref).abs().max().item()
+    else:
+        o, r = ours.reshape(ours.shape[0], -1, ours.shape[-1] if ours.dim() == 3 else 1), \
+            ref.reshape(ref.shape[0], -1, ref.shape[-1] if ref.dim() == 3 else 1)
+        assert per_step_rel(o, r) <= 1e-5
+
+
 @pytest.mark.parametrize("ck", ["K4_F32", "K2_F16"])
 def test_oracle_single_step(ck):
     fx = golden(f"fx_tiny_{ck}_step")
@@ -37,7 +64,7 @@ def test_oracle_single_step(ck):
     g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=48), seed=1)
     assert np.array_equal(_digest(g), fx["digest"]), "mesh generator drifted"
     y = orc.forward(weights(ck), cfg, g)
-    assert torch.equal(y, torch.from_numpy(fx["y"]))
+    assert_pinned(y, torch.from_numpy(fx["y"]))
 
 
 @pytest.mark.parametrize("ck", ["K4_F32", "K2_F16"])
@@ -47,7 +74,7 @@ def test_oracle_rollout48(ck):
     g = make_multiscale_mesh(**mesh_config("small"), T=48)
     assert np.array_equal(_digest(g), fx["digest"])
     r = orc.rollout(weights(ck), cfg, g)
-    assert torch.equal(r, torch.from_numpy(fx["rollout"]))
+    assert_pinned(r, torch.from_numpy(fx["rollout"]))
 
 
 def test_oracle_msgnn3_wet():
@@ -56,8 +83,8 @@ def test_oracle_msgnn3_wet():
     g = wet_state(make_multiscale_mesh(**mesh_config("small3"), T=6), seed=3)
     assert np.array_equal(_digest(g), fx["digest"])
     P = weights("msgnn3_F32_seed666")
-    assert torch.equal(orc.forward(P, cfg, g), torch.from_numpy(fx["y"]))
-    assert torch.equal(orc.rollout(P, cfg, g), torch.from_numpy(fx["rollout"]))
+    assert_pinned(orc.forward(P, cfg, g), torch.from_numpy(fx["y"]))
+    assert_pinned(orc.rollout(P, cfg, g), torch.from_numpy(fx["rollout"]))
 
 
 def test_oracle_gnn_config1():
@@ -66,8 +93,8 @@ def test_oracle_gnn_config1():
     g = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=10), seed=2)
     assert np.array_equal(_digest(g), fx["digest"])
     P = weights("gnn_F32_seed42")
-    assert torch.equal(orc.forward(P, cfg, g), torch.from_numpy(fx["y"]))
-    assert torch.equal(orc.rollout(P, cfg, g), torch.from_numpy(fx["rollout"]))
+    assert_pinned(orc.forward(P, cfg, g), torch.from_numpy(fx["y"]))
+    assert_pinned(orc.rollout(P, cfg, g), torch.from_numpy(fx["rollout"]))
 
 
 def test_oracle_zenodo_size_rollout():
@@ -77,4 +104,16 @@ def test_oracle_zenodo_size_rollout():
     g = make_multiscale_mesh(**mesh_config("zenodo4"), T=48)
     assert np.array_equal(_digest(g), fx["digest"])
     r = orc.rollout(weights("K4_F32"), cfg, g)
-    assert torch.equal(r[..., fx["steps"]], torch.from_numpy(fx["rollout_sel"]))
+    assert_pinned(r[..., fx["steps"]], torch.from_numpy(fx["rollout_sel"]))
+
+
+def test_oracle_dk15_first_steps():
+    """Config 4 (dk15-like, T = 200): the oracle's first 20 steps against the reference's
+    stored steps 0 and 19 (the GPU test checks every stored step up to 199)."""
+    fx = golden("fx_dk15_K4_F32_rollout200")
+    cfg = manifest()["weights_K4_F32_cfg"]
+    g = make_multiscale_mesh(**mesh_config("dk15"), T=200)
+    assert np.array_equal(_digest(g), fx["digest"])
+    r = orc.rollout(weights("K4_F32"), cfg, g, 20)
+    idx = [i for i, s in enumerate(fx["steps"]) if s < 20]
+    assert_pinned(r[..., fx["steps"][idx]], torch.from_numpy(fx["rollout_sel"][..., idx]))

@@ -18,7 +18,7 @@ MODE=${1:-all}
 if [[ $MODE == all || $MODE == tests ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   if ! grep -q "smoke ok" $OUT/smoke.log; then echo "stopping: smoke failed" >> $OUT/steps.log; exit 3; fi
-  step gputests 900 python -m pytest tests -m gpu -q > $OUT/gpu_tests.log 2>&1
+  step gputests 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -x > $OUT/gpu_tests.log 2>&1
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
   step bench 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err
