@@ -33,7 +33,7 @@ def source_hash(variant=""):
         h.update(os.path.basename(path).encode())
         with open(path, "rb") as fh:
             h.update(fh.read())
-    h.update(" ".join(FLAGS + [variant]).encode())
+    h.update(" ".join(FLAGS + [variant]).replace(ROOT, "<root>").encode())  # path-independent
     return h.hexdigest()
 
 

@@ -305,6 +305,22 @@ class _GraphRef:
                 and all(a is b for a, b in zip(ts, self.tensors))
                 and self.versions == tuple(t._version for t in ts))
 
+    def same_content(self, model, graph):
+        """Equal values in other tensors (e.g. ``graph.clone()``, which the reference's
+        rollout_test makes once per rollout, train.py:80): one device compare per tensor."""
+        ts = tuple(getattr(graph, n) for n in _TOPOLOGY[model.type_model])
+        if self.shape != (tuple(graph.x.shape), str(graph.x.device)):
+            return False
+        for a, b in zip(ts, self.tensors):
+            if a.shape != b.shape or a.dtype != b.dtype:
+                return False
+        return all(torch.equal(a, b.to(a.device)) for a, b in zip(ts, self.tensors))
+
+    def adopt(self, model, graph):
+        """Hold the new (equal) tensors so the next calls with them hit by identity."""
+        self.tensors = tuple(getattr(graph, n) for n in _TOPOLOGY[model.type_model])
+        self.versions = tuple(t._version for t in self.tensors)
+
 
 def _weights_key(model):
     return tuple((p.data_ptr(), p._version) for p in model.parameters())
@@ -333,6 +349,14 @@ def plan_for(model, graph, unsupported_ok=False):
             if plan is not None:
                 plan.close()
             break
+    else:
+        for i, (ref, w, plan) in enumerate(entries):
+            if w == wk and ref.same_content(model, graph):
+                ref.adopt(model, graph)
+                entries.insert(0, entries.pop(i))
+                if plan is None and not unsupported_ok:
+                    break
+                return plan
     try:
         plan = EnginePlan(model, graph, graph.x.device)
     except (NotImplementedError, L.EngineError) as e:

@@ -130,3 +130,35 @@ def batch_model(spec):
     P = weights(spec["ckpt"] or "msgnn3_F32_seed666")
     return (build_msgnn(num_scales=spec["S"], hid=spec["F"], K=spec["K"], state=P), P,
             orc.msgnn_config(num_scales=spec["S"], hid_features=spec["F"], K=spec["K"]))
+
+
+def oracle_fp64_rollout(P, cfg, g, T):
+    """The oracle in float64 (weights, inputs and arithmetic): the exact-arithmetic yardstick
+    for rollouts whose fp32 result is itself sensitive to rounding."""
+    import msgnn_torch as orc
+    P64 = {k: v.double() for k, v in P.items()}
+    g64 = g.clone()
+    for k in ("x", "edge_attr", "BC"):
+        setattr(g64, k, getattr(g, k).double())
+    return orc.rollout(P64, cfg, g64, T).float()
+
+
+def assert_rollout_parity(ours, ref, P, cfg, g, T, label=""):
+    """The north star's bar, 1e-4 relative per step against the fp32 reference, with one
+    documented exception: a rollout the reference itself cannot resolve in fp32 -- its fp32
+    result differs from exact (fp64) arithmetic by more than 1e-4, which happens when a
+    cell's depth lands within rounding of the 1e-4 threshold of _mask_small_WD
+    (models/models.py:79-91) and the mask flips.  There ours must be no further from the
+    fp64 result than the fp32 reference is (x1.5), and the event is reported.
+    Returns (error vs fp32 reference, error of the fp32 reference vs fp64 or None)."""
+    e = per_step_rel(ours, ref)
+    if e <= REL_TOL:
+        return e, None
+    r64 = oracle_fp64_rollout(P, cfg, g, T)
+    e_ref = per_step_rel(ref, r64)
+    e_ours = per_step_rel(ours, r64)
+    print(f"{label}: rel err {e:.2e} vs the fp32 reference; fp32 reference vs fp64 {e_ref:.2e}, "
+          f"ours vs fp64 {e_ours:.2e} (mask-threshold flip)")
+    assert e_ref > REL_TOL, f"{label}: {e:.2e} > {REL_TOL} on a well-conditioned rollout"
+    assert e_ours <= 1.5 * e_ref, f"{label}: ours {e_ours:.2e} vs fp64, reference {e_ref:.2e}"
+    return e, e_ref

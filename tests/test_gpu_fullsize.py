@@ -19,7 +19,7 @@ import sys
 import pytest
 import torch
 
-from conftest import REL_TOL, ROOT, per_step_rel, rel_err
+from conftest import REL_TOL, ROOT, assert_rollout_parity, per_step_rel, rel_err
 import msgnn_torch as orc
 
 pytestmark = pytest.mark.gpu
@@ -120,10 +120,13 @@ def test_config3_batch_of_8_meshes_vs_oracle(cuda, S):
     mh, bd = _hip(m, b, cuda)
     parts = split_rollout(rollout_test(mh, bd).cpu(), b)
     _oracle_threads()
-    worst = 0.0
+    worst, flips = 0.0, []
     for i, g in enumerate(gs):
         ref = orc.rollout(P, cfg, g, T)
-        e = per_step_rel(parts[i], ref)
+        e, e_ref = assert_rollout_parity(parts[i], ref, P, cfg, g, T, label=f"config 3 member {i}")
         worst = max(worst, e)
-        assert e <= REL_TOL, (i, e)
-    print(f"config 3 ({S} scales): worst member rel err {worst:.2e}")
+        if e_ref is not None:
+            flips.append(i)
+    assert len(flips) <= 1, flips
+    print(f"config 3 ({S} scales): worst member rel err {worst:.2e}; members with a mask-threshold "
+          f"flip in the fp32 reference itself: {flips}")

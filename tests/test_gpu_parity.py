@@ -407,7 +407,7 @@ def test_auto_engine_falls_back_for_unsupported_models(cuda):
             y = m(g)
             m.engine = "torch"
             y_t = m(g)
-        assert torch.equal(y, y_t)
+        assert rel_err(y, y_t) <= 1e-5  # torch's GPU index_add_ is not bit-deterministic
         m.engine = "hip"
         with pytest.raises(RuntimeError):
             with torch.no_grad():

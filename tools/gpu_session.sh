@@ -18,7 +18,7 @@ MODE=${1:-all}
 if [[ $MODE == all || $MODE == tests ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   if ! grep -q "smoke ok" $OUT/smoke.log; then echo "stopping: smoke failed" >> $OUT/steps.log; exit 3; fi
-  step gputests 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -x > $OUT/gpu_tests.log 2>&1
+  step gputests 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
   step bench 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err
@@ -27,6 +27,11 @@ if [[ $MODE == all || $MODE == prof ]]; then
   export TMPDIR=/tmp
   rm -rf $OUT/prof
   step rocprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+fi
+if [[ $MODE == all || $MODE == extra ]]; then
+  step bench_refloop 300 python bench.py --caller reference-loop --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_refloop.json 2> $OUT/bench_refloop.err
+  step bench_config3 300 python bench.py --workload config3 --global-batch 8 --no-roofline-large --steps 5 --warmup 2 > $OUT/bench_config3.json 2> $OUT/bench_config3.err
+  step strong 900 python tools/strong_scaling.py --workload config3 --G 8 20 64 > $OUT/strong_scaling.jsonl 2> $OUT/strong_scaling.err
 fi
 if [[ $MODE == pmc ]]; then
   export TMPDIR=/tmp
