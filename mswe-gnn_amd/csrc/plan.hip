@@ -350,6 +350,7 @@ struct msw_plan {
   // turns chains of up to m hops on.
   int hop_pairs = 0;
   int chain_max = kChainMax;
+  int chain_max_tiles = 1 << 30;  // chains only on scales with at most this many edge tiles (MSW_HOP_CHAIN_TILES)
   // A layer's last hop on a scale with at least this many edge tiles runs as a middle hop
   // + a row epilogue launch (engine.h EpiArgs); MSW_EPI_SPLIT_TILES overrides (0: never).
   // Measured on MI355X (profiles/r01_v7/ab_epi_split.txt).
@@ -1247,7 +1248,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     for (size_t q = 0; q < pcsr.size(); ++q)
       if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
     if ((rc = pupload(P, &c.recs, recs))) return rc;
-    for (int m = 2; P->hop_pairs && m <= P->chain_max; ++m)
+    for (int m = 2; P->hop_pairs && c.ntiles <= P->chain_max_tiles && m <= P->chain_max; ++m)
       if ((rc = build_chain(P, c, rowptr, so, tl, pcsr, m))) return rc;
   }
   // intra-scale levels
@@ -1444,6 +1445,9 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
 
   if (const char* es = getenv("MSW_EPI_SPLIT_TILES")) P->epi_split_tiles = atoi(es);
   if (const char* gs = getenv("MSW_GRAPH_STEPS")) P->graph_steps = std::max(1, atoi(gs));
+  // F = 64: four-wave cooperative kernels on every scale whose grid stays resident
+  // (zenodo4_f64 +3.3 %, profiles/r02_v1/ab_coop_f64.txt); F = 32 keeps 1024 (no gain above)
+  if (P->NT == 4) P->coop_waves = 4096;
   if (const char* cw = getenv("MSW_COOP_WAVES")) P->coop_waves = std::max(0, atoi(cw));
   {
     const char* kinds[3] = {"MSW_COOP_WAVES_EH", "MSW_COOP_WAVES_HOP", "MSW_COOP_WAVES_POOL"};
@@ -1455,6 +1459,7 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
   if (const char* cm = getenv("MSW_HOP_CHAINS")) {  // a chain's halo is m-1 rings deep: not on parts
     P->chain_max = std::max(2, std::min(kChainMax, atoi(cm)));
     P->hop_pairs = xch ? 0 : 1;
+    if (const char* ct = getenv("MSW_HOP_CHAIN_TILES")) P->chain_max_tiles = std::max(0, atoi(ct));
   }
   P->part_rank = xch ? rank : -1;
   int rc = build_graph_plan(P.get(), g);
