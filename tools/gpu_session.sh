@@ -31,7 +31,7 @@ fi
 if [[ $MODE == all || $MODE == extra ]]; then
   step bench_refloop 300 python bench.py --caller reference-loop --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_refloop.json 2> $OUT/bench_refloop.err
   step bench_config3 300 python bench.py --workload config3 --global-batch 8 --no-roofline-large --steps 5 --warmup 2 > $OUT/bench_config3.json 2> $OUT/bench_config3.err
-  step strong 900 python tools/strong_scaling.py --workload config3 --G 8 20 64 > $OUT/strong_scaling.jsonl 2> $OUT/strong_scaling.err
+  [[ -n "${STRONG:-}" ]] && step strong 900 python tools/strong_scaling.py --workload config3 --G 8 20 64 > $OUT/strong_scaling.jsonl 2> $OUT/strong_scaling.err
 fi
 if [[ $MODE == pmc ]]; then
   export TMPDIR=/tmp
