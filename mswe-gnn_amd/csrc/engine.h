@@ -47,7 +47,9 @@ struct RolloutIO {
   int bc_tstride;
   int type_bc;
   int T;
-  int step;         // current step, advanced by the encoder kernel of each step
+  int step;         // rollout mode: -1 before step 0; advanced once per step -- by the encoder
+                    // when the last hops decode, by the first edge-MLP launch when the decoder
+                    // is deferred to the next encoder (which then reads t - 1, the step it decodes)
 };
 
 // Node projection of one SWEGNN layer from [x_s ; x_in] of a node tile:
@@ -109,7 +111,15 @@ struct EncodeArgs {
   int vu_a[kMaxScales];    // unpool V (x_s part) for fine rows of level s, -1 = none
   int vu_h1t;
   float* Vu;
-  RolloutIO* io;           // rollout mode: advance io->step
+  RolloutIO* io;           // rollout mode with the decoder in the last hops: advance io->step
+  // Rollout mode: the decoder of the PREVIOUS step runs here, row-locally, before the
+  // encoders (its input, the last SWEGNN layer's output, is stored by that layer's last
+  // hop): prediction -> rollout output, window shift + BC of this step into X, and the
+  // encoders read the updated state.  dec.on = 0 in forward mode (the decoder then runs in
+  // the last hops' epilogues).  decode_only = 1: the rollout's final decode (no encoders).
+  DecDesc dec;
+  const float* dec_in;     // [Npad][F] decoder input rows (x_up / the GNN's last layer output)
+  int decode_only;
 };
 
 // Edge tile: whole destination neighbourhoods, <= 16 edges and <= 16 destinations (host).
@@ -165,6 +175,8 @@ struct EdgeHopArgs {
   Epilogue epi;
   int coop;                        // waves per tile (k_edge_coop: MFMA output tiles split
                                    // across them), 0/1 = one wave per tile
+  int* step_inc;                   // rollout mode, first edge-MLP launch of a step:
+                                   // &RolloutIO::step, advanced once (workgroup 0, lane 0)
 };
 
 // Hops 2..K over the same edge tiles as the fused first hop.

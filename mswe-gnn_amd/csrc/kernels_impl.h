@@ -327,6 +327,65 @@ __device__ __forceinline__ void decode_tail(const f32x4 (&o)[1], const DecDesc& 
   }
 }
 
+// Rollout mode, in the NEXT step's encoder: the decoder of a 16-row node tile (x: the last
+// SWEGNN layer's output rows, pre-activation applied here) + decode_tail's arithmetic (the
+// same operations in the same order) and state update.  Every lane of a row ends with the
+// row's new dynamic columns in nd (window shifted, prediction appended, BC of step t + 1);
+// lane group 0 writes the rollout output and the state row.  W: the decoder operands.
+template <int NT, int ACT>
+__device__ __forceinline__ void decode_state(const f32x4 (&x)[NT], const DecDesc& d, const Common& c,
+                                             const float* W, const EpiPre<NT>& pre, int n, bool valid,
+                                             int lane, int g, float (&nd)[kMaxDyn]) {
+#pragma clang fp contract(off)
+  f32x4 x0[NT], o[1];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) x0[t] = x[t];
+  act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
+  run_mlp<NT, NT, 1, ACT>(x0, o, d.dec, W, lane, g);
+  // output features 0 (h) and 1 (|q|) live in lane group 0: every lane of the row takes them
+  float h = __shfl(o[0].x, lane & 15), v = __shfl(o[0].y, lane & 15);
+  if (d.resw_off >= 0) {
+    const float* rw = W + d.resw_off;
+    float rh = pre.xd[0] * rw[0];
+    float rv = pre.xd[1] * rw[1];
+#pragma unroll
+    for (int tau = 1; tau < kMaxDyn / 2; ++tau) {
+      if (tau < c.p) {
+        rh = rh + pre.xd[2 * tau] * rw[2 * tau];
+        rv = rv + pre.xd[2 * tau + 1] * rw[2 * tau + 1];
+      }
+    }
+    h = h + rh;
+    v = v + rv;
+  }
+  h = h > 0.f ? h : 0.f;  // torch.relu
+  v = v > 0.f ? v : 0.f;
+  const float hm = h * (fabsf(h) > 1e-4f ? 1.f : 0.f);  // _mask_small_WD(epsilon=1e-4)
+  const float vm = v * (h != 0.f ? 1.f : 0.f);
+  // use_prediction (window shift) + apply_boundary_condition of the next step; selects keep
+  // nd in registers (run-time column indices would put it in scratch)
+  const RolloutIO* io = d.io;
+  const int t = pre.step, b = pre.bc;
+  const bool bc_on = b >= 0 && t + 1 < io->bc_tstride;
+  const int c0 = io->type_bc - 1;
+#pragma unroll
+  for (int k = 0; k < kMaxDyn; ++k) {
+    float val = k + 2 < c.dyn ? pre.xd[k + 2] : (k == c.dyn - 2 ? hm : (k == c.dyn - 1 ? vm : 0.f));
+    const int tau = (k - c0) >> 1;
+    if (bc_on && k >= c0 && ((k - c0) & 1) == 0 && tau < c.p)
+      val = io->bc[((size_t)b * c.p + tau) * io->bc_tstride + t + 1];
+    nd[k] = val;
+  }
+  if (!valid || g || pre.ext < 0) return;
+  const int ext = pre.ext;
+  io->out[((size_t)ext * 2 + 0) * io->T + t] = hm;
+  io->out[((size_t)ext * 2 + 1) * io->T + t] = vm;
+  float* xw = const_cast<float*>(d.X) + (size_t)n * c.nnf + (c.nnf - c.dyn);
+#pragma unroll
+  for (int k = 0; k < kMaxDyn; ++k)
+    if (k < c.dyn) xw[k] = nd[k];
+}
+
 // What follows the last hop of a SWEGNN layer, on the layer's destination rows.
 template <int NT, int ACT>
 __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& e, const Common& c,
@@ -398,8 +457,12 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   MSW_MARK(a.c, 0);
-  if (a.io && blockIdx.x == 0 && threadIdx.x == 0) a.io->step += 1;
   Common c = a.c;
+  // rollout mode: the step whose prediction this launch decodes (the previous one; -1 at
+  // step 0, whose state k_init_state wrote)
+  const int dstep = a.dec.on ? a.dec.io->step : -1;
+  // rollout mode, decoder in the last hops (large meshes): advance the step they read
+  if (!a.dec.on && a.io && blockIdx.x == 0 && threadIdx.x == 0) a.io->step += 1;
   const int nchunks = a.Npad / kRowsPerBlock;
   int staged = -1;  // scale whose region is in LDS
   // grid-stride over 64-row chunks (scale ranges are 64-aligned: a chunk has one scale);
@@ -415,13 +478,24 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     const float* xr = a.x + (size_t)xrow * a.c.nnf;
     const int nstat = a.c.nstat_raw;
     float raw[4], dyn[4];
+    float wlv;
+    EpiPre<NT> pre;
+    f32x4 xu[NT];
+    if (dstep >= 0) {  // the decoder's inputs, loaded before the weight staging
+      load_row<NT>(xu, a.dec_in + (size_t)n * F, g);
+      pre.ext = ext;
+      pre.step = dstep;
+      pre.bc = a.dec.bc_slot[n];
+#pragma unroll
+      for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[nstat + k] : 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * g + r;
       raw[r] = f < nstat ? xr[f] : 0.f;
       dyn[r] = f < a.c.dyn ? xr[nstat + f] : 0.f;
     }
-    const float wlv = xr[nstat - 1] + xr[a.c.nnf - 2];  // water level = bed elevation + depth
+    wlv = xr[nstat - 1] + xr[a.c.nnf - 2];  // water level = bed elevation + depth
     MSW_MARK(c, 1);
     if constexpr (kStaged<NT>) {
       if (s != staged) {  // uniform across the workgroup: every wave walks the same chunks
@@ -434,6 +508,23 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     // weight reads straight from the LDS pointer (not through c.W, which the compiler cannot
     // prove to be LDS across the loop: it emitted flat loads, which wait on vmcnt too)
     const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
+    if (dstep >= 0) {  // decode the previous step; the encoders read the updated state
+      float nd[kMaxDyn];
+      decode_state<NT, ACT>(xu, a.dec, c, Wl, pre, n, valid, lane, g, nd);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 4 * g + r;
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < kMaxDyn; ++k) v = (k == f && f < c.dyn) ? nd[k] : v;
+        dyn[r] = v;
+      }
+      float hn = 0.f;
+#pragma unroll
+      for (int k = 0; k < kMaxDyn; ++k) hn = (k == c.dyn - 2) ? nd[k] : hn;
+      wlv = xr[nstat - 1] + hn;
+    }
+    if (a.decode_only) continue;
     MSW_MARK(c, 2);
     f32x4 xs[NT];
     {
@@ -737,6 +828,7 @@ void k_edge_hop(EdgeHopArgs a) {
   int tile = blockIdx.x * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   f32x4 wf[NT][NT];
   if constexpr (!LOOP || !kStaged<NT>)
     load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
@@ -895,6 +987,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   const int tile = blockIdx.x * G + grp;
   const bool live = tile < a.ntiles;
   Common c = a.c;
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
   EdgeHopRows<NT> q;
@@ -1024,6 +1117,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, r = wave_id();
   const int tile = blockIdx.x;
   Common c = a.c;  // c.W stays the blob: the epilogue reads it there
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   // this rank's filter row (out tile r): wr[ti] = W_1 block (r, ti)
   f32x4 wr[NT];
   {

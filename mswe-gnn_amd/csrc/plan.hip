@@ -684,8 +684,23 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
     ea.vu_h1t = P->unpools[0].h1t;
     ea.Vu = P->Vu;
   }
-  q.push_back(LE);
   const DecDesc dd = dec_of(P, rollout ? P->X : nullptr, rollout, nullptr);
+  // rollout mode: the decoder of step t runs in the encoder launch of step t + 1 (and in a
+  // final decode-only launch after the last step, msw_rollout); its input is the last
+  // layer's output, stored by that layer's last hop (x_up rows / the GNN's last layer)
+  // Deferred where the step is latency-bound (zenodo4 +3.2 %, batch of 8 +1.8 %); on meshes
+  // whose finest last hop splits off a row epilogue (>= epi_split_tiles edge tiles) the
+  // decoder stays there (config 5: -1.2 % deferred; profiles/r02_v3/ab_defer_decode.txt).
+  // MSW_DEFER_DECODE=0/1 overrides.
+  bool defer = rollout && P->sc[0].ntiles < P->epi_split_tiles;
+  if (const char* dv = getenv("MSW_DEFER_DECODE")) defer = rollout && atoi(dv) != 0;
+  ea.dec = dd;
+  ea.dec.on = defer ? 1 : 0;
+  ea.dec_in = P->model_type == 0 ? P->xup : P->xgnn;
+  ea.decode_only = 0;
+  q.push_back(LE);
+  DecDesc dl = dd;  // the last hops' decoder: forward mode, or rollout mode not deferred
+  dl.on = defer ? 0 : 1;
   if (P->model_type == 0) {
     Epilogue none{};
     none.np = np_none(); none.uu_a = -1; none.dec.on = 0;
@@ -713,7 +728,7 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
         const Proc& up = P->unpools[i];
         e.uu_a = up.a_u; e.uu_h1t = up.h1t; e.Uu = P->Uu;
       }
-      e.dec = dd;  // every scale's rows are decoded once final (gnn.py:335-348)
+      e.dec = dl;  // every scale's rows are decoded once final (gnn.py:335-348)
       sched_proc(P, q, P->procs[j], P->xup, e);
       if (s > 0) {                      // intra_scale_gnn[i] on level s-1 (+ skip) + projection
         const Proc& up = P->unpools[i];
@@ -741,10 +756,16 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
       e.post_act = P->gnn_act; e.post_slope = P->gnn_slope;
       e.np = j + 1 < L ? np_of(P, P->procs[j + 1]) : np_none();
       e.uu_a = -1;
-      if (j + 1 == L) e.dec = dd; else e.dec.on = 0;
+      if (j + 1 == L) e.dec = dl; else e.dec.on = 0;
       sched_proc(P, q, P->procs[j], P->xgnn, e);
     }
   }
+  if (defer)  // the step counter the next step's encoder reads advances here
+    for (Launch& L : q)
+      if (L.kind == L_EDGE_HOP) {
+        L.eh.step_inc = &P->io_d->step;
+        break;
+      }
 }
 
 // ---------------------------------------------------------------------------- weight regions
@@ -831,7 +852,8 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       // encoder first -- identical relative offsets in every scale's region -- then the
       // dynamic encoder + projection 0 (scale 0) and that scale's unpool V operand
       EncodeArgs& a = L.enc;
-      const MlpDev stat0 = a.stat;
+      const MlpDev stat0 = a.stat, dec0 = a.dec.dec;
+      const int resw0 = a.dec.resw_off;
       a.reg = WReg{0, 0, 0};
       a.lds_floats = 0;
       for (int s = 0; s < a.S; ++s) {
@@ -839,6 +861,12 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
         MlpDev st = stat0;
         rl.mlp(Rs, st);
         a.stat = st;
+        if (a.dec.on) {  // the decoder (rollout mode): same offsets in every scale's region
+          MlpDev dm = dec0;
+          rl.mlp(Rs, dm);
+          a.dec.dec = dm;
+          a.dec.resw_off = Rs.put(resw0, 2 * P->p);
+        }
         if (s == 0) {
           rl.mlp(Rs, a.dynm);
           rl.np(Rs, a.np0);
@@ -1056,6 +1084,21 @@ int schedule_dispatch(msw_plan* P, const std::vector<Launch>& q, hipStream_t st)
     case 2: return run_schedule<2>(P, q, st);
     default: return run_schedule<4>(P, q, st);
   }
+}
+
+// After a rollout's last step: the decoder of that step (the encoder launch of the rollout
+// schedule with decode_only set: no encoders run).
+int final_decode(msw_plan* P, hipStream_t st) {
+  if (P->sched_roll.empty() || P->sched_roll[0].kind != L_ENCODE || !P->sched_roll[0].enc.dec.on)
+    return MSW_OK;
+  Launch L = P->sched_roll[0];
+  L.enc.decode_only = 1;
+  switch (P->NT) {
+    case 1: HIP_TRY(launch_one<1>(L, st)); break;
+    case 2: HIP_TRY(launch_one<2>(L, st)); break;
+    default: HIP_TRY(launch_one<4>(L, st)); break;
+  }
+  return MSW_OK;
 }
 
 // Forward mode: point the encoder at x (graph rows) and the decoder at x / y.
@@ -1329,9 +1372,10 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
   if (L.kind == L_HOP && L.hop.last) { L.hop.last = 0; L.hop.out = P->T[1]; }
   if (L.kind == L_HOPM && L.hopm.last) { L.hopm.last = 0; L.hopm.out = P->T[1]; L.hopm.wfloats = 0; }
   if (L.kind == L_EDGE_HOP && L.eh.last && !unpool) { L.eh.last = 0; L.eh.out = P->T[1]; }
+  if (L.kind == L_EDGE_HOP) L.eh.step_inc = nullptr;  // the rollout's step counter stays put
   if (unpool) edges = P->lv[scale].I;  // the unpool epilogue only writes the next layer's U/V/O
   if (L.kind == L_POOL) edges = P->lv[scale - 1].I;
-  if (L.kind == L_ENCODE) { L.enc.io = nullptr; rows = P->N; edges = 0; }
+  if (L.kind == L_ENCODE) { L.enc.io = nullptr; L.enc.dec.on = 0; rows = P->N; edges = 0; }
   std::vector<Launch> q(1, L);
   for (int it = 0; it < iters; ++it) {
     int rc = schedule_dispatch(P, q, st);
@@ -1784,6 +1828,8 @@ int msw_group_rollout(msw_plan* const* plans, int32_t num_plans, const float* co
                          : group_step<4>(plans, num_plans, st);
     if (rc) return rc;
   }
+  for (int k = 0; k < num_plans; ++k)
+    if (int rc = final_decode(plans[k], st)) return rc;
   for (int k = 0; k < num_plans; ++k) {
     plans[k]->rollout_steps += T;
     plans[k]->forward_calls += T;
@@ -1857,6 +1903,7 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
       if (rc) return rc;
     }
   }
+  if (int rc = final_decode(P, st)) return rc;
   P->rollout_steps += T;
   P->forward_calls += T;
   return MSW_OK;

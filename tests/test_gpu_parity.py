@@ -427,3 +427,26 @@ def test_broadcast_bc_column(cuda):
     g.BC = torch.zeros(1, 2, 7)
     with pytest.raises(ValueError):
         m.rollout(g.to(cuda), 6)
+
+
+@pytest.mark.parametrize("model", ["msgnn_K4_F32", "gnn"])
+def test_deferred_decoder_matches_fused_decoder(cuda, model, monkeypatch):
+    """Rollout mode runs the decoder of step t in the encoder launch of step t + 1 (plus a
+    final decode launch) on latency-bound meshes, in the last hops' epilogues on large ones
+    (MSW_DEFER_DECODE forces either): both orders give the same rollout bit for bit, and
+    the reference's."""
+    outs = {}
+    for dv in ("0", "1"):
+        monkeypatch.setenv("MSW_DEFER_DECODE", dv)
+        if model == "gnn":
+            fx = golden("fx_gnn_small_rollout10")
+            g = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=10), seed=2).to(cuda)
+            m = _hip(build_gnn(state=weights("gnn_F32_seed42")), cuda)
+            outs[dv] = m.rollout(g, 10).cpu()
+        else:
+            fx = golden("fx_small_K4_F32_rollout48")
+            g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
+            m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+            outs[dv] = m.rollout(g).cpu()
+        assert per_step_rel(outs[dv], torch.from_numpy(fx["rollout"])) <= REL_TOL
+    assert torch.equal(outs["0"], outs["1"])
