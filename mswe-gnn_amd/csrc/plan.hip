@@ -688,11 +688,12 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
   // rollout mode: the decoder of step t runs in the encoder launch of step t + 1 (and in a
   // final decode-only launch after the last step, msw_rollout); its input is the last
   // layer's output, stored by that layer's last hop (x_up rows / the GNN's last layer)
-  // Deferred where the step is latency-bound (zenodo4 +3.2 %, batch of 8 +1.8 %); on meshes
-  // whose finest last hop splits off a row epilogue (>= epi_split_tiles edge tiles) the
-  // decoder stays there (config 5: -1.2 % deferred; profiles/r02_v3/ab_defer_decode.txt).
+  // Deferred where the step is latency-bound (zenodo4 +3.2 %, the batch of 8 +1.8 %); on
+  // meshes whose finest scale has >= kDeferMaxTiles edge tiles the decoder stays in the last
+  // hops' row epilogue (config 5: -1.2 % deferred; profiles/r02_v3/ab_defer_decode.txt).
   // MSW_DEFER_DECODE=0/1 overrides.
-  bool defer = rollout && P->sc[0].ntiles < P->epi_split_tiles;
+  constexpr int kDeferMaxTiles = 65536;
+  bool defer = rollout && P->sc[0].ntiles < kDeferMaxTiles;
   if (const char* dv = getenv("MSW_DEFER_DECODE")) defer = rollout && atoi(dv) != 0;
   ea.dec = dd;
   ea.dec.on = defer ? 1 : 0;
