@@ -450,3 +450,23 @@ def test_deferred_decoder_matches_fused_decoder(cuda, model, monkeypatch):
             outs[dv] = m.rollout(g).cpu()
         assert per_step_rel(outs[dv], torch.from_numpy(fx["rollout"])) <= REL_TOL
     assert torch.equal(outs["0"], outs["1"])
+
+
+@pytest.mark.parametrize("act", ["relu", "leakyrelu", "elu", "swish", "sigmoid", "tanh"])
+def test_mlp_activations_vs_oracle(cuda, act):
+    """Every make_mlp activation of activation_functions (models/models.py:149-169) other
+    than the shipped PReLU: the run-time activation path of the kernels (ACT = -1), a
+    3-scale MSGNN rollout against the oracle; the GNN's gnn_activation too."""
+    g = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=3, T=3), seed=9)
+    m = build_msgnn(3, 32, 2, mlp_activation=act)
+    cfg = orc.msgnn_config(num_scales=3, hid_features=32, K=2, mlp_activation=act)
+    ref = orc.rollout(state_dict_of(m), cfg, g)
+    m = _hip(m, cuda)
+    assert per_step_rel(m.rollout(g.to(cuda)).cpu(), ref) <= REL_TOL, act
+    gs = wet_state(make_single_scale_mesh(n_coarse=2, refinements=2, T=3), seed=10)
+    m = build_gnn(hid=16, K=2, n_layers=2, mlp_layers=2, mlp_activation=act, gnn_activation=act)
+    cfg = orc.gnn_config(hid_features=16, K=2, n_GNN_layers=2, mlp_layers=2, mlp_activation=act,
+                         gnn_activation=act)
+    ref = orc.rollout(state_dict_of(m), cfg, gs)
+    m = _hip(m, cuda)
+    assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL, act
