@@ -30,6 +30,12 @@ constexpr int kBlock = 64 * kWaves;
 // staging traffic of a large mesh and the LDS the copies take.
 template <int NT, bool LOOP>
 constexpr int waves_of() { return LOOP && NT <= 2 ? 8 : kWaves; }
+// the grid-stride middle / last hop (k_hop, large meshes): its own workgroup size
+#ifndef MSW_HOP_WAVES
+#define MSW_HOP_WAVES 8
+#endif
+template <int NT, bool LOOP>
+constexpr int hop_waves() { return LOOP && NT <= 2 ? MSW_HOP_WAVES : kWaves; }
 // the fused edge MLP + hop keeps one tile per wave in flight in its grid-stride loop:
 // a software-pipelined loop (next tile's gathers during the MLP) needs > 256 registers,
 // i.e. one wave per SIMD, and measured 24 % slower on the 1M-node mesh
@@ -1255,9 +1261,9 @@ __device__ __forceinline__ void hop_load(HopRows<NT>& r, const HopArgs& a, int t
   hop_gather<NT, LAST>(r, a, load_rec(a.recs, tile, j), tile, j, g);
 }
 template <int NT, int ACT, bool LAST, bool LOOP>
-__global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_hop(HopArgs a) {
+__global__ __launch_bounds__((64 * hop_waves<NT, LOOP>())) void k_hop(HopArgs a) {
 #pragma clang fp contract(off)
-  constexpr int WV = waves_of<NT, LOOP>();
+  constexpr int WV = hop_waves<NT, LOOP>();
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
   __shared__ __attribute__((aligned(16))) float slab_all[WV][kRowsPerWave][XS];
@@ -1956,7 +1962,8 @@ hipError_t prepare_kernels() {
       {(const void*)k_edge_hop<NT, 1, true, 1>, edge_waves<NT, true, 1>()},
       {(const void*)k_edge_hop<NT, -1, true, 1>, edge_waves<NT, true, 1>()},
       {(const void*)k_hop<NT, 1, true, false>, kWaves}, {(const void*)k_hop<NT, -1, true, false>, kWaves},
-      {(const void*)k_hop<NT, 1, true, true>, WL}, {(const void*)k_hop<NT, -1, true, true>, WL},
+      {(const void*)k_hop<NT, 1, true, true>, hop_waves<NT, true>()},
+      {(const void*)k_hop<NT, -1, true, true>, hop_waves<NT, true>()},
       {(const void*)k_pool<NT, false>, kWaves}, {(const void*)k_pool<NT, true>, WL},
       {(const void*)k_pool_edge<NT>, kWaves}, {(const void*)k_pool_edge<NT, NT >= 2 ? NT : 1>, kWaves},
       {(const void*)k_epi<NT, 1, false>, kWaves}, {(const void*)k_epi<NT, -1, false>, kWaves},
@@ -2061,7 +2068,7 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
                            lds_bytes<NT>(a.reg.len), st);
   }
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  const dim3 grid(tile_grid(a)), block(64 * (loop ? hop_waves<NT, true>() : kWaves));
   if (!a.last) {
     if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_hop<NT, 1, false, false>), grid, block, 0, st, a);
@@ -2160,7 +2167,8 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
-                    : 64 * (loop && (kind == 2 || kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
+                    : kind == 2 ? 64 * (loop ? hop_waves<NT, true>() : kWaves)
+                    : 64 * (loop && (kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
     return 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
