@@ -112,7 +112,7 @@ def make_gatherer(dist, world, n0, T, device):
     pad = torch.zeros(nmax, 2, T, device=device)
 
     def gather(out_fine):
-        src = out_fine
+        src = out_fine.to(device)
         if n0 != nmax:
             pad[:n0].copy_(out_fine)
             src = pad
@@ -204,11 +204,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one rank per GPU; MSW_DIST_BACKEND=gloo + more ranks than GPUs rehearses the N > 1 path
+    # on a one-GPU box (ranks share the device; RCCL refuses two ranks on one device)
+    backend = os.environ.get("MSW_DIST_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     T = args.T
@@ -230,7 +237,8 @@ def main():
     from mswegnn import _lib
     plan = plan_for(model, g)
     out = torch.empty(g.num_nodes, 2, T, device=dev)
-    gather = make_gatherer(dist, world, fine_rank, T, dev)
+    # the all-gather runs on the GPU over RCCL; gloo (rehearsal) gathers host copies
+    gather = make_gatherer(dist, world, fine_rank, T, dev if backend == "nccl" else torch.device("cpu"))
 
     if args.caller == "fused":
         def rollout():
@@ -270,13 +278,14 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        red_dev = dev if backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([dt], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / max(args.steps, 1) * 1e3
     nodes_all = fine_rank  # fine nodes simulated per step, summed over ranks (meshes may differ)
     if world > 1:
-        tn = torch.tensor([fine_rank], device=dev, dtype=torch.float64)
+        tn = torch.tensor([fine_rank], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tn, op=dist.ReduceOp.SUM)
         nodes_all = float(tn.item())
     value = nodes_all * T * args.steps / dt
@@ -430,7 +439,8 @@ def main():
             "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (own multi-scale triangular mesh generator; dry start + hydrograph BC)",
             "config": dict(desc, caller=args.caller, global_batch=args.global_batch or None,
-                           parallelism=f"sim-sharded x{world} ({B} sim on rank 0, RCCL all-gather at end)"
+                           parallelism=f"sim-sharded x{world} ({B} sim on rank 0, "
+                           f"{'RCCL' if backend == 'nccl' else backend} all-gather at end)"
                            if world > 1 else ("single GPU" if B == 1 else f"single GPU, batch of {B} sims")),
             "timed_region": "whole rollouts (T steps each) incl. the per-rollout edge encoder + edge "
                             "terms of every processor (msw_rollout prologue); inputs resident in HBM",
