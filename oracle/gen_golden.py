@@ -195,6 +195,7 @@ def main():
          digest=np.frombuffer(bytes.fromhex(graph_digest(g)), np.uint8))
 
     gen_batches()
+    gen_variants()
 
     manifest["cpu"] = cpu_model()
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
@@ -228,6 +229,23 @@ BATCHES = {
     "fx_batch_gnn": dict(kind="gnn", T=5, members=[
         dict(n_coarse=2, seed=31, wet=8), dict(n_coarse=3, seed=32, wet=9)]),
 }
+
+
+def gen_variants():
+    """Reference outputs for options no shipped config sets: upwind_mode=True on every
+    processor (gnn.py:365,431-432) of the seeded 3-scale MSGNN, wet start."""
+    cfg = orc.msgnn_config(num_scales=3, hid_features=32, K=2, upwind_mode=True)
+    model = ref_msgnn(dict(cfg, K_list=[2, 2, 2, 2, 2]))
+    for p in model.gnn_processor:
+        p.upwind_mode = True
+    P = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    g = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=3, T=4), seed=11)
+    with torch.no_grad():
+        r = rollout_test(model, g)
+    check_oracle(P, cfg, g, r, steps=4, label="msgnn3 K2 upwind rollout4")
+    # weights: the seeded init (seed 666), which the drop-in reproduces bit for bit
+    save("fx_upwind_msgnn3_K2", rollout=r, digest=np.frombuffer(bytes.fromhex(graph_digest(g)), np.uint8))
+    manifest["fx_upwind_msgnn3_K2_cfg"] = cfg
 
 
 def batch_member(spec, m):
@@ -273,10 +291,13 @@ def gen_batches():
 
 
 if __name__ == "__main__":
-    if "--batches-only" in sys.argv:  # add the batch fixtures to an existing manifest
+    if "--batches-only" in sys.argv or "--variants-only" in sys.argv:  # add to an existing manifest
         with open(os.path.join(OUT, "manifest.json")) as f:
             manifest.update(json.load(f))
-        gen_batches()
+        if "--batches-only" in sys.argv:
+            gen_batches()
+        if "--variants-only" in sys.argv:
+            gen_variants()
         with open(os.path.join(OUT, "manifest.json"), "w") as f:
             json.dump(manifest, f, indent=1, default=str)
     else:

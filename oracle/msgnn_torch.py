@@ -192,7 +192,8 @@ def msgnn_forward(P, cfg, graph):
     x_up = torch.zeros_like(x_d)
     ef = edge_attr.shape[1]
     kw = dict(normalize=cfg["normalize"], with_filter_matrix=cfg["with_filter_matrix"],
-              with_gradient=cfg["with_gradient"], edge_features=ef)
+              with_gradient=cfg["with_gradient"], edge_features=ef,
+              upwind_mode=cfg.get("upwind_mode", False))  # SWEGNN(upwind_mode=...), gnn.py:365
     for i in range(S - 1):
         x_d = swegnn(P, f"gnn_processor.{i}", x_s, x_d, edge_index[:, edge_ptr[i]:edge_ptr[i + 1]],
                      edge_attr[edge_ptr[i]:edge_ptr[i + 1]], Kl[i], L, act, **kw)
@@ -243,7 +244,8 @@ def gnn_forward(P, cfg, graph):
     for i in range(cfg["n_GNN_layers"]):
         x = swegnn(P, f"gnn_processor.{i}", x_s, x_d, edge_index, edge_attr, cfg["K"], L, act,
                    normalize=cfg["normalize"], with_filter_matrix=cfg["with_filter_matrix"],
-                   with_gradient=cfg["with_gradient"], edge_features=edge_attr.shape[1])
+                   with_gradient=cfg["with_gradient"], edge_features=edge_attr.shape[1],
+                   upwind_mode=cfg.get("upwind_mode", False))
         x = activation(cfg["gnn_activation"], x, P.get("gnn_activation.weight"))
         x_d = x
     x = mlp(P, "node_decoder", x, L, act, dropout=bool(cfg.get("dropout", 0)))

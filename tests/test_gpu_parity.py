@@ -470,3 +470,26 @@ def test_mlp_activations_vs_oracle(cuda, act):
     ref = orc.rollout(state_dict_of(m), cfg, gs)
     m = _hip(m, cuda)
     assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL, act
+
+
+def test_upwind_mode_vs_oracle(cuda):
+    """SWEGNN(upwind_mode=True) (gnn.py:365,431-432: negative hydraulic gradients clamped to
+    0) on every processor -- no shipped config sets it -- against the oracle, MSGNN and GNN."""
+    g = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=3, T=4), seed=11)
+    m = build_msgnn(3, 32, 2)
+    for p in m.gnn_processor:
+        p.upwind_mode = True
+    cfg = orc.msgnn_config(num_scales=3, hid_features=32, K=2, upwind_mode=True)
+    ref = torch.from_numpy(golden("fx_upwind_msgnn3_K2")["rollout"])  # the reference's own
+    ref_plain = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=3, hid_features=32, K=2), g)
+    assert not torch.equal(ref, ref_plain)  # the clamp changes the result on this state
+    m = _hip(m, cuda)
+    assert per_step_rel(m.rollout(g.to(cuda)).cpu(), ref) <= REL_TOL
+    gs = wet_state(make_single_scale_mesh(n_coarse=2, refinements=2, T=4), seed=12)
+    m = build_gnn(hid=32, K=2, n_layers=2, mlp_layers=2)
+    for p in m.gnn_processor:
+        p.upwind_mode = True
+    cfg = orc.gnn_config(hid_features=32, K=2, n_GNN_layers=2, mlp_layers=2, upwind_mode=True)
+    ref = orc.rollout(state_dict_of(m), cfg, gs)
+    m = _hip(m, cuda)
+    assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL

@@ -117,3 +117,17 @@ def test_oracle_dk15_first_steps():
     r = orc.rollout(weights("K4_F32"), cfg, g, 20)
     idx = [i for i, s in enumerate(fx["steps"]) if s < 20]
     assert_pinned(r[..., fx["steps"][idx]], torch.from_numpy(fx["rollout_sel"][..., idx]))
+
+
+def test_oracle_upwind_mode_and_seeded_init():
+    """upwind_mode=True on every processor (gnn.py:431-432), pinned to the reference's own
+    rollout; the weights are the drop-in's seeded init (seed 666), so this also pins that
+    construction order against the reference's."""
+    from conftest import build_msgnn, state_dict_of
+    fx = golden("fx_upwind_msgnn3_K2")
+    cfg = manifest()["fx_upwind_msgnn3_K2_cfg"]
+    g = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=3, T=4), seed=11)
+    assert np.array_equal(_digest(g), fx["digest"])
+    m = build_msgnn(3, 32, 2)
+    r = orc.rollout(state_dict_of(m), cfg, g)
+    assert_pinned(r, torch.from_numpy(fx["rollout"]))
