@@ -457,7 +457,10 @@ __device__ __forceinline__ int chunk_ceil(int n) { return (n + kChunk - 1) / kCh
 // Static / dynamic node encoders incl. the water-level feature (MSGNN.forward
 // gnn.py:284-294, GNN.forward :112-123) + projection of processor 0 + the x_s part of
 // every unpooling layer's V.  One workgroup = 64 rows of one scale.
-template <int NT, int ACT>
+// DEC: the rollout variant that decodes the previous step first (EncodeArgs::dec.on); the
+// other variant keeps the encoders' register budget (four waves per SIMD) for forward mode
+// and the large meshes whose last hops decode.
+template <int NT, int ACT, bool DEC>
 __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
   constexpr int F = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -466,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
   Common c = a.c;
   // rollout mode: the step whose prediction this launch decodes (the previous one; -1 at
   // step 0, whose state k_init_state wrote)
-  const int dstep = a.dec.on ? a.dec.io->step : -1;
+  const int dstep = DEC ? a.dec.io->step : -1;
   // rollout mode, decoder in the last hops (large meshes): advance the step they read
   if (!a.dec.on && a.io && blockIdx.x == 0 && threadIdx.x == 0) a.io->step += 1;
   const int nchunks = a.Npad / kRowsPerBlock;
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     float wlv;
     EpiPre<NT> pre;
     f32x4 xu[NT];
-    if (dstep >= 0) {  // the decoder's inputs, loaded before the weight staging
+    if (DEC && dstep >= 0) {  // the decoder's inputs, loaded before the weight staging
       load_row<NT>(xu, a.dec_in + (size_t)n * F, g);
       pre.ext = ext;
       pre.step = dstep;
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     // weight reads straight from the LDS pointer (not through c.W, which the compiler cannot
     // prove to be LDS across the loop: it emitted flat loads, which wait on vmcnt too)
     const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
-    if (dstep >= 0) {  // decode the previous step; the encoders read the updated state
+    if (DEC && dstep >= 0) {  // decode the previous step; the encoders read the updated state
       float nd[kMaxDyn];
       decode_state<NT, ACT>(xu, a.dec, c, Wl, pre, n, valid, lane, g, nd);
 #pragma unroll
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
       for (int k = 0; k < kMaxDyn; ++k) hn = (k == c.dyn - 2) ? nd[k] : hn;
       wlv = xr[nstat - 1] + hn;
     }
-    if (a.decode_only) continue;
+    if (DEC && a.decode_only) continue;
     MSW_MARK(c, 2);
     f32x4 xs[NT];
     {
@@ -1954,7 +1957,8 @@ hipError_t prepare_kernels() {
   auto mx = [](int wv) { return 160 * 1024 - wv * kRowsPerWave * (16 * 2 * NT + 16 * NT + 4) * (int)sizeof(float); };
   constexpr int WL = waves_of<NT, true>();
   const std::pair<const void*, int> fns[] = {
-      {(const void*)k_encode<NT, 1>, kWaves}, {(const void*)k_encode<NT, -1>, kWaves},
+      {(const void*)k_encode<NT, 1, false>, kWaves}, {(const void*)k_encode<NT, -1, false>, kWaves},
+      {(const void*)k_encode<NT, 1, true>, kWaves}, {(const void*)k_encode<NT, -1, true>, kWaves},
       {(const void*)k_edge_hop<NT, 1, false, 0>, kWaves}, {(const void*)k_edge_hop<NT, -1, false, 0>, kWaves},
       {(const void*)k_edge_hop<NT, 1, false, 1>, kWaves}, {(const void*)k_edge_hop<NT, -1, false, 1>, kWaves},
       {(const void*)k_edge_hop<NT, 1, true, 0>, edge_waves<NT, true, 0>()},
@@ -2014,10 +2018,16 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   const int n = a.Npad / kRowsPerBlock;
   const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.lds_floats);
-  if (a.c.prelu)
-    hipLaunchKernelGGL((k_encode<NT, 1>), grid, block, sh, st, a);
-  else
-    hipLaunchKernelGGL((k_encode<NT, -1>), grid, block, sh, st, a);
+  if (a.dec.on) {
+    if (a.c.prelu)
+      hipLaunchKernelGGL((k_encode<NT, 1, true>), grid, block, sh, st, a);
+    else
+      hipLaunchKernelGGL((k_encode<NT, -1, true>), grid, block, sh, st, a);
+  } else if (a.c.prelu) {
+    hipLaunchKernelGGL((k_encode<NT, 1, false>), grid, block, sh, st, a);
+  } else {
+    hipLaunchKernelGGL((k_encode<NT, -1, false>), grid, block, sh, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -2144,7 +2154,7 @@ hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
 template <int NT, bool LOOP>
 static const void* kernel_of(int kind, int prelu, int last) {
   switch (kind) {
-    case 0: return prelu ? (const void*)k_encode<NT, 1> : (const void*)k_encode<NT, -1>;
+    case 0: return prelu ? (const void*)k_encode<NT, 1, false> : (const void*)k_encode<NT, -1, false>;
     case 1: return edge_hop_kernel<NT>(prelu, LOOP, last);
     case 2:
       return !last ? (const void*)k_hop<NT, 1, false, LOOP>
