@@ -130,6 +130,13 @@ struct TileRange {
 // (source row, local lane of its destination); as node lane, destination j (row, slot
 // range [q & 255, q >> 8) of its in-edges).  Per-edge arrays (Pe, s) are tile-padded:
 // edge slot j of tile t lives at row 16 t + j.
+// Dense edge chunks of a scale (k_edge_mlp): 16 consecutive real edges of the tile order,
+// padding slots skipped; src / dst internal rows and the edge's tile-padded slot p
+// (-1 = past the last edge).
+struct EdgeChunk {
+  int src, dst, p, pad;
+};
+
 struct LaneRec {
   int src;  // internal source row, -1 = no edge in this slot
   int dl;   // destination lane (0..15) of the edge
@@ -177,6 +184,7 @@ struct EdgeHopArgs {
                                    // across them), 0/1 = one wave per tile
   int* step_inc;                   // rollout mode, first edge-MLP launch of a step:
                                    // &RolloutIO::step, advanced once (workgroup 0, lane 0)
+  const EdgeChunk* chunks; int nchunks;  // k_edge_mlp: dense 16-edge chunks [nchunks][16]
 };
 
 // Hops 2..K over the same edge tiles as the fused first hop.
@@ -327,6 +335,7 @@ template <int NT> hipError_t prepare_kernels();
 template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop);
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hopm(const HopMArgs& a, hipStream_t st);

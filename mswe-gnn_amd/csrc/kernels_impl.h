@@ -890,6 +890,79 @@ void k_edge_hop(EdgeHopArgs a) {
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- edge MLP alone
+// F = 64 scales whose edge tiles exceed one round of the fused kernel (plan.hip sched_proc,
+// MSW_SPLIT_EDGE_MLP): the edge MLP of a layer's first hop on its own, s for every edge;
+// hop 1 then runs as a k_hop launch.  Without the hop state (source / own rows, filter,
+// node -> edge slab) the kernel fits two waves per SIMD where the fused kernel runs one, and
+// it needs no whole neighbourhoods: it walks dense chunks of 16 real edges (EdgeChunk), so
+// the last partly filled round of the tile order disappears (zenodo4: 2,050 tiles on 1,024
+// fused waves = three rounds; 1,927 chunks on 2,048 waves = one).  The arithmetic is
+// edge_hop_core's, operation for operation: s is bit-identical.
+constexpr int kMlpWaves = 8;
+template <int NT, int ACT>
+__global__ __launch_bounds__(64 * kMlpWaves) __attribute__((amdgpu_waves_per_eu(2)))
+void k_edge_mlp(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = wave_id();
+  const int stride = gridDim.x * kMlpWaves;
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
+  const float* Wm = a.c.W;
+  if (a.reg.len > 0) {
+    stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
+    __syncthreads();
+    Wm = smem;
+  }
+  const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  for (int ch = blockIdx.x * kMlpWaves + w; ch < a.nchunks; ch += stride) {
+    const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+    const int4 e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+    const bool ev = e.z >= 0;
+    const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
+    const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
+    const float* Pb = a.Pe && ev ? a.Pe + (size_t)e.z * hs : z;
+    f32x4 H[T2];
+#pragma unroll
+    for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
+      const int off = 16 * t + 4 * g;
+      const bool on = t < a.h1t;
+      const f32x4 u = ld4((on ? Ub : z) + off);
+      const f32x4 v = ld4((on ? Vb : z) + off);
+      const f32x4 pe = ld4((on ? Pb : z) + off);
+      const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
+      H[t] = on ? (u + v) + p : zero4();
+    }
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 q = sv[t] / nrm;
+        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+        q.y = (q.y == q.y) ? q.y : 0.f;
+        q.z = (q.z == q.z) ? q.z : 0.f;
+        q.w = (q.w == q.w) ? q.w : 0.f;
+        sv[t] = q;
+      }
+    }
+    if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  }
+}
+
 // ---------------------------------------------------------------------------- cooperative edge hop
 // The fused edge MLP + hop with P waves per tile, for scales whose tiles are far fewer than
 // the chip's SIMDs (the MLP chain of one wave is then the launch's critical path): every
@@ -1976,6 +2049,10 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
+  for (const void* f : {(const void*)k_edge_mlp<NT, 1>, (const void*)k_edge_mlp<NT, -1>}) {  // no slab
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
   if constexpr (NT >= 2) {  // cooperative last hops (F = 32, 64)
     for (int prelu = 0; prelu < 2; ++prelu) {
       hipError_t e = hipFuncSetAttribute(hop_coop_kernel<NT>(prelu), hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
@@ -2049,6 +2126,17 @@ static const void* edge_hop_kernel(int prelu, bool loop, int last) {
   }
   if (last) return prelu ? (const void*)k_edge_hop<NT, 1, false, 1> : (const void*)k_edge_hop<NT, -1, false, 1>;
   return prelu ? (const void*)k_edge_hop<NT, 1, false, 0> : (const void*)k_edge_hop<NT, -1, false, 0>;
+}
+template <int NT>
+hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st) {
+  if (a.nchunks <= 0) return hipSuccess;
+  const int n = cdiv(a.nchunks, kMlpWaves);
+  const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(64 * kMlpWaves);
+  if (a.c.prelu)
+    hipLaunchKernelGGL((k_edge_mlp<NT, 1>), grid, block, eh_lds_bytes(a.reg.len), st, a);
+  else
+    hipLaunchKernelGGL((k_edge_mlp<NT, -1>), grid, block, eh_lds_bytes(a.reg.len), st, a);
+  return hipGetLastError();
 }
 template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
@@ -2164,6 +2252,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     case 7: return edge_coop_kernel<NT>(prelu, last);
     case 9: return hop_coop_kernel<NT>(prelu);
+    case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }
@@ -2173,10 +2262,11 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
-  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7) ? eh_lds_bytes((int)(dyn_bytes / 4))
+  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7 || kind == 10) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
+                    : kind == 10 ? 64 * kMlpWaves
                     : kind == 2 ? 64 * (loop ? hop_waves<NT, true>() : kWaves)
                     : 64 * (loop && (kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
@@ -2191,6 +2281,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template int resident_blocks<NT>(int, int, int, size_t, int);                   \
   template hipError_t launch_encode<NT>(const EncodeArgs&, hipStream_t);          \
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
+  template hipError_t launch_edge_mlp<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
   template hipError_t launch_hopm<NT>(const HopMArgs&, hipStream_t);              \

@@ -191,6 +191,8 @@ struct ScaleCSR {
   int E = 0;                    // edges of this scale
   LaneRec* recs = nullptr;      // [ntiles][16]
   int ntiles = 0;
+  EdgeChunk* chunks = nullptr;  // [nchunks][16] dense edge chunks (k_edge_mlp)
+  int nchunks = 0;
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
   // hop chains of m = 2, 3 hops (engine.h HopMArgs), indexed by m; ok = false -> not built
   struct Chain {
@@ -266,7 +268,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOPM, L_EXCHANGE, L_EPI };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOPM, L_EXCHANGE, L_EPI, L_EDGE_MLP };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -294,7 +296,8 @@ struct Launch {
   Common& common() {
     switch (kind) {
       case L_ENCODE: return enc.c;
-      case L_EDGE_HOP: return eh.c;
+      case L_EDGE_HOP:
+      case L_EDGE_MLP: return eh.c;
       case L_HOP: return hop.c;
       case L_HOPM: return hopm.c;
       case L_EXCHANGE: return xch.c;
@@ -572,6 +575,7 @@ bool chain_fits(const msw_plan* P, const ScaleCSR& g, int m, bool last, const Ep
   return chain_lds(P, g.chain[m], m, last ? epi_floats(P, epi) : 0) <= 160 * 1024;
 }
 
+constexpr int kSplitMlpTiles = 1024;  // F = 64: split edge MLP from this many edge tiles up
 void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi) {
   const ScaleCSR& g = P->sc[pr.scale];
   const Common c = common_of(P);
@@ -591,7 +595,31 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   eh.last = pr.K == 1;
   eh.out = pr.K == 1 ? out : P->T[0];
   eh.epi = epi;
-  q.push_back(L1);
+  // F = 64 scales beyond one round of the fused kernel (one wave per SIMD): the edge MLP
+  // alone over dense edge chunks (k_edge_mlp, two waves per SIMD) + hop 1 as a k_hop launch
+  // (MSW_SPLIT_EDGE_MLP=0/1 overrides the size rule)
+  bool split = P->NT == 4 && pr.K > 1 && P->part_rank < 0 && g.ntiles >= kSplitMlpTiles;
+  if (const char* sv = getenv("MSW_SPLIT_EDGE_MLP")) split = pr.K > 1 && P->part_rank < 0 && atoi(sv) != 0;
+  if (split) {
+    L1.kind = L_EDGE_MLP;
+    eh.chunks = g.chunks; eh.nchunks = g.nchunks;
+    q.push_back(L1);
+    Launch H;
+    H.kind = L_HOP;
+    H.scale = pr.scale;
+    HopArgs& h = H.hop;
+    h.c = c;
+    h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
+    h.s = P->s; h.xs = P->xs;
+    h.in = P->O[pr.par]; h.out = P->T[0];
+    h.filt_a = eh.filt_a;
+    h.grad = pr.with_gradient; h.upwind = pr.upwind;
+    h.last = 0;
+    h.epi = epi;
+    q.push_back(H);
+  } else {
+    q.push_back(L1);
+  }
   const float* cur = P->T[0];
   for (int k = 2; k <= pr.K;) {
     sched_exchange(P, q, pr.scale, {{cur == P->T[0] ? B_T0 : B_T1, P->F}});
@@ -763,7 +791,7 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
   }
   if (defer)  // the step counter the next step's encoder reads advances here
     for (Launch& L : q)
-      if (L.kind == L_EDGE_HOP) {
+      if (L.kind == L_EDGE_HOP || L.kind == L_EDGE_MLP) {
         L.eh.step_inc = &P->io_d->step;
         break;
       }
@@ -831,7 +859,7 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
     WReg* reg = nullptr;
     int tot = 0;
     if (mlp_only) {
-      if (L.kind != L_EDGE_HOP) continue;
+      if (L.kind != L_EDGE_HOP && L.kind != L_EDGE_MLP) continue;
       EdgeHopArgs& a = L.eh;
       const int len = 16 * a.h1t + [&] {
         int n = 0;
@@ -877,6 +905,15 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
         a.lds_floats = std::max(a.lds_floats, a.sreg[s].len);
       }
       tot = (a.lds_floats + 255) / 256 * 256;
+    } else if (L.kind == L_EDGE_MLP) {
+      EdgeHopArgs& a = L.eh;  // the MLP operands only
+      RegionBuilder R(P->blob, 0);
+      a.b1_off = R.put(a.b1_off, 16 * a.h1t);
+      rl.mlp(R, a.rest);
+      a.reg = R.done();
+      a.reg_nf = a.reg.len;
+      a.filt_l = -1;
+      reg = &a.reg;
     } else if (L.kind == L_EDGE_HOP) {
       EdgeHopArgs& a = L.eh;
       RegionBuilder R(P->blob, 0);
@@ -953,6 +990,9 @@ void set_grid_cap(msw_plan* P, Launch& L) {
     case L_ENCODE:
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
       break;
+    case L_EDGE_MLP:
+      L.eh.max_blocks = resident_of(P->NT, 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
+      break;
     case L_EDGE_HOP: {
       EdgeHopArgs& a = L.eh;
       caps(P, a, 1, a.c.prelu, a.last, a.reg.len);
@@ -1021,6 +1061,7 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
   switch (L.kind) {
     case L_ENCODE: return launch_encode<NT>(L.enc, st);
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
+    case L_EDGE_MLP: return launch_edge_mlp<NT>(L.eh, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
     case L_HOPM: return launch_hopm<NT>(L.hopm, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
@@ -1292,6 +1333,15 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     for (size_t q = 0; q < pcsr.size(); ++q)
       if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
     if ((rc = pupload(P, &c.recs, recs))) return rc;
+    {
+      std::vector<EdgeChunk> ck;
+      for (size_t q = 0; q < recs.size(); ++q)
+        if (recs[q].src >= 0)
+          ck.push_back(EdgeChunk{recs[q].src, recs[q / kRowsPerWave * kRowsPerWave + recs[q].dl].n, (int)q, 0});
+      c.nchunks = (int)((ck.size() + kRowsPerWave - 1) / kRowsPerWave);
+      ck.resize((size_t)c.nchunks * kRowsPerWave, EdgeChunk{-1, -1, -1, 0});
+      if (c.nchunks > 0 && (rc = pupload(P, &c.chunks, ck))) return rc;
+    }
     for (int m = 2; P->hop_pairs && c.ntiles <= P->chain_max_tiles && m <= P->chain_max; ++m)
       if ((rc = build_chain(P, c, rowptr, so, tl, pcsr, m))) return rc;
   }
@@ -1360,7 +1410,8 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
   const bool unpool = kernel == 4;  // the intra-scale (unpooling) layer into `scale`
   const Launch* src = nullptr;
   for (const Launch& L : P->sched_roll)
-    if (L.kind == kind_of[kernel] && (L.kind == L_ENCODE || L.scale == scale) &&
+    if ((L.kind == kind_of[kernel] || (kernel == 1 && L.kind == L_EDGE_MLP)) &&
+        (L.kind == L_ENCODE || L.scale == scale) &&
         (L.kind != L_EDGE_HOP || (L.eh.own_zero != 0) == unpool)) {
       if (!src) src = &L;
       if (L.kind == L_HOP && !L.hop.last) { src = &L; break; }  // prefer a middle hop
@@ -1373,7 +1424,7 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
   if (L.kind == L_HOP && L.hop.last) { L.hop.last = 0; L.hop.out = P->T[1]; }
   if (L.kind == L_HOPM && L.hopm.last) { L.hopm.last = 0; L.hopm.out = P->T[1]; L.hopm.wfloats = 0; }
   if (L.kind == L_EDGE_HOP && L.eh.last && !unpool) { L.eh.last = 0; L.eh.out = P->T[1]; }
-  if (L.kind == L_EDGE_HOP) L.eh.step_inc = nullptr;  // the rollout's step counter stays put
+  if (L.kind == L_EDGE_HOP || L.kind == L_EDGE_MLP) L.eh.step_inc = nullptr;  // the rollout's step counter stays put
   if (unpool) edges = P->lv[scale].I;  // the unpool epilogue only writes the next layer's U/V/O
   if (L.kind == L_POOL) edges = P->lv[scale - 1].I;
   if (L.kind == L_ENCODE) { L.enc.io = nullptr; L.enc.dec.on = 0; rows = P->N; edges = 0; }

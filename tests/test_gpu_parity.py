@@ -493,3 +493,32 @@ def test_upwind_mode_vs_oracle(cuda):
     ref = orc.rollout(state_dict_of(m), cfg, gs)
     m = _hip(m, cuda)
     assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL
+
+
+@pytest.mark.parametrize("F", [64, 32])
+def test_split_edge_mlp_matches_fused(cuda, F, monkeypatch):
+    """MSW_SPLIT_EDGE_MLP=1: each processor's edge MLP over dense 16-edge chunks (k_edge_mlp,
+    padding slots skipped, the last chunk partly filled) + hop 1 as a k_hop launch -- the
+    default for F = 64 scales with >= 1024 edge tiles -- gives the fused kernel's forward and
+    rollout bit for bit, on one mesh and on a batch of two meshes of different sizes; and the
+    oracle's rollout."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import rollout_test
+    ga = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=5)
+    gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=2, T=6), seed=6)
+    outs = {}
+    for sv in ("0", "1"):
+        monkeypatch.setenv("MSW_SPLIT_EDGE_MLP", sv)
+        m = _hip(build_msgnn(4, F, 4), cuda)
+        gd = ga.to(cuda)
+        with torch.no_grad():
+            y = m(gd).cpu()
+        outs[sv] = (y, m.rollout(gd).cpu(), _stats(m, gd)["kernels_per_step"],
+                    rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
+    assert outs["1"][2] > outs["0"][2]  # the split launches were scheduled
+    for i in (0, 1, 3):
+        assert torch.equal(outs["0"][i], outs["1"][i])
+    m = build_msgnn(4, F, 4)
+    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), ga)
+    assert per_step_rel(outs["1"][1], ref) <= REL_TOL
+    assert per_step_rel(outs["1"][3][:ga.num_nodes], ref) <= REL_TOL
