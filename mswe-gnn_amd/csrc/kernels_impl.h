@@ -422,6 +422,9 @@ __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& 
 // its memory counters and records {shader clock, 100 MHz clock} at each phase mark, so the
 // dependent-latency chain of one launch can be read phase by phase.
 #ifdef MSW_TRACE
+// Every workgroup also records its start (mark 0, thread 0) and the end of its last wave
+// (mark 9, max over waves) in 100 MHz ticks at trace[32 + 2 b] / [33 + 2 b], b < kTraceWG.
+constexpr int kTraceWG = 8192;
 #define MSW_MARK(c, k)                                                          \
   do {                                                                          \
     if ((c).trace && blockIdx.x == 0 && threadIdx.x < 64) {                     \
@@ -429,6 +432,13 @@ __device__ __forceinline__ void node_epilogue(f32x4 (&res)[NT], const Epilogue& 
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();               \
       const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();           \
       if (threadIdx.x == 0) { (c).trace[2 * (k)] = t0; (c).trace[2 * (k) + 1] = t1; } \
+    }                                                                           \
+    if ((c).trace && (k) == 0 && threadIdx.x == 0 && blockIdx.x < kTraceWG)     \
+      (c).trace[32 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();       \
+    if ((c).trace && (k) == 9 && blockIdx.x < kTraceWG) {                       \
+      __builtin_amdgcn_s_waitcnt(0);                                            \
+      const unsigned long long te = __builtin_amdgcn_s_memrealtime();           \
+      if ((threadIdx.x & 63) == 0) atomicMax(&(c).trace[33 + 2 * blockIdx.x], te); \
     }                                                                           \
   } while (0)
 #else

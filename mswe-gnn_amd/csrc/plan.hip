@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/mswegnn.h"
+#include "tiling.h"
 #include "engine.h"
 
 using namespace msw;
@@ -1279,14 +1280,28 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   P->E = g->num_edges;
   // internal numbering: scale-major (graph-major inside a scale), scale starts padded to
   // multiples of 16 rows so that every 16-row wave tile lies in one scale
+  // (each graph's destinations of a scale in pack_order; MSW_TILE_PACK=0: graph order)
   P->perm.clear();
   P->sc.assign(S, ScaleCSR{});
+  const bool pack = !getenv("MSW_TILE_PACK") || atoi(getenv("MSW_TILE_PACK")) != 0;
+  std::vector<int> indeg(pack ? N : 0, 0);
+  if (pack)
+    for (int64_t e = 0; e < g->num_edges; ++e) {
+      const int64_t cl = g->edge_index[g->num_edges + e];
+      if (cl >= 0 && cl < N) ++indeg[cl];
+    }
   for (int s = 0; s < S; ++s) {
     P->sc[s].n0 = (int)P->perm.size();
     for (int gi = 0; gi < G; ++gi) {
       const int64_t a = g->node_ptr[gi * (S + 1) + s], b = g->node_ptr[gi * (S + 1) + s + 1];
       if (a < 0 || b < a || b > N) return fail(MSW_ERR_INVALID, "node_ptr out of range");
-      for (int64_t v = a; v < b; ++v) P->perm.push_back((int)v);
+      if (pack) {
+        std::vector<int> d((size_t)(b - a));
+        for (int64_t v = a; v < b; ++v) d[v - a] = indeg[v];
+        for (int k : pack_order(d)) P->perm.push_back((int)(a + k));
+      } else {
+        for (int64_t v = a; v < b; ++v) P->perm.push_back((int)v);
+      }
     }
     P->sc[s].ns = (int)P->perm.size() - P->sc[s].n0;
     P->perm.resize(round64((int)P->perm.size()), -1);

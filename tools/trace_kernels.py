@@ -27,6 +27,34 @@ PHASES = {0: "entry", 1: "tile/args", 2: "weights staged", 3: "indices", 4: "gat
           5: "edge MLP", 6: "message", 7: "segmented sum", 8: "filter", 9: "end (epilogue)"}
 
 
+def wg_report(t):
+    """Span of the launch over all workgroups (first start -> last wave's end) and where the
+    late workgroups are: start / end percentiles, in us from the first start."""
+    st = t[32::2]
+    en = t[33::2]
+    wgs = [(b, st[b], en[b]) for b in range(len(st)) if st[b] and en[b]]
+    if not wgs:
+        return
+    s0 = min(w[1] for w in wgs)
+    ends = sorted((w[2] - s0) / 100.0 for w in wgs)
+    starts = sorted((w[1] - s0) / 100.0 for w in wgs)
+    durs = sorted((w[2] - w[1]) / 100.0 for w in wgs)
+    pct = lambda v, q: v[min(len(v) - 1, int(q * len(v)))]
+    late = max(wgs, key=lambda w: w[2])
+    print(f"    {len(wgs)} workgroups: span {ends[-1]:6.2f} us; start p50/p90/max {pct(starts, .5):.2f}/"
+          f"{pct(starts, .9):.2f}/{starts[-1]:.2f}; end p10/p50/p90 {pct(ends, .1):.2f}/{pct(ends, .5):.2f}/"
+          f"{pct(ends, .9):.2f}; own duration p50/max {pct(durs, .5):.2f}/{durs[-1]:.2f}; last = wg {late[0]}")
+    nb = 8
+    n = len(st)
+    hi = max(w[0] for w in wgs) + 1
+    row = []
+    for i in range(nb):
+        grp = [w for w in wgs if i * hi // nb <= w[0] < (i + 1) * hi // nb]
+        if grp:
+            row.append(f"{i * hi // nb}-: {max((w[2] - s0) / 100.0 for w in grp):.1f}")
+    print("    latest end by workgroup range (us): " + ", ".join(row))
+
+
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "zenodo4"
     dev = torch.device("cuda:0")
@@ -36,7 +64,8 @@ def main():
     m.engine = "hip"
     plan = plan_for(m, g)
     plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, 8)
-    buf = torch.zeros(20, dtype=torch.int64, device=dev)
+    NWG = 8192  # kernels_impl.h kTraceWG: per-workgroup start / end at [32 + 2 b], [33 + 2 b]
+    buf = torch.zeros(32 + 2 * NWG, dtype=torch.int64, device=dev)
     L.check(L.lib().msw_set_trace(plan._h, C.c_void_p(buf.data_ptr())))
     S = desc["num_scales"]
     cases = [("encode", 0)] + [(k, s) for s in range(S) for k in ("edge_hop", "hop")] + \
@@ -60,6 +89,7 @@ def main():
         last = marks[-1]
         mhz = last[1] / (last[2] / 1e3) if last[2] > 0 else float("nan")
         print(f"{kern:9s} scale {scale}: {last[2] / 1e3:6.2f} us on wave 0 (~{mhz:.0f} MHz)")
+        wg_report(t)
         prev = 0.0
         for k, cyc, ns in marks[1:]:
             print(f"    {PHASES[k]:16s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
