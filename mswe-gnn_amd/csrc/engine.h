@@ -120,6 +120,7 @@ struct EncodeArgs {
   DecDesc dec;
   const float* dec_in;     // [Npad][F] decoder input rows (x_up / the GNN's last layer output)
   int decode_only;
+  int coop;                // = NT: k_encode_coop (NT waves per 16-row tile), else k_encode
 };
 
 // Edge tile: whole destination neighbourhoods, <= 16 edges and <= 16 destinations (host).

@@ -338,6 +338,10 @@ __device__ __forceinline__ void decode_tail(const f32x4 (&o)[1], const DecDesc& 
 // same operations in the same order) and state update.  Every lane of a row ends with the
 // row's new dynamic columns in nd (window shifted, prediction appended, BC of step t + 1);
 // lane group 0 writes the rollout output and the state row.  W: the decoder operands.
+template <int NT>
+__device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const DecDesc& d, const Common& c,
+                                                  const float* W, const EpiPre<NT>& pre, int n, bool valid,
+                                                  int lane, int g, float (&nd)[kMaxDyn]);
 template <int NT, int ACT>
 __device__ __forceinline__ void decode_state(const f32x4 (&x)[NT], const DecDesc& d, const Common& c,
                                              const float* W, const EpiPre<NT>& pre, int n, bool valid,
@@ -348,6 +352,13 @@ __device__ __forceinline__ void decode_state(const f32x4 (&x)[NT], const DecDesc
   for (int t = 0; t < NT; ++t) x0[t] = x[t];
   act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
   run_mlp<NT, NT, 1, ACT>(x0, o, d.dec, W, lane, g);
+  decode_state_tail<NT>(o, d, c, W, pre, n, valid, lane, g, nd);
+}
+template <int NT>
+__device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const DecDesc& d, const Common& c,
+                                                  const float* W, const EpiPre<NT>& pre, int n, bool valid,
+                                                  int lane, int g, float (&nd)[kMaxDyn]) {
+#pragma clang fp contract(off)
   // output features 0 (h) and 1 (|q|) live in lane group 0: every lane of the row takes them
   float h = __shfl(o[0].x, lane & 15), v = __shfl(o[0].y, lane & 15);
   if (d.resw_off >= 0) {
@@ -1319,6 +1330,153 @@ static const void* edge_coop_kernel(int prelu, int last) {
   return nullptr;
 }
 
+// ---------------------------------------------------------------------------- cooperative encoder
+// k_encode with P waves per 16-row tile, for meshes whose row tiles leave most SIMDs idle
+// (zenodo4: 864 row tiles, 1,024 SIMDs -- one wave per tile puts the whole chain of decoder,
+// encoders, projection 0 and unpool V on one wave): every MFMA layer's output tiles are split
+// over the ranks (rank r: tiles [r T/P, (r+1) T/P)) and exchanged through LDS, a layer with
+// fewer output tiles than ranks (the decoder's last) runs on every rank.  Every output element
+// is the same MFMA chain in the same k order as in k_encode: bit-identical results.
+// Exchange buffers alternate with a running count, so a buffer is rewritten only two
+// barriers after its last read, also across MLPs.
+template <int IN0, int T, int TL, int ACT, int P, int XW>
+__device__ __forceinline__ void enc_coop_mlp(const f32x4 (&in)[IN0], f32x4 (&out)[TL], const MlpDev& m,
+                                             const float* __restrict__ W, int lane, int g, int j, int r,
+                                             float* buf, int& xc) {
+  static_assert(T % P == 0, "hidden tiles split evenly over the ranks");
+  auto last = [&](const auto& h) {
+    constexpr int TI = sizeof(h) / sizeof(f32x4);
+    if constexpr (TL % P == 0) {
+      f32x4 o[TL / P];
+      mfma_layer_sub<TI, TL / P, ACT>(h, o, m.l[m.n - 1], W, r * (TL / P), lane, g);
+      coop_exchange<TL, P>(o, out, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+    } else {
+      mfma_layer<TI, TL, ACT>(h, out, m.l[m.n - 1], W, lane, g);
+    }
+  };
+  if (m.n == 1) {
+    last(in);
+    return;
+  }
+  f32x4 h[T];
+  {
+    f32x4 o[T / P];
+    mfma_layer_sub<IN0, T / P, ACT>(in, o, m.l[0], W, r * (T / P), lane, g);
+    coop_exchange<T, P>(o, h, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+  }
+  for (int li = 1; li + 1 < m.n; ++li) {
+    f32x4 o[T / P];
+    mfma_layer_sub<T, T / P, ACT>(h, o, m.l[li], W, r * (T / P), lane, g);
+    coop_exchange<T, P>(o, h, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+  }
+  last(h);
+}
+template <int NT, int ACT, bool DEC, int P>
+__global__ __launch_bounds__(kBlock) void k_encode_coop(EncodeArgs a) {
+  constexpr int F = 16 * NT, T2 = 2 * NT, G = kWaves / P;
+  constexpr int XW = 16 * T2 + 4;
+  __shared__ __attribute__((aligned(16))) float xbuf[G][2][kRowsPerWave][XW];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int grp = w / P, r = w % P;
+  MSW_MARK(a.c, 0);
+  Common c = a.c;
+  const int dstep = DEC ? a.dec.io->step : -1;
+  if (!a.dec.on && a.io && blockIdx.x == 0 && threadIdx.x == 0) a.io->step += 1;
+  // one chunk of G row tiles per workgroup (scale starts are 64-aligned: one scale)
+  const int rb = blockIdx.x * (G * kRowsPerWave);
+  int s = 0;
+  while (s + 1 < a.S && rb >= a.n0[s + 1]) ++s;
+  const int n = rb + grp * kRowsPerWave + j;
+  const bool valid = (n - a.n0[s]) < a.ns[s];
+  const int ext = a.c.perm ? a.c.perm[n] : n;
+  const int xrow = a.x_internal ? (valid ? n : a.n0[s]) : (valid ? ext : 0);
+  const float* xr = a.x + (size_t)xrow * a.c.nnf;
+  const int nstat = a.c.nstat_raw;
+  float raw[4], dyn[4];
+  float wlv;
+  EpiPre<NT> pre;
+  f32x4 xu[NT];
+  if (DEC && dstep >= 0) {
+    load_row<NT>(xu, a.dec_in + (size_t)n * F, g);
+    pre.ext = ext;
+    pre.step = dstep;
+    pre.bc = a.dec.bc_slot[n];
+#pragma unroll
+    for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[nstat + k] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = 4 * g + q;
+    raw[q] = f < nstat ? xr[f] : 0.f;
+    dyn[q] = f < a.c.dyn ? xr[nstat + f] : 0.f;
+  }
+  wlv = xr[nstat - 1] + xr[a.c.nnf - 2];
+  MSW_MARK(c, 1);
+  if constexpr (kStaged<NT>) {
+    stage_glds(smem, a.c.W, a.sreg[s], 0, a.sreg[s].len);
+    __syncthreads();
+  }
+  const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
+  float* buf = &xbuf[grp][0][0][0];
+  int xc = 0;
+  if (DEC && dstep >= 0) {
+#pragma clang fp contract(off)
+    float nd[kMaxDyn];
+    {
+      f32x4 x0[NT], o[1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x0[t] = xu[t];
+      act_tiles<-1, NT>(x0, a.dec.pre_act, a.dec.pre_slope);
+      enc_coop_mlp<NT, NT, 1, ACT, P, XW>(x0, o, a.dec.dec, Wl, lane, g, j, r, buf, xc);
+      decode_state_tail<NT>(o, a.dec, c, Wl, pre, n, valid && r == 0, lane, g, nd);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 4 * g + q;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < kMaxDyn; ++k) v = (k == f && f < c.dyn) ? nd[k] : v;
+      dyn[q] = v;
+    }
+    float hn = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxDyn; ++k) hn = (k == c.dyn - 2) ? nd[k] : hn;
+    wlv = xr[nstat - 1] + hn;
+  }
+  if (DEC && a.decode_only) return;
+  MSW_MARK(c, 2);
+  f32x4 xs[NT];
+  {
+    f32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = (c.with_wl && 4 * g + q == nstat) ? wlv : raw[q];
+    const f32x4 in[1] = {v};
+    enc_coop_mlp<1, NT, NT, ACT, P, XW>(in, xs, a.stat, Wl, lane, g, j, r, buf, xc);
+    if (valid && r == 0) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
+  }
+  MSW_MARK(c, 5);
+  if (s == 0) {
+    f32x4 xd[NT];
+    const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
+    enc_coop_mlp<1, NT, NT, ACT, P, XW>(in, xd, a.dynm, Wl, lane, g, j, r, buf, xc);
+    if (valid && r == P - 1 && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
+    MSW_MARK(c, 6);
+    if (a.np0.h1t == T2)
+      np_project_coop<NT, T2, P>(xs, xd, a.np0, Wl, n, valid, r, lane, g);
+    else
+      np_project_coop<NT, NT, P>(xs, xd, a.np0, Wl, n, valid, r, lane, g);
+  }
+  MSW_MARK(c, 8);
+  if (a.vu_a[s] >= 0) {
+    if (a.vu_h1t == T2)
+      proj_store_part<NT, T2 / P>(xs, Wl + a.vu_a[s], r, a.Vu, n, T2, valid, lane, g);
+    else
+      proj_store_part<NT, NT / P>(xs, Wl + a.vu_a[s], r, a.Vu, n, NT, valid, lane, g);
+  }
+  MSW_MARK(c, 9);
+}
+
 // ---------------------------------------------------------------------------- hop
 // Hops 2..K (gnn.py:406-443) over the same tiles:
 //   active(e) = rowsum(out[src]) != 0 || rowsum(out[dst]) != 0          (gnn.py:408-411)
@@ -2063,6 +2221,13 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
   }
+  if constexpr (NT >= 2) {  // cooperative encoders
+    for (const void* f : {(const void*)k_encode_coop<NT, 1, false, NT>, (const void*)k_encode_coop<NT, -1, false, NT>,
+                          (const void*)k_encode_coop<NT, 1, true, NT>, (const void*)k_encode_coop<NT, -1, true, NT>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
+      if (e != hipSuccess) return e;
+    }
+  }
   if constexpr (NT >= 2) {  // cooperative last hops (F = 32, 64)
     for (int prelu = 0; prelu < 2; ++prelu) {
       hipError_t e = hipFuncSetAttribute(hop_coop_kernel<NT>(prelu), hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
@@ -2102,6 +2267,24 @@ hipError_t prepare_kernels() {
 template <int NT>
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   if (a.Npad <= 0) return hipSuccess;
+  if constexpr (NT >= 2) {
+    if (a.coop == NT) {  // P = NT waves per row tile (F = 32: 2, F = 64: 4)
+      constexpr int P = NT;
+      const dim3 grid(a.Npad / ((kWaves / P) * kRowsPerWave)), block(kBlock);
+      const size_t sh = lds_bytes<NT>(a.lds_floats);
+      if (a.dec.on) {
+        if (a.c.prelu)
+          hipLaunchKernelGGL((k_encode_coop<NT, 1, true, P>), grid, block, sh, st, a);
+        else
+          hipLaunchKernelGGL((k_encode_coop<NT, -1, true, P>), grid, block, sh, st, a);
+      } else if (a.c.prelu) {
+        hipLaunchKernelGGL((k_encode_coop<NT, 1, false, P>), grid, block, sh, st, a);
+      } else {
+        hipLaunchKernelGGL((k_encode_coop<NT, -1, false, P>), grid, block, sh, st, a);
+      }
+      return hipGetLastError();
+    }
+  }
   const int n = a.Npad / kRowsPerBlock;
   const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.lds_floats);

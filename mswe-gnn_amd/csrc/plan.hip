@@ -982,15 +982,23 @@ void caps(msw_plan* P, A& a, int kind, int prelu, int last, int floats) {
 // A/B measurements: MSW_NO_LOOP=eh,hop,epi,all keeps those launches one tile per wave at
 // any size (no grid-stride loop).
 constexpr int kHopLoopTiles = 65536;
+constexpr long kEncCoopWaves = 4096;
 bool no_loop(const char* kind) {
   const char* e = getenv("MSW_NO_LOOP");
   return e && (strstr(e, kind) || strstr(e, "all"));
 }
 void set_grid_cap(msw_plan* P, Launch& L) {
   switch (L.kind) {
-    case L_ENCODE:
+    case L_ENCODE: {
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
+      // F = 64: four waves per row tile while that leaves <= 4 waves per SIMD (k_encode_coop;
+      // zenodo4_f64 +5.0 %; at F = 32 the halved chains are too short for the seven LDS
+      // exchanges: -2.5 %; MSW_ENC_COOP=0/1 overrides)
+      bool coop = P->NT == 4 && (long)(L.enc.Npad / kRowsPerWave) * P->NT <= kEncCoopWaves;
+      if (const char* ec = getenv("MSW_ENC_COOP")) coop = P->NT >= 2 && atoi(ec) != 0;
+      L.enc.coop = coop ? P->NT : 0;
       break;
+    }
     case L_EDGE_MLP:
       L.eh.max_blocks = resident_of(P->NT, 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;

@@ -522,3 +522,25 @@ def test_split_edge_mlp_matches_fused(cuda, F, monkeypatch):
     ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), ga)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
     assert per_step_rel(outs["1"][3][:ga.num_nodes], ref) <= REL_TOL
+
+
+@pytest.mark.parametrize("F", [32, 64])
+def test_coop_encoder_matches_single_wave(cuda, F, monkeypatch):
+    """k_encode_coop (F / 16 waves per 16-row tile, every MFMA layer's output tiles split over
+    them; the F = 64 default while that leaves <= 4 waves per SIMD) == k_encode (MSW_ENC_COOP=0), bit
+    for bit: forward (encoders, projection 0, unpool V) and rollout (the previous step's
+    decoder in the encoder launch, the final decode-only launch); and vs the oracle."""
+    g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=7)
+    outs = {}
+    for sv in ("0", "1"):
+        monkeypatch.setenv("MSW_ENC_COOP", sv)
+        m = _hip(build_msgnn(4, F, 4), cuda)
+        gd = g.to(cuda)
+        with torch.no_grad():
+            y = m(gd).cpu()
+        outs[sv] = (y, m.rollout(gd).cpu())
+    assert torch.equal(outs["0"][0], outs["1"][0])
+    assert torch.equal(outs["0"][1], outs["1"][1])
+    m = build_msgnn(4, F, 4)
+    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), g)
+    assert per_step_rel(outs["1"][1], ref) <= REL_TOL
