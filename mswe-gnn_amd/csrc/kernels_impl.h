@@ -250,7 +250,20 @@ struct EpiPre {
   float xd[kMaxDyn];  // X[row, nstat : nnf] (lane group 0 uses it)
   int ext, step;
   int bc;             // the row's BC slot (rollout mode), -1 = none
+  float bcv[kMaxDyn / 2];  // deferred decoder: the row's BC values of step + 1 (bc_prefetch)
 };
+// Deferred decoder (k_encode): the BC values the state update writes, loaded with the tile's
+// other inputs instead of after the decoder chain (a BC row's wave would otherwise wait for
+// one more global load on the launch's critical path).
+template <int NT>
+__device__ __forceinline__ void bc_prefetch(EpiPre<NT>& p, const DecDesc& d, const Common& c) {
+  const RolloutIO* io = d.io;
+  const bool on = p.bc >= 0 && p.step + 1 < io->bc_tstride;
+  const float* bp = on ? io->bc + (size_t)p.bc * c.p * io->bc_tstride + p.step + 1 : c.zrow;
+  const int ts = on ? io->bc_tstride : 0;
+#pragma unroll
+  for (int u = 0; u < kMaxDyn / 2; ++u) p.bcv[u] = u < c.p ? bp[u * ts] : 0.f;
+}
 template <int NT>
 __device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, const Common& c,
                                              const float* xs_rows, size_t n, int g) {
@@ -389,8 +402,10 @@ __device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const Dec
   for (int k = 0; k < kMaxDyn; ++k) {
     float val = k + 2 < c.dyn ? pre.xd[k + 2] : (k == c.dyn - 2 ? hm : (k == c.dyn - 1 ? vm : 0.f));
     const int tau = (k - c0) >> 1;
-    if (bc_on && k >= c0 && ((k - c0) & 1) == 0 && tau < c.p)
-      val = io->bc[((size_t)b * c.p + tau) * io->bc_tstride + t + 1];
+    float bv = 0.f;  // pre.bcv[tau] by selects (a run-time register index would use scratch)
+#pragma unroll
+    for (int u = 0; u < kMaxDyn / 2; ++u) bv = u == tau ? pre.bcv[u] : bv;
+    if (bc_on && k >= c0 && ((k - c0) & 1) == 0 && tau < c.p) val = bv;
     nd[k] = val;
   }
   if (!valid || g || pre.ext < 0) return;
@@ -516,6 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
       pre.ext = ext;
       pre.step = dstep;
       pre.bc = a.dec.bc_slot[n];
+      bc_prefetch<NT>(pre, a.dec, c);
 #pragma unroll
       for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[nstat + k] : 0.f;
     }
@@ -1402,6 +1418,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_coop(EncodeArgs a) {
     pre.ext = ext;
     pre.step = dstep;
     pre.bc = a.dec.bc_slot[n];
+    bc_prefetch<NT>(pre, a.dec, c);
 #pragma unroll
     for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[nstat + k] : 0.f;
   }
