@@ -88,6 +88,8 @@ struct Common {
   int prelu;               // every MLP activation is PReLU (compile-time activation path)
   const float* zrow;       // kZeroRow zeros: the address of a load a flag switches off
   unsigned long long* trace;  // diagnostic builds (-DMSW_TRACE): per-phase timestamps of wave 0
+  int xcd_max;             // XCD packing of small grids: at most this many XCDs (0 = off)
+  int xcd;                 // set by the launcher: this launch runs on XCDs 0 .. xcd-1 (0 = all)
 };
 
 // Encoder.  Scale ranges start at multiples of 64 rows, so a workgroup has one scale.

@@ -73,6 +73,17 @@ __device__ __forceinline__ float row_sum(float v) {
 }
 
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// XCD packing (Common::xcd = k > 0, small one-round grids): the launch has 8x the workgroups
+// it needs and only those the dispatcher places on XCDs 0 .. k-1 (workgroup i -> XCD i % 8)
+// work.  The XCDs start a launch's workgroups up to ~1.3 us apart, most of a small hop's
+// span; on k XCDs the skew is k XCDs' instead of eight.  Logical workgroup, -1 = idle.
+constexpr int kXcds = 8, kCusPerXcd = 32;
+__device__ __forceinline__ int logical_block(const Common& c) {
+  const int b = blockIdx.x;
+  if (c.xcd <= 0) return b;
+  const int x = b % kXcds;
+  return x < c.xcd ? (b / kXcds) * c.xcd + x : -1;
+}
 __device__ __forceinline__ int wave_row0() { return (blockIdx.x * kWaves + wave_id()) * kRowsPerWave; }
 
 // activation_functions, models/models.py:149-169
@@ -871,7 +882,9 @@ void k_edge_hop(EdgeHopArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int stride = gridDim.x * WV;
-  int tile = blockIdx.x * WV + w;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  int tile = xb * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
@@ -1103,7 +1116,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int grp = w / P, r = w % P;
-  const int tile = blockIdx.x * G + grp;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  const int tile = xb * G + grp;
   const bool live = tile < a.ntiles;
   Common c = a.c;
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
@@ -1234,7 +1249,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   __shared__ __attribute__((aligned(16))) float xbuf[2][kRowsPerWave][XW];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, r = wave_id();
-  const int tile = blockIdx.x;
+  const int tile = logical_block(a.c);
+  if (tile < 0) return;
   Common c = a.c;  // c.W stays the blob: the epilogue reads it there
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   // this rank's filter row (out tile r): wr[ti] = W_1 block (r, ti)
@@ -1531,7 +1547,9 @@ __global__ __launch_bounds__((64 * hop_waves<NT, LOOP>())) void k_hop(HopArgs a)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int stride = gridDim.x * WV;
-  int tile = blockIdx.x * WV + w;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  int tile = xb * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   f32x4 wf[NT][NT];
@@ -1692,7 +1710,9 @@ __global__ __launch_bounds__(kBlock) void k_hop_coop(HopArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int grp = w / P, r = w % P;
-  const int tile = blockIdx.x * G + grp;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  const int tile = xb * G + grp;
   const bool live = tile < a.ntiles;
   Common c = a.c;
   // this rank's filter rows (out tiles r TS .. r TS + TS - 1), by address
@@ -1959,7 +1979,9 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_pool(PoolArgs a
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int stride = gridDim.x * WV;
-  int tile = blockIdx.x * WV + w;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  int tile = xb * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   struct Rows {
@@ -2044,7 +2066,9 @@ __global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
   __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  int tile = blockIdx.x * (kWaves / P) + w / P;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  int tile = xb * (kWaves / P) + w / P;
   const int rk = w % P;
   Common c = a.c;
   MSW_MARK(c, 0);
@@ -2103,7 +2127,9 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_epi(EpiArgs a) 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int stride = gridDim.x * WV;
-  int tile = blockIdx.x * WV + w;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  int tile = xb * WV + w;
   Common c = a.c;
   MSW_MARK(c, 0);
   struct Rows {
@@ -2318,6 +2344,19 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// XCD packing of a one-round grid of g workgroups (b: the launch's argument copy): the
+// fewest XCDs (1, 2, 4 <= c.xcd_max) that hold one workgroup per CU, else all eight
+template <class A>
+static inline dim3 xcd_grid(A& b, long g) {
+  b.c.xcd = 0;
+  for (int k = 1; k <= b.c.xcd_max && k < kXcds; k *= 2)
+    if (g <= (long)kCusPerXcd * k) {
+      b.c.xcd = k;
+      return dim3((unsigned)(cdiv(g, k) * kXcds));
+    }
+  return dim3((unsigned)g);
+}
+
 // one tile per wave while that grid is resident at once; grid-stride loop beyond that
 template <class A>
 static inline bool tile_loop(const A& a) {
@@ -2354,29 +2393,42 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
     const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last);
     if (!f) return hipErrorInvalidValue;
-    void* args[] = {const_cast<EdgeHopArgs*>(&a)};
-    return hipLaunchKernel(f, dim3(cdiv((long)a.ntiles * a.coop, kWaves)), dim3(kBlock), args,
-                           eh_lds_bytes(a.reg_nf), st);
+    EdgeHopArgs b = a;
+    const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
+    void* args[] = {&b};
+    return hipLaunchKernel(f, grid, dim3(kBlock), args, eh_lds_bytes(a.reg_nf), st);
   }
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)),
-      block(64 * (loop ? (a.last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves));
+  EdgeHopArgs b = a;
+  const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
+  if (loop) b.c.xcd = 0;
+  const dim3 block(64 * (loop ? (a.last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves));
   const size_t sh = eh_lds_bytes(loop ? a.reg.len : a.reg_nf);
-  void* args[] = {const_cast<EdgeHopArgs*>(&a)};
+  void* args[] = {&b};
   return hipLaunchKernel(edge_hop_kernel<NT>(a.c.prelu, loop, a.last), grid, block, args, sh, st);
 }
+template <int NT>
+hipError_t launch_hop_kernel(const HopArgs& a, bool loop, dim3 grid, dim3 block, hipStream_t st);
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.coop > 1 && a.last) {  // waves per tile = NT (2 for F = 32, 4 for F = 64)
     const void* f = hop_coop_kernel<NT>(a.c.prelu);
     if (!f) return hipErrorInvalidValue;
-    void* args[] = {const_cast<HopArgs*>(&a)};
-    return hipLaunchKernel(f, dim3(cdiv((long)a.ntiles * a.coop, kWaves)), dim3(kBlock), args,
-                           lds_bytes<NT>(a.reg.len), st);
+    HopArgs b = a;
+    const dim3 grid = xcd_grid(b, cdiv((long)a.ntiles * a.coop, kWaves));
+    void* args[] = {&b};
+    return hipLaunchKernel(f, grid, dim3(kBlock), args, lds_bytes<NT>(a.reg.len), st);
   }
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)), block(64 * (loop ? hop_waves<NT, true>() : kWaves));
+  HopArgs b = a;
+  const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
+  if (loop) b.c.xcd = 0;
+  const dim3 block(64 * (loop ? hop_waves<NT, true>() : kWaves));
+  return launch_hop_kernel<NT>(b, loop, grid, block, st);
+}
+template <int NT>
+hipError_t launch_hop_kernel(const HopArgs& a, bool loop, dim3 grid, dim3 block, hipStream_t st) {
   if (!a.last) {
     if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_hop<NT, 1, false, false>), grid, block, 0, st, a);
@@ -2397,21 +2449,25 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (!a.rows) {
+    PoolArgs b = a;
     if constexpr (NT >= 2) {  // waves per tile: 2 (F = 32), 4 (F = 64)
       if (a.coop == NT) {
-        hipLaunchKernelGGL((k_pool_edge<NT, NT>), dim3(cdiv((long)a.ntiles * NT, kWaves)), dim3(kBlock), sh, st, a);
+        hipLaunchKernelGGL((k_pool_edge<NT, NT>), xcd_grid(b, cdiv((long)a.ntiles * NT, kWaves)), dim3(kBlock), sh, st, b);
         return hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((k_pool_edge<NT>), dim3(cdiv(a.ntiles, kWaves)), dim3(kBlock), sh, st, a);
+    hipLaunchKernelGGL((k_pool_edge<NT>), xcd_grid(b, cdiv(a.ntiles, kWaves)), dim3(kBlock), sh, st, b);
     return hipGetLastError();
   }
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  PoolArgs b = a;
+  const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
+  if (loop) b.c.xcd = 0;
+  const dim3 block(64 * (loop ? waves_of<NT, true>() : kWaves));
   if (loop)
-    hipLaunchKernelGGL((k_pool<NT, true>), grid, block, sh, st, a);
+    hipLaunchKernelGGL((k_pool<NT, true>), grid, block, sh, st, b);
   else
-    hipLaunchKernelGGL((k_pool<NT, false>), grid, block, sh, st, a);
+    hipLaunchKernelGGL((k_pool<NT, false>), grid, block, sh, st, b);
   return hipGetLastError();
 }
 template <int NT>
@@ -2427,14 +2483,17 @@ template <int NT>
 hipError_t launch_epi(const EpiArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const bool loop = tile_loop(a);
-  const dim3 grid(tile_grid(a)), block(64 * (loop ? waves_of<NT, true>() : kWaves));
+  EpiArgs b = a;
+  const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
+  if (loop) b.c.xcd = 0;
+  const dim3 block(64 * (loop ? waves_of<NT, true>() : kWaves));
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (a.c.prelu) {
-    if (loop) hipLaunchKernelGGL((k_epi<NT, 1, true>), grid, block, sh, st, a);
-    else hipLaunchKernelGGL((k_epi<NT, 1, false>), grid, block, sh, st, a);
+    if (loop) hipLaunchKernelGGL((k_epi<NT, 1, true>), grid, block, sh, st, b);
+    else hipLaunchKernelGGL((k_epi<NT, 1, false>), grid, block, sh, st, b);
   } else {
-    if (loop) hipLaunchKernelGGL((k_epi<NT, -1, true>), grid, block, sh, st, a);
-    else hipLaunchKernelGGL((k_epi<NT, -1, false>), grid, block, sh, st, a);
+    if (loop) hipLaunchKernelGGL((k_epi<NT, -1, true>), grid, block, sh, st, b);
+    else hipLaunchKernelGGL((k_epi<NT, -1, false>), grid, block, sh, st, b);
   }
   return hipGetLastError();
 }

@@ -382,6 +382,9 @@ struct msw_plan {
   // Fused edge MLP + hop with two waves per tile (k_edge_coop) when 2 x tiles <= coop_waves
   // (MSW_COOP_WAVES; 0: never).  Per launch kind: coop_w[0] edge hop, [1] last hop,
   // [2] pooling (MSW_COOP_WAVES_EH / _HOP / _POOL override the shared value).
+  // small one-round grids on at most this many XCDs (engine.h Common::xcd, MSW_XCD_MAX;
+  // 0 = all eight)
+  int xcd_max = 1;
   int coop_waves = 1024;
   int coop_w[3] = {1024, 1024, 1024};
   std::vector<void*> owned;
@@ -507,6 +510,7 @@ NpDesc np_none() {
 Common common_of(msw_plan* P) {
   Common c{};
   c.W = P->dW; c.perm = P->perm_d; c.nnf = P->nnf; c.dyn = P->dyn; c.p = P->p; c.zrow = P->zrow_d;
+  c.xcd_max = P->xcd_max;
   c.nstat_raw = P->nstat_raw; c.with_wl = P->with_wl; c.prelu = P->prelu;
   return c;
 }
@@ -988,6 +992,13 @@ bool no_loop(const char* kind) {
   return e && (strstr(e, kind) || strstr(e, "all"));
 }
 void set_grid_cap(msw_plan* P, Launch& L) {
+  {  // XCD packing per launch kind (MSW_XCD_KINDS bit mask: 1 hop, 2 last hop, 4 edge MLP,
+     // 8 pooling, 16 row epilogue)
+    static const int kinds = getenv("MSW_XCD_KINDS") ? atoi(getenv("MSW_XCD_KINDS")) : 31;
+    const int bit = L.kind == L_HOP ? (L.hop.last ? 2 : 1) : L.kind == L_EDGE_HOP ? 4 : L.kind == L_POOL ? 8
+                  : L.kind == L_EPI ? 16 : 0;
+    if (!(kinds & bit)) L.common().xcd_max = 0;
+  }
   switch (L.kind) {
     case L_ENCODE: {
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
@@ -1564,6 +1575,7 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
 
   if (const char* es = getenv("MSW_EPI_SPLIT_TILES")) P->epi_split_tiles = atoi(es);
   if (const char* gs = getenv("MSW_GRAPH_STEPS")) P->graph_steps = std::max(1, atoi(gs));
+  if (const char* xm = getenv("MSW_XCD_MAX")) P->xcd_max = std::max(0, atoi(xm));
   // F = 64: four-wave cooperative kernels on every scale whose grid stays resident
   // (zenodo4_f64 +3.3 %, profiles/r02_v1/ab_coop_f64.txt); F = 32 keeps 1024 (no gain above)
   if (P->NT == 4) P->coop_waves = 4096;
