@@ -544,3 +544,27 @@ def test_coop_encoder_matches_single_wave(cuda, F, monkeypatch):
     m = build_msgnn(4, F, 4)
     ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), g)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
+
+
+@pytest.mark.parametrize("knob", ["MSW_XCD_MAX", "MSW_TILE_PACK"])
+def test_launch_layout_knobs_are_bit_identical(cuda, knob, monkeypatch):
+    """XCD packing of small grids (MSW_XCD_MAX=0: all eight XCDs) and the degree-aware
+    destination order (MSW_TILE_PACK=0: graph order) change where rows and workgroups go,
+    never a result bit: forward, rollout and a batch of two meshes, vs the default."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import rollout_test
+    ga = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=3)
+    gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=4, T=6), seed=4)
+    outs = {}
+    for sv in ("0", None):
+        if sv is None:
+            monkeypatch.delenv(knob, raising=False)
+        else:
+            monkeypatch.setenv(knob, sv)
+        m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+        gd = ga.to(cuda)
+        with torch.no_grad():
+            y = m(gd).cpu()
+        outs[sv] = (y, m.rollout(gd).cpu(), rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
+    for a, b in zip(outs["0"], outs[None]):
+        assert torch.equal(a, b)
