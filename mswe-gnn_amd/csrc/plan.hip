@@ -1155,6 +1155,7 @@ int final_decode(msw_plan* P, hipStream_t st) {
     return MSW_OK;
   Launch L = P->sched_roll[0];
   L.enc.decode_only = 1;
+  if (getenv("MSW_TRACE_ENCODE")) L.enc.c.trace = nullptr;  // keep the last step's encoder marks
   switch (P->NT) {
     case 1: HIP_TRY(launch_one<1>(L, st)); break;
     case 2: HIP_TRY(launch_one<2>(L, st)); break;
@@ -2025,8 +2026,12 @@ int msw_debug_buffer(msw_plan* P, const char* name, float* dst, void* stream) {
 
 int msw_set_trace(msw_plan* P, uint64_t* buf) {
   if (!P) return fail(MSW_ERR_INVALID, "null plan");
+  // MSW_TRACE_ENCODE: the encoder launches only (a rollout then leaves the marks of its last
+  // step's encoder: the deferred decoder + encoders, tools/trace_kernels.py)
+  const bool enc_only = getenv("MSW_TRACE_ENCODE") != nullptr;
   for (auto* q : {&P->sched_fwd, &P->sched_roll})
-    for (Launch& L : *q) L.common().trace = reinterpret_cast<unsigned long long*>(buf);
+    for (Launch& L : *q)
+      L.common().trace = (!enc_only || L.kind == L_ENCODE) ? reinterpret_cast<unsigned long long*>(buf) : nullptr;
   P->drop_graphs();  // the captured steps hold the old arguments
   return MSW_OK;
 }

@@ -94,6 +94,22 @@ def main():
         for k, cyc, ns in marks[1:]:
             print(f"    {PHASES[k]:16s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
             prev = ns
+    if os.environ.get("MSW_TRACE_ENCODE"):  # rollout-mode encoder (deferred decoder first)
+        L.check(L.lib().msw_set_trace(plan._h, C.c_void_p(buf.data_ptr())))
+        buf.zero_()
+        plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, 3)
+        torch.cuda.synchronize()
+        t = buf.cpu().tolist()
+        clk0, rt0 = t[0], t[1]
+        marks = [(k, t[2 * k] - clk0, (t[2 * k + 1] - rt0) * 10.0) for k in range(10) if t[2 * k] != 0]
+        print(f"encode (rollout step 2, decoder of step 1 first): {marks[-1][2] / 1e3:6.2f} us on wave 0")
+        wg_report(t)
+        prev = 0.0
+        names = dict(PHASES, **{2: "weights + decoder", 5: "static encoder", 6: "dynamic encoder",
+                                8: "projection 0", 9: "unpool V (end)"})
+        for k, cyc, ns in marks[1:]:
+            print(f"    {names[k]:18s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
+            prev = ns
     # the finest scale's last hop + decoder epilogue: the last launch of a rollout step, so a
     # one-step rollout leaves its marks in the buffer (marks it does not set are skipped)
     buf.zero_()
