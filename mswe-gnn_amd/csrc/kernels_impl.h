@@ -1403,9 +1403,12 @@ __device__ __forceinline__ void enc_coop_mlp(const f32x4 (&in)[IN0], f32x4 (&out
   }
   last(h);
 }
-template <int NT, int ACT, bool DEC, int P>
-__global__ __launch_bounds__(kBlock) void k_encode_coop(EncodeArgs a) {
-  constexpr int F = 16 * NT, T2 = 2 * NT, G = kWaves / P;
+// Workgroup: WV waves = WV / P row tiles (F = 32: eight waves, the four row tiles of k_encode's
+// workgroup, so the weight region is staged as often as there; F = 64 reads the blob).
+template <int NT> constexpr int enc_coop_waves() { return NT == 2 ? 8 : kWaves; }
+template <int NT, int ACT, bool DEC, int P, int WV = enc_coop_waves<NT>()>
+__global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
+  constexpr int F = 16 * NT, T2 = 2 * NT, G = WV / P;
   constexpr int XW = 16 * T2 + 4;
   __shared__ __attribute__((aligned(16))) float xbuf[G][2][kRowsPerWave][XW];
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1447,7 +1450,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_coop(EncodeArgs a) {
   wlv = xr[nstat - 1] + xr[a.c.nnf - 2];
   MSW_MARK(c, 1);
   if constexpr (kStaged<NT>) {
-    stage_glds(smem, a.c.W, a.sreg[s], 0, a.sreg[s].len);
+    stage_glds<WV>(smem, a.c.W, a.sreg[s], 0, a.sreg[s].len);
     __syncthreads();
   }
   const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
@@ -2267,7 +2270,7 @@ hipError_t prepare_kernels() {
   if constexpr (NT >= 2) {  // cooperative encoders
     for (const void* f : {(const void*)k_encode_coop<NT, 1, false, NT>, (const void*)k_encode_coop<NT, -1, false, NT>,
                           (const void*)k_encode_coop<NT, 1, true, NT>, (const void*)k_encode_coop<NT, -1, true, NT>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx(enc_coop_waves<NT>()));
       if (e != hipSuccess) return e;
     }
   }
@@ -2312,8 +2315,8 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   if (a.Npad <= 0) return hipSuccess;
   if constexpr (NT >= 2) {
     if (a.coop == NT) {  // P = NT waves per row tile (F = 32: 2, F = 64: 4)
-      constexpr int P = NT;
-      const dim3 grid(a.Npad / ((kWaves / P) * kRowsPerWave)), block(kBlock);
+      constexpr int P = NT, WV = enc_coop_waves<NT>();
+      const dim3 grid(a.Npad / ((WV / P) * kRowsPerWave)), block(64 * WV);
       const size_t sh = lds_bytes<NT>(a.lds_floats);
       if (a.dec.on) {
         if (a.c.prelu)

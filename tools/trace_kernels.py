@@ -105,8 +105,8 @@ def main():
         print(f"encode (rollout step 2, decoder of step 1 first): {marks[-1][2] / 1e3:6.2f} us on wave 0")
         wg_report(t)
         prev = 0.0
-        names = dict(PHASES, **{2: "weights + decoder", 5: "static encoder", 6: "dynamic encoder",
-                                8: "projection 0", 9: "unpool V (end)"})
+        names = {**PHASES, 2: "weights + decoder", 5: "static encoder", 6: "dynamic encoder",
+                 8: "projection 0", 9: "unpool V (end)"}
         for k, cyc, ns in marks[1:]:
             print(f"    {names[k]:18s} +{(ns - prev) / 1e3:6.2f} us  (at {ns / 1e3:6.2f} us, {cyc} clk)")
             prev = ns
