@@ -537,12 +537,13 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     float wlv;
     EpiPre<NT> pre;
     f32x4 xu[NT];
-    if (DEC && dstep >= 0) {  // the decoder's inputs, loaded before the weight staging
+    // the decoder's inputs, loaded before the weight staging and whatever the step (at step
+    // 0 nothing reads them): not behind the load of the step counter, whose dependent loads
+    // (the BC values) are issued after the staging barrier, in flight during the decoder MLP
+    if (DEC) {
       load_row<NT>(xu, a.dec_in + (size_t)n * F, g);
       pre.ext = ext;
-      pre.step = dstep;
       pre.bc = a.dec.bc_slot[n];
-      bc_prefetch<NT>(pre, a.dec, c);
 #pragma unroll
       for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[nstat + k] : 0.f;
     }
@@ -566,6 +567,8 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     // prove to be LDS across the loop: it emitted flat loads, which wait on vmcnt too)
     const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
     if (DEC && dstep >= 0) {  // decode the previous step; the encoders read the updated state
+      pre.step = dstep;
+      bc_prefetch<NT>(pre, a.dec, c);
       float nd[kMaxDyn];
       decode_state<NT, ACT>(xu, a.dec, c, Wl, pre, n, valid, lane, g, nd);
 #pragma unroll
@@ -1432,12 +1435,10 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
   float wlv;
   EpiPre<NT> pre;
   f32x4 xu[NT];
-  if (DEC && dstep >= 0) {
+  if (DEC) {  // as k_encode: not behind the step counter
     load_row<NT>(xu, a.dec_in + (size_t)n * F, g);
     pre.ext = ext;
-    pre.step = dstep;
     pre.bc = a.dec.bc_slot[n];
-    bc_prefetch<NT>(pre, a.dec, c);
 #pragma unroll
     for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[nstat + k] : 0.f;
   }
@@ -1458,6 +1459,8 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
   int xc = 0;
   if (DEC && dstep >= 0) {
 #pragma clang fp contract(off)
+    pre.step = dstep;
+    bc_prefetch<NT>(pre, a.dec, c);
     float nd[kMaxDyn];
     {
       f32x4 x0[NT], o[1];
