@@ -53,6 +53,14 @@ def wg_report(t):
         if grp:
             row.append(f"{i * hi // nb}-: {max((w[2] - s0) / 100.0 for w in grp):.1f}")
     print("    latest end by workgroup range (us): " + ", ".join(row))
+    if len(wgs) >= 64:  # by XCD (workgroup i -> XCD i % 8): median start, latest end
+        per = []
+        for x in range(8):
+            grp = [w for w in wgs if w[0] % 8 == x]
+            if grp:
+                ss = sorted((w[1] - s0) / 100.0 for w in grp)
+                per.append(f"{x}: {ss[len(ss) // 2]:.2f}/{max((w[2] - s0) / 100.0 for w in grp):.2f}")
+        print("    by XCD (median start / latest end, us): " + ", ".join(per))
 
 
 def main():
