@@ -207,6 +207,7 @@ struct HopArgs {
   int last;
   Epilogue epi;
   int coop;          // last hop: waves per tile (k_hop_coop), 0 = one
+  int split;         // middle hop: features split over two waves per tile (k_hop_split)
 };
 
 // Hop chain: M = 2 or 3 consecutive hops (k .. k+M-1) in one launch, the last of them

@@ -1646,6 +1646,118 @@ __global__ __launch_bounds__((64 * hop_waves<NT, LOOP>())) void k_hop(HopArgs a)
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- feature-split middle hop
+// A middle hop (no epilogue) with each edge tile's features split over two waves: rank r
+// gathers, messages and sums features [F r / 2, F (r + 1) / 2) only (half the loads per wave,
+// twice the waves in flight), the two ranks exchange through LDS what crosses the split --
+// the per-lane partial row sums of the activity predicate (recombined in k_hop's order,
+// ((h0 + h1) + h2) + h3, on both ranks) and the aggregated messages (the filter's B operand:
+// rank r computes output tiles [NT r / 2, NT (r + 1) / 2) over all input tiles in k_hop's k
+// order).  Bit-identical to k_hop.
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_hop_split(HopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, TH = NT / 2, G = kWaves / 2;
+  constexpr int XS = 16 * TH + 4;
+  __shared__ __attribute__((aligned(16))) float slab_all[G][2][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float hx[G][2][2 * TH][64];  // partial row sums
+  __shared__ __attribute__((aligned(16))) f32x4 ax[G][NT][64];          // aggregated messages
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int grp = w / 2, r = w % 2, t0 = r * TH;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  const int tile = xb * G + grp;
+  const bool live = tile < a.ntiles;  // dead groups compute tile 0 and store nothing
+  MSW_MARK(a.c, 0);
+  const Lanes L = lanes_of(load_rec(a.recs, live ? tile : 0, j), live ? tile : 0, j, a.n0);
+  f32x4 os[TH], sv[TH], inn[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    const int off = 16 * (t0 + t) + 4 * g;
+    os[t] = ld4(a.in + L.sr * F + off);
+    sv[t] = ld4(a.s + L.p * F + off);
+    inn[t] = ld4(a.in + L.n * F + off);
+  }
+  f32x4 wf[TH][NT];  // this rank's output tiles of the filter
+  {
+    const int fa = a.filt_a >= 0 ? a.filt_a : 0;
+#pragma unroll
+    for (int to = 0; to < TH; ++to)
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti) wf[to][ti] = ld4(a.c.W + fa + ((size_t)((t0 + to) * NT + ti) * 64 + lane) * 4);
+  }
+  float* slab = &slab_all[grp][r][0][0];
+  float* my = slab + j * XS;
+#pragma unroll
+  for (int t = 0; t < TH; ++t) st4(my + 16 * t + 4 * g, inn[t]);
+  wave_lds_sync();
+  f32x4 od[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) od[t] = ld4(slab + L.dl * XS + 16 * t + 4 * g);
+  // activity predicate (put_message): per-lane partial sums of both ranks, combined in t order
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    hx[grp][r][t][lane] = hsum(os[t]);
+    hx[grp][r][TH + t][lane] = hsum(od[t]);
+  }
+  __syncthreads();
+  float rs = 0.f, rd = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      rs += hx[grp][q][t][lane];
+      rd += hx[grp][q][TH + t][lane];
+    }
+  const bool act = (row_sum(rs) != 0.f) || (row_sum(rd) != 0.f);  // gnn.py:408-411
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    f32x4 gv;
+    if (a.grad) {
+      gv = od[t] - os[t];
+      if (a.upwind) {
+        gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
+        gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
+      }
+    } else {
+      gv = os[t];
+    }
+    const f32x4 m = gv * sv[t];
+    st4(my + 16 * t + 4 * g, (L.ev && act) ? m : zero4());
+  }
+  f32x4 agg[TH];
+  gather_messages<TH, XS>(agg, slab, L.q0, L.q1, g);
+#pragma unroll
+  for (int t = 0; t < TH; ++t) ax[grp][t0 + t][lane] = agg[t];
+  __syncthreads();
+  f32x4 res[TH];
+#pragma unroll
+  for (int t = 0; t < TH; ++t) res[t] = inn[t];
+  if (a.filt_a >= 0) {
+    f32x4 full[NT], acc[TH];
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) full[ti] = ax[grp][ti][lane];
+#pragma unroll
+    for (int to = 0; to < TH; ++to) acc[to] = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int to = 0; to < TH; ++to) acc[to] = MSW_MFMA(wf[to][ti][q], full[ti][q], acc[to]);
+#pragma unroll
+    for (int t = 0; t < TH; ++t) res[t] = res[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < TH; ++t) res[t] = res[t] + agg[t];
+  }
+  if (live && L.nv) {
+#pragma unroll
+    for (int t = 0; t < TH; ++t) st4(a.out + L.n * F + 16 * (t0 + t) + 4 * g, res[t]);
+  }
+  MSW_MARK(a.c, 9);
+}
+
 // ---------------------------------------------------------------------------- cooperative last hop
 // A layer's last hop + its epilogue with P waves per tile (small scales, as k_edge_coop):
 // every rank does the hop's VALU / LDS work; the filter, the projections (next layer U/V/O,
@@ -2425,6 +2537,13 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
     const dim3 grid = xcd_grid(b, cdiv((long)a.ntiles * a.coop, kWaves));
     void* args[] = {&b};
     return hipLaunchKernel(f, grid, dim3(kBlock), args, lds_bytes<NT>(a.reg.len), st);
+  }
+  if constexpr (NT >= 2) {
+    if (a.split && !a.last) {  // feature-split middle hop: two waves per tile
+      HopArgs b = a;
+      hipLaunchKernelGGL((k_hop_split<NT>), xcd_grid(b, cdiv((long)a.ntiles * 2, kWaves)), dim3(kBlock), 0, st, b);
+      return hipGetLastError();
+    }
   }
   const bool loop = tile_loop(a);
   HopArgs b = a;

@@ -1038,6 +1038,12 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
       // (profiles/r01_v7/ab_edge_waves.txt)
       if (no_loop("hop") || (!getenv("MSW_HOP_LOOP") && L.hop.ntiles < kHopLoopTiles)) L.hop.max_blocks = 0;
+      {  // F = 64: feature-split middle hops below the grid-stride size (k_hop_split;
+         // zenodo4_f64 +4.6 %, F = 32 neutral; MSW_HOP_SPLIT=0/1 overrides the rule)
+        bool sp = P->NT == 4 && L.hop.max_blocks == 0;
+        if (const char* hs = getenv("MSW_HOP_SPLIT")) sp = atoi(hs) != 0;
+        L.hop.split = (sp && P->NT >= 2 && !L.hop.last) ? 1 : 0;
+      }
       {  // a last hop with an epilogue on few tiles: P = F / 16 waves per tile (k_hop_coop)
         HopArgs& h = L.hop;
         const bool loop = h.fit_blocks > 0 && h.max_blocks > 0 && (h.ntiles + kWaves - 1) / kWaves > h.fit_blocks;

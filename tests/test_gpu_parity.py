@@ -568,3 +568,27 @@ def test_launch_layout_knobs_are_bit_identical(cuda, knob, monkeypatch):
         outs[sv] = (y, m.rollout(gd).cpu(), rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
     for a, b in zip(outs["0"], outs[None]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("F", [32, 64])
+def test_feature_split_hop_matches_k_hop(cuda, F, monkeypatch):
+    """k_hop_split (a middle hop's features split over two waves per tile, predicate partial
+    sums and aggregated messages exchanged through LDS) == k_hop (MSW_HOP_SPLIT=0), bit for
+    bit: forward, rollout, a batch of two meshes; and the oracle's rollout."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import rollout_test
+    ga = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=8)
+    gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=9, T=6), seed=9)
+    outs = {}
+    for sv in ("0", "1"):
+        monkeypatch.setenv("MSW_HOP_SPLIT", sv)
+        m = _hip(build_msgnn(4, F, 4), cuda)
+        gd = ga.to(cuda)
+        with torch.no_grad():
+            y = m(gd).cpu()
+        outs[sv] = (y, m.rollout(gd).cpu(), rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b)
+    m = build_msgnn(4, F, 4)
+    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), ga)
+    assert per_step_rel(outs["1"][1], ref) <= REL_TOL
