@@ -1242,26 +1242,36 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
 // F = 64 (NT = 4): the whole workgroup (4 waves) on one tile, one slab shared by the four
 // ranks (rank 0 writes the node rows and the messages) so that the 96 KB edge-MLP region
 // still fits beside it; the epilogue's operands stay in the blob (F = 64 relocation).
-template <int ACT, int LST>
+// P = 2: two tiles per workgroup, two waves each (a slab and exchange buffers per tile);
+// P = 4: the whole workgroup on one tile.
+template <int ACT, int LST, int P = 4>
 __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma clang fp contract(off)
-  constexpr int NT = 4, P = 4, F = 16 * NT, T2 = 2 * NT;
+  constexpr int NT = 4, F = 16 * NT, T2 = 2 * NT, G = kWaves / P, TS = NT / P;
   constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
   constexpr int XW = 16 * T2 + 4;
-  __shared__ __attribute__((aligned(16))) float slab[kRowsPerWave][XS];
-  __shared__ __attribute__((aligned(16))) float xbuf[2][kRowsPerWave][XW];
+  __shared__ __attribute__((aligned(16))) float slab_g[G][kRowsPerWave][XS];
+  __shared__ __attribute__((aligned(16))) float xbuf_g[G][2][kRowsPerWave][XW];
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, r = wave_id();
-  const int tile = logical_block(a.c);
-  if (tile < 0) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int grp = w / P, r = w % P;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  const int tile0 = xb * G + grp;
+  const bool live = tile0 < a.ntiles;  // dead groups compute tile 0 and store nothing
+  const int tile = live ? tile0 : 0;
+  float (&slab)[kRowsPerWave][XS] = slab_g[grp];
+  float (&xbuf)[2][kRowsPerWave][XW] = xbuf_g[grp];
   Common c = a.c;  // c.W stays the blob: the epilogue reads it there
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
-  // this rank's filter row (out tile r): wr[ti] = W_1 block (r, ti)
-  f32x4 wr[NT];
+  // this rank's filter rows (out tiles r TS .. r TS + TS - 1): wr[t][ti] = W_1 block (r TS + t, ti)
+  f32x4 wr[TS][NT];
   {
     const int fa = a.filt_a >= 0 ? a.filt_a : 0;
 #pragma unroll
-    for (int ti = 0; ti < NT; ++ti) wr[ti] = ld4(c.W + fa + ((size_t)(r * NT + ti) * 64 + lane) * 4);
+    for (int t = 0; t < TS; ++t)
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti) wr[t][ti] = ld4(c.W + fa + ((size_t)((r * TS + t) * NT + ti) * 64 + lane) * 4);
   }
   EdgeHopRows<NT> q;
   edge_hop_load<NT, LST>(q, a, tile, j, g);
@@ -1313,7 +1323,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
       sv[t] = v;
     }
   }
-  if (r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
+  if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
   // every rank has read the slab's node rows before the first MLP exchange barrier: rank 0
   // may overwrite them with the messages (a.rest.n == 0 has no barrier: add one)
   if (a.rest.n == 0) __syncthreads();
@@ -1323,42 +1333,58 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   gather_messages<NT, XS>(agg, &slab[0][0], L.q0, L.q1, g);
   // this rank's tile of inn / agg / skip by address (a 4-way select over a register array
   // was turned back into a scratch-indexed load): inn sits past the messages in the slab row
-  f32x4 rs[1];
-  rs[0] = ld4(&slab[j][16 * T2 + 16 * r + 4 * g]);
+  f32x4 rs[TS];
+#pragma unroll
+  for (int t = 0; t < TS; ++t) rs[t] = ld4(&slab[j][16 * T2 + 16 * (r * TS + t) + 4 * g]);
   if (a.filt_a >= 0) {
-    f32x4 acc = zero4();
+    f32x4 acc[TS];
+#pragma unroll
+    for (int t = 0; t < TS; ++t) acc[t] = zero4();
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc = MSW_MFMA(wr[ti][rr], agg[ti][rr], acc);
-    rs[0] = rs[0] + acc;
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int t = 0; t < TS; ++t) acc[t] = MSW_MFMA(wr[t][ti][rr], agg[ti][rr], acc[t]);
+#pragma unroll
+    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
   } else {
-    f32x4 ag = zero4();
-    for (int qq = L.q0; qq < L.q1; ++qq) ag = ag + ld4(&slab[qq][16 * r + 4 * g]);
-    rs[0] = rs[0] + ag;
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+      f32x4 ag = zero4();
+      for (int qq = L.q0; qq < L.q1; ++qq) ag = ag + ld4(&slab[qq][16 * (r * TS + t) + 4 * g]);
+      rs[t] = rs[t] + ag;
+    }
   }
-  if (a.skip) rs[0] = rs[0] + ld4(a.skip + L.n * F + 16 * r + 4 * g);
+  if (a.skip) {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + ld4(a.skip + L.n * F + 16 * (r * TS + t) + 4 * g);
+  }
   f32x4 res[NT];
   coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? &xbuf[1][0][0] : &xbuf[0][0][0], XW, r, j, g);
   if (LST && a.last) {
     const Epilogue& e = a.epi;
     if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
-    if (r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
+    if (live && r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
     if (e.np.h1t == T2)
-      np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv, r, lane, g);
+      np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv && live, r, lane, g);
     else
-      np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv, r, lane, g);
-  } else if (r == 0 && L.nv && a.out) {
+      np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv && live, r, lane, g);
+  } else if (live && r == 0 && L.nv && a.out) {
     store_row<NT>(a.out + L.n * F, res, NT, g);
   }
 }
 
 template <int NT>
-static const void* edge_coop_kernel(int prelu, int last) {
+static const void* edge_coop_kernel(int prelu, int last, int pw = 0) {
   if constexpr (NT == 2) {  // F = 32: each MLP layer's output tiles halve (F = 16 has one)
     if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
     return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
-  } else if constexpr (NT == 4) {  // F = 64: four waves per tile
+  } else if constexpr (NT == 4) {  // F = 64: four waves per tile (pw = 2: two)
+    if (pw == 2) {
+      if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2> : (const void*)k_edge_coop4<-1, 1, 2>;
+      return prelu ? (const void*)k_edge_coop4<1, 0, 2> : (const void*)k_edge_coop4<-1, 0, 2>;
+    }
     if (last) return prelu ? (const void*)k_edge_coop4<1, 1> : (const void*)k_edge_coop4<-1, 1>;
     return prelu ? (const void*)k_edge_coop4<1, 0> : (const void*)k_edge_coop4<-1, 0>;
   }
@@ -2395,14 +2421,16 @@ hipError_t prepare_kernels() {
       if (e != hipSuccess) return e;
     }
   }
-  if constexpr (NT == 4) {  // F = 64 cooperative edge hops: one shared slab + exchange buffers
-    const int st = kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4;
-    for (int prelu = 0; prelu < 2; ++prelu)
-      for (int last = 0; last < 2; ++last) {
-        hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024 - st);
-        if (e != hipSuccess) return e;
-      }
+  if constexpr (NT == 4) {  // F = 64 cooperative edge hops: a slab + exchange buffers per tile
+    for (int pw = 2; pw <= 4; pw += 2) {
+      const int st = (kWaves / pw) * (kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4);
+      for (int prelu = 0; prelu < 2; ++prelu)
+        for (int last = 0; last < 2; ++last) {
+          hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, pw),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st);
+          if (e != hipSuccess) return e;
+        }
+    }
   }
   if constexpr (NT == 2) {  // cooperative edge hops: 160 KB minus slabs and exchange buffers
     const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
@@ -2509,7 +2537,7 @@ template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
-    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last);
+    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop);
     if (!f) return hipErrorInvalidValue;
     EdgeHopArgs b = a;
     const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
@@ -2645,6 +2673,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 5: return (const void*)k_pool_edge<NT>;
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     case 7: return edge_coop_kernel<NT>(prelu, last);
+    case 12: return edge_coop_kernel<NT>(prelu, last, 2);
     case 9: return hop_coop_kernel<NT>(prelu);
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
@@ -2656,7 +2685,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
-  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7 || kind == 10) ? eh_lds_bytes((int)(dyn_bytes / 4))
+  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7 || kind == 10 || kind == 12) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)

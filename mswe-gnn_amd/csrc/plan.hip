@@ -1029,6 +1029,14 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       const int coop_fit = pw ? resident_of(P->NT, 7, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0) : 0;
       a.coop = (pw && !loop && epi_ok && P->coop_w[0] > 0 && (long)pw * a.ntiles <= P->coop_w[0] &&
                 (pw * a.ntiles + kWaves - 1) / kWaves <= coop_fit) ? pw : 0;
+      // F = 64 where four waves per tile do not fit one round: two, two tiles per workgroup
+      // (zenodo4_f64 scale 1: 508 tiles in one round, +2.0 %; MSW_COOP2_F64=0 off, =2 also in
+      // place of four, for tests)
+      const int c2 = getenv("MSW_COOP2_F64") ? atoi(getenv("MSW_COOP2_F64")) : 1;
+      if (c2 == 2 && a.coop == 4) a.coop = 0;
+      if (P->NT == 4 && !a.coop && !loop && epi_ok && P->coop_w[0] > 0 && 2L * a.ntiles <= P->coop_w[0] && c2 &&
+          (2 * a.ntiles + kWaves - 1) / kWaves <= resident_of(P->NT, 12, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0))
+        a.coop = 2;
       break;
     }
     case L_HOP:

@@ -592,3 +592,23 @@ def test_feature_split_hop_matches_k_hop(cuda, F, monkeypatch):
     m = build_msgnn(4, F, 4)
     ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), ga)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
+
+
+def test_f64_two_wave_coop_edge_hop_matches_single_wave(cuda, monkeypatch):
+    """F = 64 cooperative edge MLP + hop with two waves per tile, two tiles per workgroup
+    (k_edge_coop4<.., P = 2>, forced by MSW_COOP2_F64=2) == one wave per tile
+    (MSW_COOP_WAVES=0), bit for bit, incl. the unpooling layers' projection epilogue and a
+    dead second tile group."""
+    g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=11).to(cuda)
+    outs = []
+    for env in ({"MSW_COOP_WAVES": "0"}, {"MSW_COOP2_F64": "2"}):
+        for k in ("MSW_COOP_WAVES", "MSW_COOP2_F64"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        m = _hip(build_msgnn(4, 64, 4), cuda)
+        with torch.no_grad():
+            y = m(g).cpu()
+        outs.append((y, m.rollout(g).cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
