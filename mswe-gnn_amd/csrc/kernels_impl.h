@@ -1104,7 +1104,11 @@ __device__ __forceinline__ void np_project_coop(const f32x4 (&xs)[NT], const f32
   }
   if (d.a_u >= 0) proj_store_part<T2, H1T / P>(in, W + d.a_u, r, d.U, n, H1T, valid, lane, g);
   if (d.a_v >= 0) proj_store_part<T2, H1T / P>(in, W + d.a_v, r, d.V, n, H1T, valid, lane, g);
-  if (d.a_o >= 0) proj_store_part<NT, NT / P>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
+  if constexpr (P <= NT) {
+    if (d.a_o >= 0) proj_store_part<NT, NT / P>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
+  } else {  // more ranks than O tiles: ranks 0..NT-1 take one O tile each
+    if (d.a_o >= 0 && r < NT) proj_store_part<NT, 1>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
+  }
 }
 
 template <int NT, int ACT, int LST, int P>
@@ -2202,17 +2206,20 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_pool(PoolArgs a
 // launch is latency-bound).
 // P = 2: two waves per tile, both summing the children, the projection's output tiles split
 // between them (as k_edge_coop; bit-identical).
-template <int NT, int P = 1>
-__global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
+// P = 2 * NT (F = 64: eight waves per tile, WV = 8): each rank projects one U and one V output
+// tile (ranks 0..NT-1 also one O tile) -- half the F = 64 projection chain of P = 4.
+template <int NT, int P = 1, int WV = kWaves>
+__global__ __launch_bounds__(64 * WV) void k_pool_edge(PoolArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
-  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
+  static_assert(WV % P == 0, "whole tiles per workgroup");
+  __shared__ __attribute__((aligned(16))) float slab_all[WV][kRowsPerWave][XS];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int xb = logical_block(a.c);
   if (xb < 0) return;
-  int tile = xb * (kWaves / P) + w / P;
+  int tile = xb * (WV / P) + w / P;
   const int rk = w % P;
   Common c = a.c;
   MSW_MARK(c, 0);
@@ -2238,10 +2245,11 @@ __global__ __launch_bounds__(kBlock) void k_pool_edge(PoolArgs a) {
     if constexpr (P == 1) {
       np_project<NT>(r.xs, acc, a.np, c.W, L.n, L.nv, lane, g);
     } else {
-      if (a.np.h1t == 2 * NT)
+      if (a.np.h1t == 2 * NT) {
         np_project_coop<NT, 2 * NT, P>(r.xs, acc, a.np, c.W, L.n, L.nv, rk, lane, g);
-      else
+      } else if constexpr (P <= NT) {  // P > NT is launched for two-layer-wide MLPs only
         np_project_coop<NT, NT, P>(r.xs, acc, a.np, c.W, L.n, L.nv, rk, lane, g);
+      }
     }
   };
   Rows r0;
@@ -2603,6 +2611,12 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (!a.rows) {
     PoolArgs b = a;
+    if constexpr (NT == 4) {  // eight waves per tile (one tile per 512-thread workgroup)
+      if (a.coop == 2 * NT) {
+        hipLaunchKernelGGL((k_pool_edge<NT, 2 * NT, 2 * NT>), xcd_grid(b, a.ntiles), dim3(64 * 2 * NT), sh, st, b);
+        return hipGetLastError();
+      }
+    }
     if constexpr (NT >= 2) {  // waves per tile: 2 (F = 32), 4 (F = 64)
       if (a.coop == NT) {
         hipLaunchKernelGGL((k_pool_edge<NT, NT>), xcd_grid(b, cdiv((long)a.ntiles * NT, kWaves)), dim3(kBlock), sh, st, b);
@@ -2671,6 +2685,9 @@ static const void* kernel_of(int kind, int prelu, int last) {
                    : (prelu ? (const void*)k_hop<NT, 1, true, LOOP> : (const void*)k_hop<NT, -1, true, LOOP>);
     case 3: return (const void*)k_pool<NT, LOOP>;
     case 5: return (const void*)k_pool_edge<NT>;
+    case 13:
+      if constexpr (NT == 4) return (const void*)k_pool_edge<NT, 2 * NT, 2 * NT>;
+      return nullptr;
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     case 7: return edge_coop_kernel<NT>(prelu, last);
     case 12: return edge_coop_kernel<NT>(prelu, last, 2);
@@ -2690,6 +2707,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
+                    : kind == 13 ? 64 * 2 * NT
                     : kind == 2 ? 64 * (loop ? hop_waves<NT, true>() : kWaves)
                     : 64 * (loop && (kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)
