@@ -2206,8 +2206,8 @@ __global__ __launch_bounds__((64 * waves_of<NT, LOOP>())) void k_pool(PoolArgs a
 // launch is latency-bound).
 // P = 2: two waves per tile, both summing the children, the projection's output tiles split
 // between them (as k_edge_coop; bit-identical).
-// P = 2 * NT (F = 64: eight waves per tile, WV = 8): each rank projects one U and one V output
-// tile (ranks 0..NT-1 also one O tile) -- half the F = 64 projection chain of P = 4.
+// P = WV = 2 * NT (F = 64: eight waves per tile): each rank projects one U and one V output
+// tile (ranks 0..NT-1 also one O tile) -- half the projection chain of P = NT.
 template <int NT, int P = 1, int WV = kWaves>
 __global__ __launch_bounds__(64 * WV) void k_pool_edge(PoolArgs a) {
 #pragma clang fp contract(off)
@@ -2256,7 +2256,7 @@ __global__ __launch_bounds__(64 * WV) void k_pool_edge(PoolArgs a) {
   load(r0, tile < a.ntiles ? tile : 0, j, g);
   MSW_MARK(c, 1);
   if constexpr (kStaged<NT>) {
-    stage_glds(smem, a.c.W, a.reg, 0, a.reg.len);
+    stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
     c.W = smem;
   }
@@ -2414,6 +2414,11 @@ hipError_t prepare_kernels() {
   }
   for (const void* f : {(const void*)k_edge_mlp<NT, 1>, (const void*)k_edge_mlp<NT, -1>}) {  // no slab
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  if constexpr (NT >= 2) {  // wide pooling (one tile per workgroup)
+    hipError_t e = hipFuncSetAttribute((const void*)k_pool_edge<NT, 2 * NT, 2 * NT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, mx(2 * NT));
     if (e != hipSuccess) return e;
   }
   if constexpr (NT >= 2) {  // cooperative encoders
@@ -2611,7 +2616,7 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   const size_t sh = lds_bytes<NT>(a.reg.len);
   if (!a.rows) {
     PoolArgs b = a;
-    if constexpr (NT == 4) {  // eight waves per tile (one tile per 512-thread workgroup)
+    if constexpr (NT >= 2) {  // 2 NT waves per tile (one tile per workgroup)
       if (a.coop == 2 * NT) {
         hipLaunchKernelGGL((k_pool_edge<NT, 2 * NT, 2 * NT>), xcd_grid(b, a.ntiles), dim3(64 * 2 * NT), sh, st, b);
         return hipGetLastError();
@@ -2686,7 +2691,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 3: return (const void*)k_pool<NT, LOOP>;
     case 5: return (const void*)k_pool_edge<NT>;
     case 13:
-      if constexpr (NT == 4) return (const void*)k_pool_edge<NT, 2 * NT, 2 * NT>;
+      if constexpr (NT >= 2) return (const void*)k_pool_edge<NT, 2 * NT, 2 * NT>;
       return nullptr;
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     case 7: return edge_coop_kernel<NT>(prelu, last);

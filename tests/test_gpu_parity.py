@@ -614,24 +614,25 @@ def test_f64_two_wave_coop_edge_hop_matches_single_wave(cuda, monkeypatch):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-def test_f64_eight_wave_pool_matches_four_wave(cuda, monkeypatch):
-    """F = 64 pooling with eight waves per tile (k_pool_edge<4, 8, 8>: one U and one V output
-    tile per rank, ranks 0..3 one O tile each; MSW_POOL_P8=1) == four waves per tile
-    (MSW_POOL_P8=0), bit for bit: forward, rollout, a batch of two meshes; and the oracle."""
+@pytest.mark.parametrize("F", [32, 64])
+def test_wide_pool_matches_default(cuda, F, monkeypatch):
+    """Pooling with 2F/16 waves per tile (k_pool_edge<NT, 2NT, 2NT>: one U and one V output
+    tile per rank, ranks 0..NT-1 one O tile each; MSW_POOL_WIDE=1) == F/16 waves per tile
+    (MSW_POOL_WIDE=0), bit for bit: forward, rollout, a batch of two meshes; and the oracle."""
     from mswegnn.batch import collate
     from mswegnn.rollout import rollout_test
     ga = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=12)
     gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=13, T=6), seed=13)
     outs = {}
     for sv in ("0", "1"):
-        monkeypatch.setenv("MSW_POOL_P8", sv)
-        m = _hip(build_msgnn(4, 64, 4), cuda)
+        monkeypatch.setenv("MSW_POOL_WIDE", sv)
+        m = _hip(build_msgnn(4, F, 4), cuda)
         gd = ga.to(cuda)
         with torch.no_grad():
             y = m(gd).cpu()
         outs[sv] = (y, m.rollout(gd).cpu(), rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
     for a, b in zip(outs["0"], outs["1"]):
         assert torch.equal(a, b)
-    m = build_msgnn(4, 64, 4)
-    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=64, K=4), ga)
+    m = build_msgnn(4, F, 4)
+    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), ga)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
