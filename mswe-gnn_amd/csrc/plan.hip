@@ -1086,10 +1086,10 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       a.coop = (!a.rows && pw && P->coop_w[2] > 0 && (long)pw * a.etiles <= P->coop_w[2] &&
                 (pw * a.etiles + kWaves - 1) / kWaves <= fe) ? pw : 0;
       // 2F-wide first edge-MLP layer: 2 * F / 16 waves per tile (one U and one V output tile
-      // each) while resident.  MSW_POOL_WIDE unset: F = 64 only (zenodo4_f64 +1.8 %);
-      // 0 / 1 forces it off / on; bit-identical either way
+      // each) while resident (zenodo4_f64 +1.8 %, zenodo4 +0.6 %, profiles/r02_s4/ab_pool_p8.txt,
+      // ab_pool_wide_f32.txt); MSW_POOL_WIDE=0: F / 16 waves; bit-identical either way
       const char* pw2 = getenv("MSW_POOL_WIDE");
-      const bool wide = pw2 ? atoi(pw2) != 0 : P->NT == 4;
+      const bool wide = pw2 ? atoi(pw2) != 0 : true;
       if (wide && pw && a.coop == pw && a.np.h1t == 2 * pw) {
         const int f8 = resident_of(P->NT, 13, 0, 0, (size_t)a.reg.len * 4, 0);
         if (f8 > 0 && a.etiles <= f8) a.coop = 2 * pw;
