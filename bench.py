@@ -66,18 +66,30 @@ WORKLOADS = {
 }
 
 
+def sim_mesh_kwargs(name, seed):
+    """make_multiscale_mesh keywords of simulation `seed` of a workload."""
+    from mswegnn.mesh import mesh_config, config3_members
+    w = WORKLOADS[name]
+    if w["mesh"] == "config3":
+        return config3_members(w["S"], count=seed + 1)[seed]
+    if w["mesh"] == "tiny_mixed":
+        return dict(n_coarse=2 + seed % 2, num_scales=4, seed=seed)
+    return dict(mesh_config(w["mesh"]), seed=seed)
+
+
+def sim_fine_nodes(name, seed):
+    """Fine-scale nodes of simulation `seed` without building it: the generator's coarse
+    n x n x 2 triangles refined 1 -> 4 (S - 1) times, plus the ghost cell (mswegnn/mesh.py)."""
+    kw = sim_mesh_kwargs(name, seed)
+    return 2 * kw["n_coarse"] ** 2 * 4 ** (kw["num_scales"] - 1) + 1
+
+
 def build_workload(name, seed, T):
     """Simulation `seed` of a workload -> (graph, model, workload row, description)."""
     from models.gnn import MSGNN
-    from mswegnn.mesh import make_multiscale_mesh, mesh_config, config3_members
+    from mswegnn.mesh import make_multiscale_mesh
     w = WORKLOADS[name]
-    if w["mesh"] == "config3":
-        kw = config3_members(w["S"], count=seed + 1)[seed]
-    elif w["mesh"] == "tiny_mixed":
-        kw = dict(n_coarse=2 + seed % 2, num_scales=4, seed=seed)
-    else:
-        kw = dict(mesh_config(w["mesh"]), seed=seed)
-    g = make_multiscale_mesh(**kw, T=T)
+    g = make_multiscale_mesh(**sim_mesh_kwargs(name, seed), T=T)
     if name == "hbm1m":
         from mswegnn.mesh import wet_state
         g = wet_state(g, seed=seed, all_wet=True)
@@ -143,23 +155,44 @@ def read_traffic(path, kernel_prefix):
         return None
 
 
-def simulations_of_rank(args, rank, world):
+def lpt_split(sizes, world):
+    """Longest-processing-time assignment of simulations (work ~ fine nodes) to `world`
+    ranks: largest first, each to the least-loaded rank (lowest rank on ties).  Returns the
+    ascending simulation ids of every rank."""
+    load = [0] * world
+    own = [[] for _ in range(world)]
+    for i in sorted(range(len(sizes)), key=lambda i: (-sizes[i], i)):
+        r = min(range(world), key=lambda q: (load[q], q))
+        load[r] += sizes[i]
+        own[r].append(i)
+    return [sorted(o) for o in own]
+
+
+def simulations_of_rank(args, rank, world, workload=None):
     """Simulation ids this rank runs.  --global-batch G: a FIXED set of G simulations split
-    round-robin over the ranks, {i : i mod W = r} (strong scaling).  Otherwise
-    --batch B per rank, ids r*B .. r*B+B-1 (weak scaling)."""
+    over the ranks by size (lpt_split on fine nodes; SURVEY §8(e), strong scaling).
+    Otherwise --batch B per rank, ids r*B .. r*B+B-1 (weak scaling)."""
     if args.global_batch:
         if args.global_batch < world:
             raise SystemExit(f"--global-batch {args.global_batch} < {world} ranks")
-        return [i for i in range(args.global_batch) if i % world == rank], "strong"
+        wl = workload or getattr(args, "workload", "zenodo4")
+        sizes = [sim_fine_nodes(wl, i) for i in range(args.global_batch)]
+        return lpt_split(sizes, world)[rank], "strong"
     B = max(1, args.batch)
     return [rank * B + i for i in range(B)], "weak"
 
 
-def rank_batch(workload, ids, T):
+def rank_batch(workload, ids, T, cache=None):
     """This rank's simulations as ONE graph: the single simulation, or a disjoint-union batch
     in the reference's layout (PyG collation + adapt_batch_training / update_batch_multiscale,
-    train.py:14-65).  -> (sims, graph, fine_rows or None, fine nodes per rollout)."""
-    sims = [build_workload(workload, seed=i, T=T) for i in ids]
+    train.py:14-65).  -> (sims, graph, fine_rows or None, fine nodes per rollout).
+    cache: optional dict id -> build_workload result, reused across calls."""
+    if cache is None:
+        cache = {}
+    for i in ids:
+        if i not in cache:
+            cache[i] = build_workload(workload, seed=i, T=T)
+    sims = [cache[i] for i in ids]
     fine = sum(s[3]["fine_nodes"] for s in sims)
     if len(sims) == 1:
         return sims, sims[0][0], None, fine
@@ -169,6 +202,159 @@ def rank_batch(workload, ids, T):
     npt = gb.node_ptr
     rows = torch.cat([torch.arange(int(npt[i, 0]), int(npt[i, 1])) for i in range(len(sims))])
     return sims, gb, rows, fine
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def make_runner(workload, ids, T, dev, engine, cache):
+    """One rank's share as ONE batch on `dev` -> (run() -> [N, 2, T], fine_of(out) -> this
+    share's fine-scale rows [sum n0, 2, T] in id order, fine nodes, close()).
+    engine 'hip': a dedicated EnginePlan (msw_rollout); 'torch': the drop-in's torch path
+    (CPU tests of the multi-rank logic)."""
+    sims, gb, rows, fine = rank_batch(workload, ids, T, cache)
+    g = gb.to(dev)
+    m = sims[0][1].to(dev)
+    m.engine = engine
+    if engine == "hip":
+        from mswegnn.engine import EnginePlan
+        plan = EnginePlan(m, g, dev)
+        out = torch.empty(g.num_nodes, 2, T, device=dev)
+
+        def run():
+            return plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T, out=out)
+
+        close = plan.close
+    else:
+        def run():
+            return m.rollout(g, T)
+
+        def close():
+            pass
+    fr = rows.to(dev) if rows is not None else None
+
+    def fine_of(r):
+        return r[:fine] if fr is None else r.index_select(0, fr)
+    return run, fine_of, fine, close
+
+
+def strong_scaling_section(dist, rank, world, dev, engine, sets, T, steps, warmup, barrier,
+                           workload="config3"):
+    """The north star's strong scaling, measured in-run (BASELINE config 3):
+    for each fixed set of G simulations, rank 0 first runs the WHOLE set alone as one batch
+    (t1) while the other ranks wait; then every rank runs its share (lpt_split by fine nodes,
+    one batch per rank) and each rollout ends with the real all-gather of the fine-scale
+    rollouts over the default process group (RCCL on nccl) -- tW = max over ranks.  Rank 0
+    also checks that the gathered rollouts equal its single-GPU ones.  Returns the record
+    (complete on rank 0)."""
+    red_dev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    cache = {}
+    rec = {"workload": workload, "rollout_steps": T, "timed_rollouts": steps, "warmup": warmup,
+           "rccl_world": dist.get_world_size(), "backend": dist.get_backend(),
+           "split": "longest-processing-time by fine nodes (bench.lpt_split)", "sets": []}
+    for G in sets:
+        if G < world:
+            rec["sets"].append({"G": G, "skipped": f"fewer simulations than the {world} ranks"})
+            continue
+        sizes = [sim_fine_nodes(workload, i) for i in range(G)]
+        split = lpt_split(sizes, world)
+        ent = {"G": G, "sims_per_rank": [len(s) for s in split],
+               "fine_nodes_per_rank": [sum(sizes[i] for i in s) for s in split],
+               "fine_nodes_total": sum(sizes)}
+        # ---- phase A: the whole set on rank 0 alone
+        ref = None
+        if rank == 0:
+            run, fine_of, _, close = make_runner(workload, list(range(G)), T, dev, engine, cache)
+            for _ in range(warmup):
+                run()
+            _sync(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                r = run()
+            _sync(dev)
+            t1 = (time.perf_counter() - t0) / steps
+            ref = fine_of(r).cpu()
+            close()
+            ent["t1_ms"] = t1 * 1e3
+        barrier()
+        # ---- phase B: every rank its share + the end-of-rollout all-gather
+        run, fine_of, fine, close = make_runner(workload, split[rank], T, dev, engine, cache)
+        gather = make_gatherer(dist, world, fine, T, red_dev)
+
+        def step():
+            return gather(fine_of(run()).contiguous())
+        parts = None
+        for _ in range(warmup):
+            parts = step()
+        _sync(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            parts = step()
+        _sync(dev)
+        dist.barrier()
+        tw_local = (time.perf_counter() - t0) / steps
+        tt = torch.tensor([tw_local], device=red_dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tw = float(tt.item())
+        tl = [torch.zeros(1, device=red_dev, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(tl, torch.tensor([tw_local], device=red_dev, dtype=torch.float64))
+        close()
+        if rank == 0:
+            start = [0]
+            for n in sizes:
+                start.append(start[-1] + n)
+            worst = 0.0
+            den = max(float(ref.abs().max()), 1e-30)
+            for q in range(world):
+                slot, o = parts[q].cpu(), 0
+                for i in split[q]:
+                    n = sizes[i]
+                    worst = max(worst, float((slot[o:o + n] - ref[start[i]:start[i] + n]).abs().max()) / den)
+                    o += n
+            t1 = ent["t1_ms"] / 1e3
+            ent.update({"tW_ms": tw * 1e3, "rank_ms": [float(x.item()) * 1e3 for x in tl],
+                        "speedup": t1 / tw,
+                        "fine_node_steps_per_s_1gpu": sum(sizes) * T / t1,
+                        "fine_node_steps_per_s_Wgpu": sum(sizes) * T / tw,
+                        "gathered_vs_single_gpu_max_rel": worst})
+        rec["sets"].append(ent)
+    return rec
+
+
+def partitioned_rollout_check(rank, world, barrier, timeout=300):
+    """Single-mesh domain decomposition over RCCL: rank 0 runs
+    tools/rccl_partition_check.py (two fresh processes on GPUs 0 and 1, DistributedRollout
+    with the RCCL halo exchange, gather_owned over RCCL, compared with the undivided plan) as
+    a child with a time limit -- recorded, never fatal, and a hang cannot stall the bench."""
+    res = None
+    if rank == 0:
+        import signal
+        import subprocess
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "rccl_partition_check.py"), "2", "--mesh", "zenodo4"]
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                            "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+        try:
+            # own session: on a time-out the checker AND its rank processes are killed
+            p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                                 start_new_session=True)
+            try:
+                so, se = p.communicate(timeout=timeout)
+                lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+                res = json.loads(lines[-1]) if lines else {"error": "no result line", "stderr_tail": se[-800:]}
+                res["exit_code"] = p.returncode
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                res = {"error": f"timed out after {timeout} s"}
+        except Exception as e:  # noqa: BLE001
+            res = {"error": repr(e)}
+    barrier()
+    return res
 
 
 def _built_from_sources():
@@ -198,6 +384,12 @@ def main():
     ap.add_argument("--caller", default="fused", choices=["fused", "reference-loop"],
                     help="fused: rollout_test as ONE msw_rollout; reference-loop: the reference's "
                          "own rollout_test loop (train.py:87-95), one HIP msw_forward per step")
+    ap.add_argument("--strong-sets", default="8,128",
+                    help="N > 1: fixed config-3 sets (G simulations each) of the strong_scaling "
+                         "record; '' = none")
+    ap.add_argument("--strong-steps", type=int, default=3)
+    ap.add_argument("--no-partition-check", action="store_true",
+                    help="N > 1: skip the RCCL single-mesh decomposition check")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,6 +400,7 @@ def main():
     # on a one-GPU box (ranks share the device; RCCL refuses two ranks on one device)
     backend = os.environ.get("MSW_DIST_BACKEND", "nccl")
     gpu = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+    cpu_group = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
@@ -215,11 +408,13 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
+        # host-side barrier for long waits (rank 0 alone on the GPU): no spinning collective
+        cpu_group = dist.new_group(backend="gloo")
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     T = args.T
-    ids, scaling = simulations_of_rank(args, rank, world)
+    ids, scaling = simulations_of_rank(args, rank, world, args.workload)
     B = len(ids)
     sims, gb, fine_rows, fine_rank = rank_batch(args.workload, ids, T)
     g_cpu, model_cpu, w, desc = sims[0]
@@ -289,6 +484,23 @@ def main():
         dist.all_reduce(tn, op=dist.ReduceOp.SUM)
         nodes_all = float(tn.item())
     value = nodes_all * T * args.steps / dt
+
+    strong = part_check = None
+    if world > 1:
+        # the north star's strong scaling (fixed config-3 sets, rank 0 alone vs all ranks with
+        # the RCCL all-gather) and the RCCL single-mesh decomposition: after the weak line's
+        # timed region, recorded, never fatal
+        def cpu_barrier():
+            dist.barrier(group=cpu_group)
+        sets = [int(s) for s in args.strong_sets.split(",") if s.strip()]
+        if sets:
+            try:
+                strong = strong_scaling_section(dist, rank, world, dev, "hip", sets, T, args.strong_steps,
+                                                1, cpu_barrier)
+            except Exception as e:  # noqa: BLE001
+                strong = {"error": repr(e)}
+        if not args.no_partition_check and backend == "nccl" and torch.cuda.device_count() >= 2:
+            part_check = partitioned_rollout_check(rank, world, cpu_barrier)
 
     result = None
     if rank == 0:
@@ -448,8 +660,14 @@ def main():
             "all_node_steps_per_s": value * desc.get("batch_nodes", desc["all_nodes"]) / fine_rank,
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "engine": {"kernels_per_step": st["kernels_per_step"], "graph_captured": st["graph_captured"],
-                       "device_bytes": st["device_bytes"]},
+                       "device_bytes": st["device_bytes"],
+                       "device_bytes_note": "plan-owned: graph tables, weights, per-node buffers and the "
+                                            "edge-encoder inputs / outputs kept for the per-rollout "
+                                            "recompute of the edge terms"},
         }
+        if world > 1:
+            result["strong_scaling"] = strong
+            result["partitioned_rollout_rccl"] = part_check
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -191,7 +191,11 @@ int msw_group_rollout(msw_plan* const* plans, int32_t num_plans, const float* co
                       int32_t T, float* const* out, void* stream);
 
 /* One forward (MSGNN.forward / GNN.forward): x [N][num_node_features] -> y [N][2].
- * Does not modify x.  Equivalent to models/gnn.py:267-350 (MSGNN) or :102-152 (GNN). */
+ * Does not modify x.  Equivalent to models/gnn.py:267-350 (MSGNN) or :102-152 (GNN).
+ * With graph capture on (the default), the first call captures the forward schedule into a
+ * hipGraph over plan-owned I/O slots; every call then enqueues copy x -> slot, one graph
+ * launch, copy slot -> y (the reference's per-step rollout loop, train.py:87-95, calls this
+ * once per step). */
 int msw_forward(msw_plan* plan, const float* x, float* y, void* stream);
 
 /* Autoregressive rollout (rollout_test, training/train.py:67-95 with
@@ -208,7 +212,8 @@ int msw_rollout(msw_plan* plan, const float* x0, const float* bc, int32_t bc_tim
  * into dst (device, [N][F], graph numbering).  Debug / parity localisation only. */
 int msw_debug_buffer(msw_plan* plan, const char* name, float* dst, void* stream);
 
-/* Enable (1) / disable (0) capturing one rollout step into a hipGraph (default 1). */
+/* Enable (1) / disable (0) graph capture of rollout steps and of msw_forward (default 1;
+ * 0 = every launch enqueued eagerly). */
 int msw_set_graph_capture(msw_plan* plan, int enable);
 
 int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);

@@ -375,6 +375,12 @@ struct msw_plan {
   hipStream_t cap_stream = nullptr;
   hipGraphExec_t step_exec = nullptr;   // one rollout step
   hipGraphExec_t multi_exec = nullptr;  // graph_steps consecutive steps (one graph launch)
+  // Forward mode (msw_forward, the reference's own rollout loop calls it once per step): the
+  // forward schedule captured once with fixed device I/O slots; a call copies x into fwd_x,
+  // replays the graph and copies fwd_y out -- three stream operations instead of ~35 eager
+  // launches (host-launch-bound at ~3.5 us each).
+  hipGraphExec_t fwd_exec = nullptr;
+  float *fwd_x = nullptr, *fwd_y = nullptr;
   // Steps per graph launch: consecutive launches of one graph leave a ~8.5 us gap on the
   // device (measured, rocprofv3 step breakdown), inside a graph the steps run back to back.
   // MSW_GRAPH_STEPS overrides (1: one graph launch per step).
@@ -391,7 +397,8 @@ struct msw_plan {
   void drop_graphs() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
     if (multi_exec) (void)hipGraphExecDestroy(multi_exec);
-    step_exec = multi_exec = nullptr;
+    if (fwd_exec) (void)hipGraphExecDestroy(fwd_exec);
+    step_exec = multi_exec = fwd_exec = nullptr;
   }
   ~msw_plan() {
     drop_graphs();
@@ -1820,6 +1827,28 @@ int rollout_prologue(msw_plan* P, const float* x0, const float* bc, int32_t bc_t
   return MSW_OK;
 }
 
+// Capture what `enqueue(stream)` launches on the plan's capture stream into `*exec`.
+template <class Fn>
+int capture_graph(msw_plan* P, hipGraphExec_t* exec, Fn enqueue) {
+  if (!P->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&P->cap_stream, hipStreamNonBlocking));
+  hipGraph_t graph = nullptr;
+  HIP_TRY(hipStreamBeginCapture(P->cap_stream, hipStreamCaptureModeThreadLocal));
+  const int rc = enqueue(P->cap_stream);
+  const hipError_t ce = hipStreamEndCapture(P->cap_stream, &graph);
+  if (rc) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  if (ce != hipSuccess) return fail(MSW_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+  const hipError_t ie = hipGraphInstantiate(exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ie != hipSuccess) {
+    *exec = nullptr;
+    return fail(MSW_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+  }
+  return MSW_OK;
+}
+
 // In-process transport (msw_group_rollout): halo rows of plan k's buffer gathered straight
 // from the owning plans' buffers, using each owner's send list for k.
 int loopback_exchange(msw_plan* const* plans, int k, const ExchangeArgs& a, hipStream_t st) {
@@ -1959,9 +1988,28 @@ int msw_plan_destroy(msw_plan* plan) {
 int msw_forward(msw_plan* P, const float* x, float* y, void* stream) {
   if (!P || !x || !y) return fail(MSW_ERR_INVALID, "null argument");
   HIP_TRY(hipSetDevice(P->device));
-  patch_forward(P->sched_fwd, x, y);
-  int rc = schedule_dispatch(P, P->sched_fwd, (hipStream_t)stream);
-  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (P->use_graph) {
+    // the schedule reads fwd_x and writes fwd_y (graph numbering, like x and y)
+    const size_t xb = (size_t)P->N * P->nnf * sizeof(float), yb = (size_t)P->N * 2 * sizeof(float);
+    if (!P->fwd_exec) {
+      if (!P->fwd_x) {
+        int rc = palloc(P, &P->fwd_x, (size_t)P->N * P->nnf);
+        if (!rc) rc = palloc(P, &P->fwd_y, (size_t)P->N * 2);
+        if (rc) return rc;
+      }
+      patch_forward(P->sched_fwd, P->fwd_x, P->fwd_y);
+      int rc = capture_graph(P, &P->fwd_exec, [&](hipStream_t cs) { return schedule_dispatch(P, P->sched_fwd, cs); });
+      if (rc) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(P->fwd_x, x, xb, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipGraphLaunch(P->fwd_exec, st));
+    HIP_TRY(hipMemcpyAsync(y, P->fwd_y, yb, hipMemcpyDeviceToDevice, st));
+  } else {
+    patch_forward(P->sched_fwd, x, y);
+    int rc = schedule_dispatch(P, P->sched_fwd, st);
+    if (rc) return rc;
+  }
   P->forward_calls++;
   return MSW_OK;
 }
@@ -1984,21 +2032,11 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
   if (P->use_graph) {
     // capture `steps` consecutive rollout steps into one executable graph
     auto capture = [&](hipGraphExec_t* exec, int steps) -> int {
-      if (!P->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&P->cap_stream, hipStreamNonBlocking));
-      hipGraph_t graph = nullptr;
-      HIP_TRY(hipStreamBeginCapture(P->cap_stream, hipStreamCaptureModeThreadLocal));
-      int rc = MSW_OK;
-      for (int k = 0; k < steps && !rc; ++k) rc = schedule_dispatch(P, P->sched_roll, P->cap_stream);
-      hipError_t ce = hipStreamEndCapture(P->cap_stream, &graph);
-      if (rc) return rc;
-      if (ce != hipSuccess) return fail(MSW_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
-      hipError_t ie = hipGraphInstantiate(exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      if (ie != hipSuccess) {
-        *exec = nullptr;
-        return fail(MSW_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
-      }
-      return MSW_OK;
+      return capture_graph(P, exec, [&](hipStream_t cs) {
+        int rc = MSW_OK;
+        for (int k = 0; k < steps && !rc; ++k) rc = schedule_dispatch(P, P->sched_roll, cs);
+        return rc;
+      });
     };
     const int G = std::max(1, P->graph_steps);
     int rc;
@@ -2070,7 +2108,7 @@ int msw_plan_get_stats(const msw_plan* P, msw_plan_stats* s) {
   s->forward_calls = P->forward_calls;
   s->rollout_steps = P->rollout_steps;
   s->device_bytes = P->dev_bytes;
-  s->graph_captured = P->step_exec != nullptr || P->multi_exec != nullptr;
+  s->graph_captured = P->step_exec != nullptr || P->multi_exec != nullptr || P->fwd_exec != nullptr;
   return MSW_OK;
 }
 

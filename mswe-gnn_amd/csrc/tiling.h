@@ -17,7 +17,7 @@ constexpr int kTileEdges = 16;  // = kRowsPerWave: in-edges and destinations per
 // tile is computed on its own, so results do not depend on the order (bit-identical).
 // zenodo4's finest scale: 2,050 -> 2,046 tiles (1,927 = all tiles full).
 constexpr int kPackWindow = 64;
-std::vector<int> pack_order(const std::vector<int>& deg) {
+inline std::vector<int> pack_order(const std::vector<int>& deg) {
   const int n = (int)deg.size();
   std::vector<char> used(n, 0);
   std::vector<int> out;

@@ -42,13 +42,26 @@ def _engine_wanted(model, x: Tensor) -> bool:
     if mode == "hip":
         if not x.is_cuda:
             raise RuntimeError("engine='hip' needs the graph on a GPU")
+        if _needs_grad(model, x):
+            raise RuntimeError("engine='hip' runs inference only: call under torch.no_grad() or freeze "
+                               "the parameters (training takes engine='auto' / 'torch')")
+        if _active_dropout(model):
+            raise RuntimeError("engine='hip' implements no dropout: call model.eval() first")
         return True
     if not x.is_cuda:
         return False
-    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in model.parameters())):
+    if _needs_grad(model, x):
         return False
     # the engine implements inference: no dropout
-    return not (model.training and any(isinstance(m, nn.Dropout) and m.p > 0 for m in model.modules()))
+    return not _active_dropout(model)
+
+
+def _needs_grad(model, x):
+    return torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in model.parameters()))
+
+
+def _active_dropout(model):
+    return model.training and any(isinstance(m, nn.Dropout) and m.p > 0 for m in model.modules())
 
 
 class SWEGNN(nn.Module):

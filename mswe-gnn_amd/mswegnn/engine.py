@@ -9,6 +9,7 @@ torch tensors plus the current HIP stream.
 from __future__ import annotations
 
 import ctypes as C
+import operator
 import weakref
 
 import numpy as np
@@ -18,6 +19,9 @@ import torch.nn as nn
 from . import _lib as L
 
 __all__ = ["EnginePlan", "plan_for", "describe_model"]
+
+_raw_stream = torch._C._cuda_getCurrentRawStream if hasattr(torch._C, "_cuda_getCurrentRawStream") \
+    else (lambda i: torch.cuda.current_stream(i).cuda_stream)
 
 
 # ------------------------------------------------------------------ model description
@@ -208,7 +212,8 @@ class EnginePlan:
             pass
 
     def _stream(self):
-        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the raw handle of torch's current stream on the plan's device (no Stream object)
+        return C.c_void_p(_raw_stream(self.device.index or 0))
 
     def _x(self, x):
         if x.device != self.device or x.dtype != torch.float32:
@@ -218,12 +223,18 @@ class EnginePlan:
         return x.contiguous()
 
     def forward(self, x):
-        """MSGNN.forward / GNN.forward on the GPU: x [N, nnf] -> y [N, 2]."""
+        """MSGNN.forward / GNN.forward on the GPU: x [N, nnf] -> y [N, 2].  The plan replays
+        its captured forward graph (msw_forward): two device copies + one graph launch."""
         x = self._x(x)
-        y = torch.empty(self.num_nodes, 2, device=self.device, dtype=torch.float32)
-        L.check(L.lib().msw_forward(self._h, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
-                                    self._stream()))
+        y = torch.empty((self.num_nodes, 2), device=self.device, dtype=torch.float32)
+        rc = self._fwd(self._h, x.data_ptr(), y.data_ptr(), _raw_stream(self.device.index or 0))
+        if rc:
+            L.check(rc)
         return y
+
+    @property
+    def _fwd(self):
+        return L.lib().msw_forward
 
     def rollout(self, x0, BC, node_BC, type_BC, T, out=None):
         """rollout_test on the GPU -> [N, 2, T] (training/train.py:67-95)."""
@@ -305,11 +316,18 @@ class _GraphRef:
                 and all(a is b for a, b in zip(ts, self.tensors))
                 and self.versions == tuple(t._version for t in ts))
 
+    def still_valid(self):
+        """The held tensors still hold the plan's content: none was modified in place since
+        the plan was built from them (or adopted them)."""
+        return all(t._version == v for t, v in zip(self.tensors, self.versions))
+
     def same_content(self, model, graph):
         """Equal values in other tensors (e.g. ``graph.clone()``, which the reference's
-        rollout_test makes once per rollout, train.py:80): one device compare per tensor."""
+        rollout_test makes once per rollout, train.py:80): one device compare per tensor.
+        Only meaningful while the held tensors are unmodified (``still_valid``): a held
+        tensor edited in place no longer shows the content the plan was built from."""
         ts = tuple(getattr(graph, n) for n in _TOPOLOGY[model.type_model])
-        if self.shape != (tuple(graph.x.shape), str(graph.x.device)):
+        if self.shape != (tuple(graph.x.shape), str(graph.x.device)) or not self.still_valid():
             return False
         for a, b in zip(ts, self.tensors):
             if a.shape != b.shape or a.dtype != b.dtype:
@@ -322,8 +340,42 @@ class _GraphRef:
         self.versions = tuple(t._version for t in self.tensors)
 
 
+# Parameter lists per model, cached: ``model.parameters()`` walks the module tree (~0.35 ms
+# for a 150-parameter MSGNN, more than a whole HIP forward).  Any parameter or submodule
+# registration anywhere bumps _STRUCT_GEN and invalidates every cached list.
+_STRUCT_GEN = [0]
+_param_lists = weakref.WeakKeyDictionary()
+
+
+def _bump_struct_gen(*_args):
+    _STRUCT_GEN[0] += 1
+
+
+try:
+    from torch.nn.modules import module as _tm
+    _tm.register_module_parameter_registration_hook(_bump_struct_gen)
+    _tm.register_module_module_registration_hook(_bump_struct_gen)
+    _HOOKED = True
+except AttributeError:  # older torch: no global registration hooks -> walk every call
+    _HOOKED = False
+
+
+def _params(model):
+    ent = _param_lists.get(model)
+    if not _HOOKED or ent is None or ent[0] != _STRUCT_GEN[0]:
+        ent = (_STRUCT_GEN[0], list(model.parameters()))
+        _param_lists[model] = ent
+    return ent[1]
+
+
+_ver = operator.attrgetter("_version")
+
+
 def _weights_key(model):
-    return tuple((p.data_ptr(), p._version) for p in model.parameters())
+    """(storage addresses, in-place versions) of every parameter: a plan holds a copy of the
+    weights, so a moved or modified parameter needs a new plan."""
+    ps = _params(model)
+    return tuple(map(torch.Tensor.data_ptr, ps)), tuple(map(_ver, ps))
 
 
 _plans = weakref.WeakKeyDictionary()
@@ -350,6 +402,11 @@ def plan_for(model, graph, unsupported_ok=False):
                 plan.close()
             break
     else:
+        # plans whose graph tensors were modified in place since: their content is gone
+        for ent in [e for e in entries if not e[0].still_valid()]:
+            entries.remove(ent)
+            if ent[2] is not None:
+                ent[2].close()
         for i, (ref, w, plan) in enumerate(entries):
             if w == wk and ref.same_content(model, graph):
                 ref.adopt(model, graph)

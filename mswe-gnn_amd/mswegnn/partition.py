@@ -328,6 +328,7 @@ class DistributedRollout:
         from . import _lib as L
         from .engine import EnginePlan
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.group = group
         self.device = torch.device(device or f"cuda:{torch.cuda.current_device()}")
         self.num_nodes = int(graph.x.shape[0])
         self.owner, self.parts, self.xplan = decompose(graph, self.world)
@@ -351,10 +352,30 @@ class DistributedRollout:
         return self.plan.rollout(x0, bc, nbc, type_BC, T)
 
     def gather_owned(self, out_local):
-        import torch.distributed as dist
-        outs = [None] * self.world
-        dist.all_gather_object(outs, out_local.cpu())
-        return assemble(self.parts, outs, self.num_nodes)
+        """The whole mesh's [N, ...] on every rank: ONE tensor all-gather of each rank's owned
+        rows (RCCL over xGMI on an nccl group, device tensors; host tensors on gloo), padded
+        to the largest part.  Every rank holds the decomposition, so no sizes are exchanged."""
+        return gather_parts(self.parts, self.rank, out_local, self.num_nodes, self.group)
 
     def close(self):
         self.plan.close()
+
+
+def gather_parts(parts, rank, out_local, num_nodes, group=None):
+    """All-gather of owned rows (DistributedRollout.gather_owned): rank `rank` contributes
+    out_local[owned rows of parts[rank]]; returns the assembled [num_nodes, ...]."""
+    import torch.distributed as dist
+    dev = out_local.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    counts = [int(lp.owned.sum()) for lp in parts]
+    own_rows = torch.from_numpy(np.nonzero(parts[rank].owned)[0]).to(out_local.device)
+    own = out_local.index_select(0, own_rows).to(dev)
+    tail = tuple(out_local.shape[1:])
+    buf = torch.zeros((max(counts),) + tail, dtype=out_local.dtype, device=dev)
+    buf[:counts[rank]] = own
+    slots = [torch.empty_like(buf) for _ in parts]
+    dist.all_gather(slots, buf, group=group)
+    full = torch.zeros((num_nodes,) + tail, dtype=out_local.dtype, device=dev)
+    for q, lp in enumerate(parts):
+        full[torch.from_numpy(lp.nodes[lp.owned]).to(dev)] = slots[q][:counts[q]]
+    return full
+

@@ -14,8 +14,12 @@ drop-in replaces only the reference's ``models`` package, so th
 reference's own ``training.train`` / ``utils.dataset`` stay importable for its callers
 (main.py, test_model.py).  ``rollout_test`` here is the fused variant: for our GNN / MSGNN
 on a GPU it is ONE engine call (msw_rollout; the T steps replay a captured hipGraph, the BC
-write and the window shift fused into the decoder kernel).  ``mswegnn.run --fused-rollout``
-installs it in place of the reference's ``training.train.rollout_test``.
+write and the window shift fused into the decoder kernel).  ``MSWEGNN_FUSED_ROLLOUT=1`` in
+the environment (read by ``models/__init__.py``, :mod:`mswegnn.hooks`) installs it in place
+of the reference's ``training.train.rollout_test``.  If ``training.train`` is itself being
+imported at that moment, the swap happens at the first model call, so that first
+``rollout_test`` call still steps the reference's loop (one graph-replayed ``msw_forward``
+per step); every later call is fused.
 """
 import numpy as np
 import torch

@@ -196,6 +196,40 @@ def test_fused_rollout_matches_step_loop_and_graph_capture(cuda):
     assert torch.equal(r1, r3)
 
 
+@pytest.mark.parametrize("mesh,S,F,K,ck", [("small", 4, 32, 4, "K4_F32"), ("small", 4, 16, 2, "K2_F16"),
+                                           ("small3", 3, 32, 4, None)])
+def test_captured_forward_matches_eager_forward(cuda, mesh, S, F, K, ck):
+    """msw_forward with graph capture (x copied into the plan's slot, one graph launch, y
+    copied out) == the eager forward bit for bit, over the reference's own step loop
+    (training/train.py:87-95: a new x tensor every step, predictions kept across steps) and
+    == the fused rollout."""
+    from mswegnn.engine import plan_for
+    from mswegnn.rollout import apply_boundary_condition, use_prediction
+    T = 12
+    g = make_multiscale_mesh(**mesh_config(mesh), T=T).to(cuda)
+    m = _hip(build_msgnn(S, F, K, state=weights(ck) if ck else None), cuda)
+    plan = plan_for(m, g)
+
+    def loop(capture):
+        plan.set_graph_capture(capture)
+        temp = g.clone()
+        preds = []
+        with torch.no_grad():
+            for t in range(T):
+                temp.x[:, -6:] = apply_boundary_condition(temp.x[:, -6:], temp.BC[:, :, t], temp.node_BC, 2)
+                p = m(temp)
+                temp.x = use_prediction(temp.x, p, 3)
+                preds.append(p)
+        return torch.stack(preds, -1)
+    eager = loop(False)
+    captured = loop(True)
+    assert plan_for(m, g) is plan and plan.stats()["graph_captured"] == 1
+    again = loop(True)  # replays the same captured forward
+    assert torch.equal(captured, eager) and torch.equal(again, eager)
+    plan.set_graph_capture(True)
+    assert torch.equal(m.rollout(g, T), eager)
+
+
 def test_rollout_test_dropin(cuda):
     from mswegnn.rollout import rollout_test
     fx = golden("fx_small_K4_F32_rollout48")

@@ -1,10 +1,14 @@
 """RCCL transport of the single-mesh decomposition (mswegnn/partition.py DistributedRollout):
-W processes, one part each, halo exchange over RCCL inside msw_rollout, compared with the
-undivided rollout of the same mesh.  On a multi-GPU node every rank takes its own GPU; with
-one GPU all ranks share cuda:0 (works only if RCCL accepts several ranks per device).
+W processes, one GPU and one part each, the halo exchange over RCCL inside msw_rollout
+(grouped ncclSend / ncclRecv) and the owned rows gathered by ONE padded tensor
+all-gather over RCCL (gather_owned), compared with the undivided rollout of the same mesh.
+Prints one JSON line.  Needs W GPUs (RCCL refuses two ranks on one device); bench.py runs it
+at N > 1 with a time limit.
 
-    python tools/rccl_partition_check.py [W]
+    python tools/rccl_partition_check.py [W] [--mesh zenodo4|small] [--steps 5]
 """
+import argparse
+import json
 import os
 import socket
 import sys
@@ -17,55 +21,88 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "mswe-gnn_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
 
 
-def worker(rank, world, port, q):
+def worker(rank, world, port, q, mesh, steps):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-    ndev = torch.cuda.device_count()
-    dev = torch.device(f"cuda:{rank % ndev}")
+    dev = torch.device(f"cuda:{rank}")
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     try:
         from conftest import build_msgnn, weights, per_step_rel
         from mswegnn.mesh import make_multiscale_mesh, mesh_config
         from mswegnn.partition import DistributedRollout
-        g = make_multiscale_mesh(**mesh_config("small"), T=48)
+        T = 48
+        g = make_multiscale_mesh(**mesh_config(mesh), T=T)
         m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(dev)
         m.engine = "hip"
         dr = DistributedRollout(m, g, device=dev)
-        out = dr.rollout(g.x.to(dev), g.BC, g.node_BC, g.type_BC, 48)
+        x0 = g.x.to(dev)
+        out = dr.rollout(x0, g.BC, g.node_BC, g.type_BC, T)
         torch.cuda.synchronize()
+        dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(5):
-            out = dr.rollout(g.x.to(dev), g.BC, g.node_BC, g.type_BC, 48)
+        for _ in range(steps):
+            out = dr.rollout(x0, g.BC, g.node_BC, g.type_BC, T)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 5
-        full = dr.gather_owned(out)
+        dist.barrier()
+        dt = torch.tensor([(time.perf_counter() - t0) / steps], device=dev, dtype=torch.float64)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        full = dr.gather_owned(out)  # RCCL all-gather of the owned rows
         if rank == 0:
-            whole = m.rollout(g.to(dev)).cpu()
-            q.put((per_step_rel(full, whole), dt))
+            gd = g.to(dev)
+            whole = m.rollout(gd)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                whole = m.rollout(gd)
+            torch.cuda.synchronize()
+            t_whole = (time.perf_counter() - t0) / steps
+            lp = dr.part
+            q.put({"world": world, "mesh": mesh, "fine_nodes": int(g.node_ptr[1]), "all_nodes": g.num_nodes,
+                   "halo_rows_rank0": int((~lp.owned).sum()), "rollout_steps": T,
+                   "max_rel_err_vs_undivided": per_step_rel(full.cpu(), whole.cpu()),
+                   "bit_identical": bool(torch.equal(full, whole)),
+                   "distributed_ms_per_rollout": float(dt.item()) * 1e3,
+                   "undivided_ms_per_rollout": t_whole * 1e3,
+                   "transport": "RCCL (msw_plan_set_comm: grouped ncclSend/ncclRecv halo exchange; "
+                                "gather_owned: torch.distributed all_gather on nccl)"})
         dr.close()
     except Exception as e:  # report, do not hang the peer
-        q.put(("error", repr(e)))
+        q.put({"error": repr(e), "rank": rank})
         raise
     finally:
         dist.destroy_process_group()
 
 
 def main():
-    W = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    ap = argparse.ArgumentParser()
+    ap.add_argument("W", nargs="?", type=int, default=2)
+    ap.add_argument("--mesh", default="small")
+    ap.add_argument("--steps", type=int, default=5)
+    a = ap.parse_args()
+    if torch.cuda.device_count() < a.W:
+        print(json.dumps({"error": f"needs {a.W} GPUs, {torch.cuda.device_count()} visible"}))
+        sys.exit(1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=worker, args=(r, W, port, q)) for r in range(W)]
+    procs = [ctx.Process(target=worker, args=(r, a.W, port, q, a.mesh, a.steps), daemon=True)
+             for r in range(a.W)]
     for p in procs:
         p.start()
-    res = q.get(timeout=300)
+    try:
+        res = q.get(timeout=240)
+    except Exception:  # noqa: BLE001  (queue.Empty: a rank hung)
+        res = {"error": "no result within 240 s"}
     for p in procs:
         p.join(60)
-    print({"world": W, "result": res, "exitcodes": [p.exitcode for p in procs]})
-    ok = res[0] != "error" and res[0] <= 1e-4
+        if p.is_alive():
+            p.kill()
+    res["exitcodes"] = [p.exitcode for p in procs]
+    print(json.dumps(res), flush=True)
+    ok = "error" not in res and res["max_rel_err_vs_undivided"] <= 1e-4
     sys.exit(0 if ok else 1)
 
 
