@@ -245,6 +245,55 @@ int msw_rollout_metrics(const float* pred, const float* real, int32_t T, const i
                         int32_t num_sims, const float* thresholds, int32_t n_thr, const float* area,
                         double* sums, uint64_t* counts, void* stream);
 
+/* ---- Training: autograd through one SWEGNN processor ------------------------
+ * Replaces the autograd of SWEGNN.forward (models/gnn.py:387-445) the reference trains through
+ * in training_step (training/train.py:125-145).  Stateless: every buffer is device memory the
+ * caller owns (mswegnn/autograd.py allocates them as torch tensors).  Parameters are the
+ * layer's own tensors: edge_mlp Linear weights [width[l+1]][width[l]] / biases, single-slope
+ * PReLU parameters, filter_matrix[k].weight [F][F]. */
+#define MSW_MAX_HOPS 8
+typedef struct {
+  int64_t num_nodes, num_edges;
+  int32_t F;             /* dynamic_node_features = static = edge_output_size */
+  int32_t edge_features; /* width of edge_attr (0 for intra_scale_gnn) */
+  int32_t K;             /* hops, 1..MSW_MAX_HOPS */
+  int32_t n_layers;      /* edge MLP depth, 1..MSW_MAX_MLP_LAYERS */
+  int32_t width[MSW_MAX_MLP_LAYERS + 1]; /* width[0] = 4F + edge_features, width[n_layers] = F */
+  int32_t act[MSW_MAX_MLP_LAYERS];       /* enum msw_activation after each layer */
+  int32_t normalize, with_filter_matrix, with_gradient, upwind_mode;
+  /* graph, device int32: row / col = edge_index[0] / [1]; CSR by destination (col) and by
+   * source (row), edges of a node in reference (edge_index) order */
+  const int32_t *row, *col;
+  const int32_t *in_ptr, *in_edge;   /* [N + 1], [E] */
+  const int32_t *out_ptr, *out_edge; /* [N + 1], [E] */
+  const float* weight[MSW_MAX_MLP_LAYERS];
+  const float* bias[MSW_MAX_MLP_LAYERS];  /* NULL = bias=False */
+  const float* slope[MSW_MAX_MLP_LAYERS]; /* device scalar (PReLU) or NULL */
+  const float* filter[MSW_MAX_HOPS + 1];  /* with_filter_matrix: K + 1 matrices */
+} msw_swegnn_train_desc;
+
+/* Gradient outputs (device; written, not accumulated).  d_x_d is required; any other NULL
+ * pointer skips that gradient. */
+typedef struct {
+  float *d_x_s, *d_x_d, *d_edge_attr;
+  float* d_weight[MSW_MAX_MLP_LAYERS];
+  float* d_bias[MSW_MAX_MLP_LAYERS];
+  float* d_slope[MSW_MAX_MLP_LAYERS];
+  float* d_filter[MSW_MAX_HOPS + 1];
+} msw_swegnn_grads;
+
+/* Floats of the forward's saved state (kept until the backward) and of the backward's scratch. */
+int msw_swegnn_train_workspace(const msw_swegnn_train_desc* desc, int64_t* saved_floats,
+                               int64_t* scratch_floats);
+/* out [N][F] = SWEGNN(x_s, x_d, edge_attr); `saved` receives the MLP inputs / pre-activations,
+ * s_ij, ||h||, out_k, the aggregated messages and the activity flags of every hop. */
+int msw_swegnn_train_forward(const msw_swegnn_train_desc* desc, const float* x_s, const float* x_d,
+                             const float* edge_attr, float* saved, float* out, void* stream);
+/* Gradients of all inputs and parameters given grad_out [N][F] and the forward's `saved`. */
+int msw_swegnn_train_backward(const msw_swegnn_train_desc* desc, const float* x_s, const float* x_d,
+                              const float* edge_attr, const float* saved, const float* grad_out,
+                              const msw_swegnn_grads* grads, float* scratch, void* stream);
+
 /* Diagnostics: route per-phase timestamps of wave 0 of workgroup 0 of every launch to the
  * device buffer `buf` (uint64[20]: {shader clock, 100 MHz clock} for phase marks 0..9).
  * Only builds compiled with -DMSW_TRACE record anything; NULL disables. */

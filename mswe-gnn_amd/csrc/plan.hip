@@ -1521,6 +1521,8 @@ int64_t msw_struct_size(const char* name) {
   if (!strcmp(name, "msw_graph_desc")) return sizeof(msw_graph_desc);
   if (!strcmp(name, "msw_plan_stats")) return sizeof(msw_plan_stats);
   if (!strcmp(name, "msw_exchange_desc")) return sizeof(msw_exchange_desc);
+  if (!strcmp(name, "msw_swegnn_train_desc")) return sizeof(msw_swegnn_train_desc);
+  if (!strcmp(name, "msw_swegnn_grads")) return sizeof(msw_swegnn_grads);
   return -1;
 }
 

@@ -1,0 +1,666 @@
+// Autograd through one SWEGNN processor on gfx950 (first slice): the training
+// forward (saving what the backward needs) and the backward of
+//   SWEGNN.forward  models/gnn.py:387-445
+// as the reference trains it (training_step, training/train.py:125-145).  The reference
+// recomputes s_ij from the active edges of every hop; s_ij depends on the hop only through
+// the mask, so by linearity of the backward ONE MLP backward of ds = sum_k [active_k] ds_k
+// gives the same parameter and input gradients.
+//
+// Kernels (all deterministic: fixed summation orders, CSR pulls, split-K partials reduced in
+// order -- no atomics):
+//   k_gemm        C = A B on v_mfma_f32_16x16x4_f32, generic strides (the three shapes of a
+//                 linear layer: X W^T forward, dY W backward, dY^T X weight gradient with
+//                 split-K over the rows), epilogues bias / activation / addend / partials
+//   k_gather_cat  the edge-MLP input rows [x_s[row], x_s[col], x_d[row], x_d[col], e]
+//   k_normalize   s = h / ||h||, NaN -> 0 (gnn.py:424-426)
+//   k_hop_agg     per destination: sum of active messages in CSR (reference edge) order
+//   k_edge_bwd / k_node_bwd   the hop's transpose: per edge ds and the message gradient,
+//                 per node the pull over in-edges (CSR by col) and out-edges (CSR by row)
+//   k_act_bwd, k_colsum, k_scatter_inputs, k_sum_splits
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../include/mswegnn.h"
+#include "engine.h"
+
+namespace {
+
+using msw::set_error;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 64, kBN = 64, kBK = 16, kGemmThreads = 256;
+constexpr int kMaxSplits = 256;
+constexpr int kMaxHops = 8;
+
+__device__ __forceinline__ float act_fwd(int act, float x, float a) {
+  switch (act) {
+    case MSW_ACT_PRELU: return x > 0.f ? x : a * x;
+    case MSW_ACT_RELU: return x > 0.f ? x : 0.f;
+    case MSW_ACT_LEAKYRELU: return x > 0.f ? x : 0.1f * x;
+    case MSW_ACT_ELU: return x > 0.f ? x : expm1f(x);
+    case MSW_ACT_SWISH: return x / (1.f + expf(-x));
+    case MSW_ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+    case MSW_ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+// d act / d x at the pre-activation x
+__device__ __forceinline__ float act_grad(int act, float x, float a) {
+  switch (act) {
+    case MSW_ACT_PRELU: return x > 0.f ? 1.f : a;
+    case MSW_ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case MSW_ACT_LEAKYRELU: return x > 0.f ? 1.f : 0.1f;
+    case MSW_ACT_ELU: return x > 0.f ? 1.f : expf(x);
+    case MSW_ACT_SWISH: {
+      const float sg = 1.f / (1.f + expf(-x));
+      return sg * (1.f + x * (1.f - sg));
+    }
+    case MSW_ACT_SIGMOID: {
+      const float sg = 1.f / (1.f + expf(-x));
+      return sg * (1.f - sg);
+    }
+    case MSW_ACT_TANH: {
+      const float t = tanhf(x);
+      return 1.f - t * t;
+    }
+    default: return 1.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------ GEMM
+// C(m, n) = sum_k A(m, k) B(k, n), A(m, k) = A[m lam + k lak], B(k, n) = B[k lbk + n lbn].
+// 64 x 64 output tile per 256-thread workgroup, 16-deep K slices staged in LDS (k-major, so
+// the MFMA fragments are read along m / n across lanes); each wave owns a 32 x 32 quarter as
+// 2 x 2 tiles of v_mfma_f32_16x16x4_f32 (A: lane l gives A(i = l & 15, k = l >> 4); B: lane l
+// gives B(k = l >> 4, j = l & 15); D: lane l holds D(4 (l >> 4) + r, l & 15)).  Split-K
+// (part != null): workgroup z sums K slice z into part[z][M][N]; k_sum_splits adds the slices
+// in order.
+struct GemmArgs {
+  int M, N, K;
+  const float* A; long lam, lak;
+  const float* B; long lbk, lbn;
+  float* C; long ldc;
+  const float* addend; long ldd;  // C = addend + AB (nullable)
+  const float* bias;              // + bias[n] (nullable)
+  float* pre; long ldp;           // pre-activation store (nullable)
+  int act; const float* slope;    // activation of the stored C (device scalar slope)
+  float* part; int kchunk;        // split-K partials
+};
+
+__global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
+  __shared__ float As[kBK][kBM + 4];
+  __shared__ float Bs[kBK][kBN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * kBM, n0 = blockIdx.y * kBN;
+  const int kb = a.part ? blockIdx.z * a.kchunk : 0;
+  const int ke = a.part ? min(a.K, kb + a.kchunk) : a.K;
+  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool a_mfast = a.lam == 1 && a.lak != 1;  // A stored m-contiguous (transposed operand)
+  const bool b_kfast = a.lbk == 1 && a.lbn != 1;  // B stored k-contiguous
+  for (int k0 = kb; k0 < ke; k0 += kBK) {
+#pragma unroll
+    for (int u = 0; u < (kBM * kBK) / kGemmThreads; ++u) {
+      const int idx = tid + u * kGemmThreads;
+      const int mm = a_mfast ? idx % kBM : idx / kBK, kk = a_mfast ? idx / kBM : idx % kBK;
+      const int m = m0 + mm, k = k0 + kk;
+      As[kk][mm] = (m < a.M && k < ke) ? a.A[(long)m * a.lam + (long)k * a.lak] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < (kBN * kBK) / kGemmThreads; ++u) {
+      const int idx = tid + u * kGemmThreads;
+      const int nn = b_kfast ? idx / kBK : idx % kBN, kk = b_kfast ? idx % kBK : idx / kBN;
+      const int n = n0 + nn, k = k0 + kk;
+      Bs[kk][nn] = (n < a.N && k < ke) ? a.B[(long)k * a.lbk + (long)n * a.lbn] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k4 = 0; k4 < kBK; k4 += 4) {
+      const int kr = k4 + (lane >> 4);
+      float av[2], bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = As[kr][wm + 16 * i + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[kr][wn + 16 * j + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const float sl = a.slope ? *a.slope : 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r, n = n0 + wn + 16 * j + (lane & 15);
+        if (m >= a.M || n >= a.N) continue;
+        float v = acc[i][j][r];
+        if (a.part) {
+          a.part[((long)blockIdx.z * a.M + m) * a.N + n] = v;
+          continue;
+        }
+        if (a.addend) v = a.addend[(long)m * a.ldd + n] + v;
+        if (a.bias) v = v + a.bias[n];
+        if (a.pre) a.pre[(long)m * a.ldp + n] = v;
+        a.C[(long)m * a.ldc + n] = act_fwd(a.act, v, sl);
+      }
+}
+
+// out[i] = sum_{s < splits} part[s][i] (in order), i < count
+__global__ void k_sum_splits(const float* __restrict__ part, int splits, long count, float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += part[(long)s * count + i];
+    out[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------ elementwise
+// X0[e] = [x_s[row], x_s[col], x_d[row], x_d[col], edge_attr[e]]  (gnn.py:414-420)
+__global__ void k_gather_cat(const int* __restrict__ row, const int* __restrict__ col, const float* __restrict__ xs,
+                             const float* __restrict__ xd, const float* __restrict__ ea, int F, int ef, long E,
+                             float* __restrict__ X0) {
+  const int w0 = 4 * F + ef;
+  const long total = E * w0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long e = i / w0;
+    const int c = (int)(i - e * w0);
+    float v;
+    if (c < F) v = xs[(long)row[e] * F + c];
+    else if (c < 2 * F) v = xs[(long)col[e] * F + c - F];
+    else if (c < 3 * F) v = xd[(long)row[e] * F + c - 2 * F];
+    else if (c < 4 * F) v = xd[(long)col[e] * F + c - 3 * F];
+    else v = ea[e * ef + c - 4 * F];
+    X0[i] = v;
+  }
+}
+
+// s = h / ||h||_2, NaN -> 0 (gnn.py:424-426); one thread per edge
+__global__ void k_normalize(const float* __restrict__ h, int F, long E, int normalize, float* __restrict__ s,
+                            float* __restrict__ nrm) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x) {
+    const float* he = h + e * F;
+    float* se = s + e * F;
+    if (!normalize) {
+      for (int f = 0; f < F; ++f) se[f] = he[f];
+      nrm[e] = 1.f;
+      continue;
+    }
+    float q = 0.f;
+    for (int f = 0; f < F; ++f) q += he[f] * he[f];
+    const float n = sqrtf(q);
+    nrm[e] = n;
+    for (int f = 0; f < F; ++f) {
+      const float v = he[f] / n;
+      se[f] = isnan(v) ? 0.f : v;
+    }
+  }
+}
+
+// nz[n] = (sum_f out[n][f]) != 0  (gnn.py:408)
+__global__ void k_node_nz(const float* __restrict__ out, int F, long N, int* __restrict__ nz) {
+  for (long n = blockIdx.x * (long)blockDim.x + threadIdx.x; n < N; n += (long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int f = 0; f < F; ++f) v += out[n * F + f];
+    nz[n] = v != 0.f ? 1 : 0;
+  }
+}
+
+// agg[c][f] = sum over active in-edges e of c (reference order) of the message
+// (out[c] - out[row]) s (upwind: clamped at 0) or s out[row] (gnn.py:410-438)
+__global__ void k_hop_agg(const int* __restrict__ in_ptr, const int* __restrict__ in_edge,
+                          const int* __restrict__ row, const float* __restrict__ out, const float* __restrict__ s,
+                          const int* __restrict__ nz, int F, long N, int grad, int upwind, float* __restrict__ agg) {
+  const long total = N * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long c = i / F;
+    const int f = (int)(i - c * F);
+    const float oc = out[c * F + f];
+    const int zc = nz[c];
+    float acc = 0.f;
+    for (int q = in_ptr[c]; q < in_ptr[c + 1]; ++q) {
+      const int e = in_edge[q], r = row[e];
+      if (!(zc | nz[r])) continue;
+      float m;
+      if (grad) {
+        float d = oc - out[(long)r * F + f];
+        if (upwind && d < 0.f) d = 0.f;
+        m = d * s[(long)e * F + f];
+      } else {
+        m = s[(long)e * F + f] * out[(long)r * F + f];
+      }
+      acc += m;
+    }
+    agg[i] = acc;
+  }
+}
+
+// The hop's transpose, per edge: dm = dagg[col] on active edges; ds += dm * gradient term;
+// t = dm * s * (upwind: [diff > 0]) -- the message's derivative w.r.t. out
+__global__ void k_edge_bwd(const int* __restrict__ row, const int* __restrict__ col, const float* __restrict__ out,
+                           const float* __restrict__ s, const int* __restrict__ nz, const float* __restrict__ dagg,
+                           int F, long E, int grad, int upwind, float* __restrict__ ds, float* __restrict__ t) {
+  const long total = E * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long e = i / F;
+    const int f = (int)(i - e * F);
+    const int r = row[e], c = col[e];
+    if (!(nz[r] | nz[c])) {
+      t[i] = 0.f;
+      continue;
+    }
+    const float dm = dagg[(long)c * F + f], se = s[i];
+    if (grad) {
+      const float d = out[(long)c * F + f] - out[(long)r * F + f];
+      const bool pass = !upwind || d >= 0.f;  // hydraulic_gradient[hg < 0] = 0 (gnn.py:431-432)
+      ds[i] += dm * (pass ? d : 0.f);
+      t[i] = pass ? dm * se : 0.f;
+    } else {
+      ds[i] += dm * out[(long)r * F + f];
+      t[i] = dm * se;
+    }
+  }
+}
+
+// Gn[c] = G[c] + sum_{e in in(c)} t_e - sum_{e in out(c)} t_e   (with_gradient)
+//       = G[c] + sum_{e in out(c)} t_e                         (s * out[row])
+__global__ void k_node_bwd(const int* __restrict__ in_ptr, const int* __restrict__ in_edge,
+                           const int* __restrict__ out_ptr, const int* __restrict__ out_edge,
+                           const float* __restrict__ G, const float* __restrict__ t, int F, long N, int grad,
+                           float* __restrict__ Gn) {
+  const long total = N * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / F;
+    const int f = (int)(i - n * F);
+    float a = 0.f, b = 0.f;
+    if (grad)
+      for (int q = in_ptr[n]; q < in_ptr[n + 1]; ++q) a += t[(long)in_edge[q] * F + f];
+    for (int q = out_ptr[n]; q < out_ptr[n + 1]; ++q) b += t[(long)out_edge[q] * F + f];
+    Gn[i] = grad ? G[i] + (a - b) : G[i] + b;
+  }
+}
+
+// dh = (ds - s (s . ds)) / ||h|| (0 where the norm is 0: s was set to 0 there)
+__global__ void k_normalize_bwd(const float* __restrict__ s, const float* __restrict__ nrm,
+                                const float* __restrict__ ds, int F, long E, int normalize, float* __restrict__ dh) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x) {
+    const float* se = s + e * F;
+    const float* de = ds + e * F;
+    float* out = dh + e * F;
+    if (!normalize) {
+      for (int f = 0; f < F; ++f) out[f] = de[f];
+      continue;
+    }
+    const float n = nrm[e];
+    if (!(n > 0.f)) {
+      for (int f = 0; f < F; ++f) out[f] = 0.f;
+      continue;
+    }
+    float dot = 0.f;
+    for (int f = 0; f < F; ++f) dot += se[f] * de[f];
+    for (int f = 0; f < F; ++f) out[f] = (de[f] - se[f] * dot) / n;
+  }
+}
+
+// dpre = dy * act'(pre); PReLU slope: per-block partial of sum(pre <= 0 ? pre * dy : 0)
+// (torch's prelu backward), written to spart[blockIdx.x]
+__global__ __launch_bounds__(256) void k_act_bwd(const float* __restrict__ pre, const float* __restrict__ dy, long count,
+                                                 int act, const float* __restrict__ slope, float* __restrict__ dpre,
+                                                 float* __restrict__ spart) {
+  __shared__ float red[256];
+  const float a = slope ? *slope : 0.f;
+  float sacc = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    const float x = pre[i], g = dy[i];
+    dpre[i] = g * act_grad(act, x, a);
+    if (act == MSW_ACT_PRELU && !(x > 0.f)) sacc += x * g;
+  }
+  red[threadIdx.x] = sacc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && spart) spart[blockIdx.x] = red[0];
+}
+
+// column sums of X [R][W] over row slice blockIdx.x -> part[blockIdx.x][W]
+__global__ void k_colsum(const float* __restrict__ X, long R, int W, long rchunk, float* __restrict__ part) {
+  const long r0 = blockIdx.x * rchunk, r1 = min(R, r0 + rchunk);
+  for (int c = threadIdx.x; c < W; c += blockDim.x) {
+    float v = 0.f;
+    for (long r = r0; r < r1; ++r) v += X[r * W + c];
+    part[(long)blockIdx.x * W + c] = v;
+  }
+}
+
+// input gradients from dX0 [E][4F + ef]: x_s / x_d rows pull their out-edge (row) and in-edge
+// (col) slices (CSR orders), dxd accumulates onto the filter-0 term already there
+__global__ void k_scatter_inputs(const int* __restrict__ in_ptr, const int* __restrict__ in_edge,
+                                 const int* __restrict__ out_ptr, const int* __restrict__ out_edge,
+                                 const float* __restrict__ dX0, int F, int ef, long N, float* __restrict__ dxs,
+                                 float* __restrict__ dxd) {
+  const int w0 = 4 * F + ef;
+  const long total = N * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / F;
+    const int f = (int)(i - n * F);
+    float as = 0.f, ad = 0.f, bs = 0.f, bd = 0.f;
+    for (int q = out_ptr[n]; q < out_ptr[n + 1]; ++q) {
+      const float* r = dX0 + (long)out_edge[q] * w0;
+      as += r[f];
+      ad += r[2 * F + f];
+    }
+    for (int q = in_ptr[n]; q < in_ptr[n + 1]; ++q) {
+      const float* r = dX0 + (long)in_edge[q] * w0;
+      bs += r[F + f];
+      bd += r[3 * F + f];
+    }
+    if (dxs) dxs[i] = as + bs;
+    if (dxd) dxd[i] = dxd[i] + (ad + bd);
+  }
+}
+
+__global__ void k_copy_cols(const float* __restrict__ src, long rows, int src_ld, int c0, int w,
+                            float* __restrict__ dst) {
+  const long total = rows * w;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / w;
+    dst[i] = src[r * src_ld + c0 + (i - r * w)];
+  }
+}
+
+__global__ void k_add(const float* __restrict__ a, const float* __restrict__ b, long n, float* __restrict__ c) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    c[i] = a[i] + b[i];
+}
+
+// ---------------------------------------------------------------------------------- host
+inline int blocks_for(long n, int threads = 256) {
+  long b = (n + threads - 1) / threads;
+  return (int)std::max<long>(1, std::min<long>(b, 16384));
+}
+
+struct Layout {  // float offsets into the saved / scratch buffers
+  long X0, pre[4], post[4], s, nrm, outk, agg, nz, saved;
+  long G0, G1, dagg, t, ds, dA, dB, part, spart, scratch;
+  int L, w[5], wmax;
+};
+
+bool layout_of(const msw_swegnn_train_desc* d, Layout& y) {
+  if (!d || d->n_layers < 1 || d->n_layers > 4 || d->F < 1 || d->K < 1 || d->K > kMaxHops || d->num_nodes < 0 ||
+      d->num_edges < 0 || d->edge_features < 0)
+    return false;
+  const long E = d->num_edges, N = d->num_nodes, F = d->F;
+  y.L = d->n_layers;
+  y.wmax = 0;
+  for (int l = 0; l <= y.L; ++l) {
+    y.w[l] = d->width[l];
+    if (y.w[l] <= 0) return false;
+    y.wmax = std::max(y.wmax, y.w[l]);
+  }
+  if (y.w[0] != 4 * F + d->edge_features || y.w[y.L] != F) return false;
+  auto al = [](long n) { return (n + 63) / 64 * 64; };
+  long o = 0;
+  y.X0 = o; o += al(E * y.w[0]);
+  for (int l = 0; l < y.L; ++l) { y.pre[l] = o; o += al(E * y.w[l + 1]); }
+  for (int l = 0; l < y.L; ++l) { y.post[l] = o; o += al(E * y.w[l + 1]); }
+  y.s = o; o += al(E * F);
+  y.nrm = o; o += al(E);
+  y.outk = o; o += al((long)(d->K + 1) * N * F);
+  y.agg = o; o += al((long)d->K * N * F);
+  y.nz = o; o += al((long)d->K * N);
+  y.saved = o;
+  o = 0;
+  y.G0 = o; o += al(N * F);
+  y.G1 = o; o += al(N * F);
+  y.dagg = o; o += al(N * F);
+  y.t = o; o += al(E * F);
+  y.ds = o; o += al(E * F);
+  y.dA = o; o += al(E * y.wmax);
+  y.dB = o; o += al(E * y.wmax);
+  y.part = o; o += al((long)kMaxSplits * y.wmax * y.wmax);
+  y.spart = o; o += al(kMaxSplits * 4L);
+  y.scratch = o;
+  return true;
+}
+
+hipError_t gemm(const GemmArgs& a0, hipStream_t st, int splits = 1) {
+  GemmArgs a = a0;
+  dim3 grid((a.M + kBM - 1) / kBM, (a.N + kBN - 1) / kBN, 1);
+  if (a.part) {
+    splits = std::max(1, std::min(splits, kMaxSplits));
+    a.kchunk = ((a.K + splits - 1) / splits + kBK - 1) / kBK * kBK;
+    grid.z = (a.K + a.kchunk - 1) / a.kchunk;
+    if (grid.z == 0) grid.z = 1;
+  }
+  hipLaunchKernelGGL(k_gemm, grid, dim3(kGemmThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+// dW [M][N] = sum_rows A(row, m) B(row, n): split-K over the rows, partials summed in order
+hipError_t weight_grad(const float* A, int lda, const float* B, int ldb, long R, int M, int N, float* part,
+                       float* dW, hipStream_t st) {
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = (int)R;
+  g.A = A; g.lam = 1; g.lak = lda;
+  g.B = B; g.lbk = ldb; g.lbn = 1;
+  g.part = part;
+  const int splits = (int)std::min<long>(kMaxSplits, std::max<long>(1, R / 1024));
+  hipError_t e = gemm(g, st, splits);
+  if (e != hipSuccess) return e;
+  const int kchunk = ((g.K + splits - 1) / splits + kBK - 1) / kBK * kBK;
+  const int used = std::max(1, (g.K + kchunk - 1) / kchunk);
+  hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N)), dim3(256), 0, st, part, used, (long)M * N, dW);
+  return hipGetLastError();
+}
+
+#define TRY(x)                                                                     \
+  do {                                                                             \
+    hipError_t _e = (x);                                                           \
+    if (_e != hipSuccess) return set_error(MSW_ERR_HIP, hipGetErrorString(_e));    \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int msw_swegnn_train_workspace(const msw_swegnn_train_desc* d, int64_t* saved_floats, int64_t* scratch_floats) {
+  Layout y;
+  if (!layout_of(d, y)) return set_error(MSW_ERR_INVALID, "inconsistent SWEGNN training descriptor");
+  if (saved_floats) *saved_floats = y.saved;
+  if (scratch_floats) *scratch_floats = y.scratch;
+  return MSW_OK;
+}
+
+int msw_swegnn_train_forward(const msw_swegnn_train_desc* d, const float* xs, const float* xd, const float* ea,
+                             float* saved, float* out, void* stream) {
+  Layout y;
+  if (!layout_of(d, y)) return set_error(MSW_ERR_INVALID, "inconsistent SWEGNN training descriptor");
+  if (!xs || !xd || !saved || !out || (d->edge_features > 0 && !ea)) return set_error(MSW_ERR_INVALID, "null argument");
+  if (d->with_filter_matrix)
+    for (int k = 0; k <= d->K; ++k)
+      if (!d->filter[k]) return set_error(MSW_ERR_INVALID, "filter matrix missing");
+  hipStream_t st = (hipStream_t)stream;
+  const long E = d->num_edges, N = d->num_nodes;
+  const int F = d->F;
+  float* X0 = saved + y.X0;
+  if (E > 0) {
+    hipLaunchKernelGGL(k_gather_cat, dim3(blocks_for(E * y.w[0])), dim3(256), 0, st, d->row, d->col, xs, xd, ea, F,
+                       d->edge_features, E, X0);
+    TRY(hipGetLastError());
+    const float* in = X0;
+    for (int l = 0; l < y.L; ++l) {  // make_mlp: Linear + activation after every layer
+      GemmArgs g{};
+      g.M = (int)E; g.N = y.w[l + 1]; g.K = y.w[l];
+      g.A = in; g.lam = y.w[l]; g.lak = 1;
+      g.B = d->weight[l]; g.lbk = 1; g.lbn = y.w[l];  // B(k, n) = W[n][k]
+      g.C = saved + y.post[l]; g.ldc = y.w[l + 1];
+      g.bias = d->bias[l];
+      g.pre = saved + y.pre[l]; g.ldp = y.w[l + 1];
+      g.act = d->act[l]; g.slope = d->slope[l];
+      TRY(gemm(g, st));
+      in = saved + y.post[l];
+    }
+    hipLaunchKernelGGL(k_normalize, dim3(blocks_for(E)), dim3(256), 0, st, saved + y.post[y.L - 1], F, E, d->normalize,
+                       saved + y.s, saved + y.nrm);
+    TRY(hipGetLastError());
+  }
+  // out_0 = filter_matrix[0] x_d (gnn.py:401-404)
+  float* o0 = saved + y.outk;
+  if (d->with_filter_matrix) {
+    GemmArgs g{};
+    g.M = (int)N; g.N = F; g.K = F;
+    g.A = xd; g.lam = F; g.lak = 1;
+    g.B = d->filter[0]; g.lbk = 1; g.lbn = F;
+    g.C = o0; g.ldc = F;
+    TRY(gemm(g, st));
+  } else {
+    TRY(hipMemcpyAsync(o0, xd, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
+  }
+  for (int k = 0; k < d->K; ++k) {
+    const float* ok = saved + y.outk + (long)k * N * F;
+    float* on = saved + y.outk + (long)(k + 1) * N * F;
+    float* agg = saved + y.agg + (long)k * N * F;
+    int* nz = reinterpret_cast<int*>(saved + y.nz + (long)k * N);
+    hipLaunchKernelGGL(k_node_nz, dim3(blocks_for(N)), dim3(256), 0, st, ok, F, N, nz);
+    hipLaunchKernelGGL(k_hop_agg, dim3(blocks_for(N * F)), dim3(256), 0, st, d->in_ptr, d->in_edge, d->row, ok,
+                       saved + y.s, nz, F, N, d->with_gradient, d->upwind_mode, agg);
+    TRY(hipGetLastError());
+    if (d->with_filter_matrix) {  // out_{k+1} = out_k + filter_matrix[k+1](agg)
+      GemmArgs g{};
+      g.M = (int)N; g.N = F; g.K = F;
+      g.A = agg; g.lam = F; g.lak = 1;
+      g.B = d->filter[k + 1]; g.lbk = 1; g.lbn = F;
+      g.C = on; g.ldc = F;
+      g.addend = ok; g.ldd = F;
+      TRY(gemm(g, st));
+    } else {
+      hipLaunchKernelGGL(k_add, dim3(blocks_for(N * F)), dim3(256), 0, st, ok, agg, N * F, on);
+      TRY(hipGetLastError());
+    }
+  }
+  TRY(hipMemcpyAsync(out, saved + y.outk + (long)d->K * N * F, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
+  return MSW_OK;
+}
+
+int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, const float* xd, const float* ea,
+                              const float* saved, const float* grad_out, const msw_swegnn_grads* gr, float* scratch,
+                              void* stream) {
+  (void)xs;
+  (void)ea;
+  Layout y;
+  if (!layout_of(d, y)) return set_error(MSW_ERR_INVALID, "inconsistent SWEGNN training descriptor");
+  if (!xd || !saved || !grad_out || !gr || !scratch) return set_error(MSW_ERR_INVALID, "null argument");
+  if (!gr->d_x_d) return set_error(MSW_ERR_INVALID, "d_x_d is required (it accumulates the filter-0 term)");
+  hipStream_t st = (hipStream_t)stream;
+  const long E = d->num_edges, N = d->num_nodes;
+  const int F = d->F;
+  float* G = scratch + y.G0;
+  float* Gn = scratch + y.G1;
+  float* dagg = scratch + y.dagg;
+  float* t = scratch + y.t;
+  float* ds = scratch + y.ds;
+  float* part = scratch + y.part;
+  TRY(hipMemcpyAsync(G, grad_out, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
+  if (E > 0) TRY(hipMemsetAsync(ds, 0, sizeof(float) * E * F, st));
+  for (int k = d->K - 1; k >= 0; --k) {
+    const float* ok = saved + y.outk + (long)k * N * F;
+    const float* agg = saved + y.agg + (long)k * N * F;
+    const int* nz = reinterpret_cast<const int*>(saved + y.nz + (long)k * N);
+    if (d->with_filter_matrix) {
+      if (gr->d_filter[k + 1]) TRY(weight_grad(G, F, agg, F, N, F, F, part, gr->d_filter[k + 1], st));
+      GemmArgs g{};  // dagg = G W_{k+1}
+      g.M = (int)N; g.N = F; g.K = F;
+      g.A = G; g.lam = F; g.lak = 1;
+      g.B = d->filter[k + 1]; g.lbk = F; g.lbn = 1;
+      g.C = dagg; g.ldc = F;
+      TRY(gemm(g, st));
+    } else {
+      TRY(hipMemcpyAsync(dagg, G, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
+    }
+    if (E > 0) {
+      hipLaunchKernelGGL(k_edge_bwd, dim3(blocks_for(E * F)), dim3(256), 0, st, d->row, d->col, ok, saved + y.s, nz,
+                         dagg, F, E, d->with_gradient, d->upwind_mode, ds, t);
+      TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_node_bwd, dim3(blocks_for(N * F)), dim3(256), 0, st, d->in_ptr, d->in_edge, d->out_ptr,
+                       d->out_edge, G, t, F, N, d->with_gradient, Gn);
+    TRY(hipGetLastError());
+    std::swap(G, Gn);
+  }
+  // out_0 = W_0 x_d
+  if (d->with_filter_matrix) {
+    if (gr->d_filter[0]) TRY(weight_grad(G, F, xd, F, N, F, F, part, gr->d_filter[0], st));
+    GemmArgs g{};
+    g.M = (int)N; g.N = F; g.K = F;
+    g.A = G; g.lam = F; g.lak = 1;
+    g.B = d->filter[0]; g.lbk = F; g.lbn = 1;
+    g.C = gr->d_x_d; g.ldc = F;
+    TRY(gemm(g, st));
+  } else {
+    TRY(hipMemcpyAsync(gr->d_x_d, G, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
+  }
+  if (E == 0) {
+    if (gr->d_x_s) TRY(hipMemsetAsync(gr->d_x_s, 0, sizeof(float) * N * F, st));
+    for (int l = 0; l < y.L; ++l) {
+      if (gr->d_weight[l]) TRY(hipMemsetAsync(gr->d_weight[l], 0, sizeof(float) * y.w[l] * y.w[l + 1], st));
+      if (gr->d_bias[l]) TRY(hipMemsetAsync(gr->d_bias[l], 0, sizeof(float) * y.w[l + 1], st));
+      if (gr->d_slope[l]) TRY(hipMemsetAsync(gr->d_slope[l], 0, sizeof(float), st));
+    }
+    return MSW_OK;
+  }
+  // s = normalize(h): ds -> dh
+  float* dcur = scratch + y.dA;
+  float* dpre = scratch + y.dB;
+  hipLaunchKernelGGL(k_normalize_bwd, dim3(blocks_for(E)), dim3(256), 0, st, saved + y.s, saved + y.nrm, ds, F, E,
+                     d->normalize, dcur);
+  TRY(hipGetLastError());
+  const long rchunk = std::max<long>(1024, (E + kMaxSplits - 1) / kMaxSplits);
+  const int nrs = (int)((E + rchunk - 1) / rchunk);
+  for (int l = y.L - 1; l >= 0; --l) {
+    const int wi = y.w[l], wo = y.w[l + 1];
+    const int ab = blocks_for(E * wo) < kMaxSplits ? blocks_for(E * wo) : kMaxSplits;
+    hipLaunchKernelGGL(k_act_bwd, dim3(ab), dim3(256), 0, st, saved + y.pre[l], dcur, E * wo, d->act[l],
+                       d->slope[l], dpre, scratch + y.spart);
+    TRY(hipGetLastError());
+    if (gr->d_slope[l]) {
+      hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(64), 0, st, scratch + y.spart, ab, 1L, gr->d_slope[l]);
+      TRY(hipGetLastError());
+    }
+    if (gr->d_bias[l]) {
+      hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, E, wo, rchunk, part);
+      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo)), dim3(256), 0, st, part, nrs, (long)wo, gr->d_bias[l]);
+      TRY(hipGetLastError());
+    }
+    const float* Xl = l == 0 ? saved + y.X0 : saved + y.post[l - 1];
+    if (gr->d_weight[l]) TRY(weight_grad(dpre, wo, Xl, wi, E, wo, wi, part, gr->d_weight[l], st));
+    GemmArgs g{};  // d X_l = dpre W_l
+    g.M = (int)E; g.N = wi; g.K = wo;
+    g.A = dpre; g.lam = wo; g.lak = 1;
+    g.B = d->weight[l]; g.lbk = wi; g.lbn = 1;
+    g.C = dcur; g.ldc = wi;
+    TRY(gemm(g, st));
+  }
+  // dcur = dX0 [E][4F + ef]
+  hipLaunchKernelGGL(k_scatter_inputs, dim3(blocks_for(N * F)), dim3(256), 0, st, d->in_ptr, d->in_edge, d->out_ptr,
+                     d->out_edge, dcur, F, d->edge_features, N, gr->d_x_s, gr->d_x_d);
+  TRY(hipGetLastError());
+  if (d->edge_features > 0 && gr->d_edge_attr) {
+    hipLaunchKernelGGL(k_copy_cols, dim3(blocks_for(E * d->edge_features)), dim3(256), 0, st, dcur, E, y.w[0], 4 * F,
+                       d->edge_features, gr->d_edge_attr);
+    TRY(hipGetLastError());
+  }
+  return MSW_OK;
+}
+
+}  // extern "C"

@@ -78,6 +78,27 @@ class MswExchangeDesc(C.Structure):
                 ("send_ptr", c_int64_p), ("send_rows", c_int32_p)]
 
 
+MAX_HOPS = 8
+
+
+class MswSwegnnTrainDesc(C.Structure):
+    _fields_ = [("num_nodes", C.c_int64), ("num_edges", C.c_int64), ("F", C.c_int32),
+                ("edge_features", C.c_int32), ("K", C.c_int32), ("n_layers", C.c_int32),
+                ("width", C.c_int32 * (MAX_MLP_LAYERS + 1)), ("act", C.c_int32 * MAX_MLP_LAYERS),
+                ("normalize", C.c_int32), ("with_filter_matrix", C.c_int32),
+                ("with_gradient", C.c_int32), ("upwind_mode", C.c_int32),
+                ("row", C.c_void_p), ("col", C.c_void_p), ("in_ptr", C.c_void_p), ("in_edge", C.c_void_p),
+                ("out_ptr", C.c_void_p), ("out_edge", C.c_void_p),
+                ("weight", C.c_void_p * MAX_MLP_LAYERS), ("bias", C.c_void_p * MAX_MLP_LAYERS),
+                ("slope", C.c_void_p * MAX_MLP_LAYERS), ("filter", C.c_void_p * (MAX_HOPS + 1))]
+
+
+class MswSwegnnGrads(C.Structure):
+    _fields_ = [("d_x_s", C.c_void_p), ("d_x_d", C.c_void_p), ("d_edge_attr", C.c_void_p),
+                ("d_weight", C.c_void_p * MAX_MLP_LAYERS), ("d_bias", C.c_void_p * MAX_MLP_LAYERS),
+                ("d_slope", C.c_void_p * MAX_MLP_LAYERS), ("d_filter", C.c_void_p * (MAX_HOPS + 1))]
+
+
 # (name, restype, argtypes) of every entry point declared in include/mswegnn.h
 SYMBOLS = [
     ("msw_plan_create", C.c_int, [C.POINTER(MswGraphDesc), C.POINTER(MswModelDesc), C.c_int,
@@ -105,11 +126,18 @@ SYMBOLS = [
     ("msw_group_rollout", C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_void_p), c_int32_p, C.POINTER(c_int32_p), c_int32_p,
                                     C.c_int32, C.c_int32, C.POINTER(C.c_void_p), C.c_void_p]),
+    ("msw_swegnn_train_workspace", C.c_int, [C.POINTER(MswSwegnnTrainDesc), c_int64_p, c_int64_p]),
+    ("msw_swegnn_train_forward", C.c_int, [C.POINTER(MswSwegnnTrainDesc), C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("msw_swegnn_train_backward", C.c_int, [C.POINTER(MswSwegnnTrainDesc), C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.POINTER(MswSwegnnGrads), C.c_void_p, C.c_void_p]),
 ]
 
 STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,
            "msw_model_desc": MswModelDesc, "msw_graph_desc": MswGraphDesc,
-           "msw_plan_stats": MswPlanStats, "msw_exchange_desc": MswExchangeDesc}
+           "msw_plan_stats": MswPlanStats, "msw_exchange_desc": MswExchangeDesc,
+           "msw_swegnn_train_desc": MswSwegnnTrainDesc, "msw_swegnn_grads": MswSwegnnGrads}
 
 _lib = None
 

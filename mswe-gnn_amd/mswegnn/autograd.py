@@ -1,0 +1,222 @@
+"""Autograd through the HIP SWEGNN kernels (first slice).
+
+``swegnn_apply(layer, x_s, x_d, edge_index, edge_attr)`` runs one ``SWEGNN`` processor
+(models/gnn.py:387-445) as a ``torch.autograd.Function`` whose forward and backward are the
+gfx950 kernels of ``csrc/train.hip`` behind the C ABI (``msw_swegnn_train_*``,
+include/mswegnn.h): every parameter and input gradient the reference's ``training_step``
+(training/train.py:125-145) back-propagates through the layer is computed by HIP kernels --
+MFMA GEMMs for the edge-MLP and filter layers (split-K weight gradients), CSR pulls by
+destination and by source for the hop's transpose, no atomics.  torch only allocates the
+buffers (saved state, scratch, gradients) and orders the work on its current stream.
+
+``SWEGNN.forward`` (models/gnn.py of this package) routes here on a GPU with autograd
+enabled; everything else of the model (encoders, pooling, decoder) keeps its torch path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .engine import _act_of, _raw_stream
+
+__all__ = ["swegnn_apply", "supported", "graph_csr"]
+
+_CSR_CACHE = OrderedDict()
+_CSR_KEEP = 32
+
+
+class GraphCSR:
+    """row / col (int32) and the CSRs by destination (col) and by source (row) of one
+    edge_index on the GPU; each node's edges in reference (edge_index) order."""
+
+    def __init__(self, edge_index, num_nodes):
+        ei = edge_index.to(torch.int64)
+        dev = ei.device
+        self.num_nodes = int(num_nodes)
+        self.num_edges = int(ei.shape[1])
+        self.row = ei[0].to(torch.int32).contiguous()
+        self.col = ei[1].to(torch.int32).contiguous()
+
+        def csr(key):
+            order = torch.sort(key, stable=True).indices.to(torch.int32).contiguous()
+            cnt = torch.bincount(key, minlength=self.num_nodes)
+            ptr = torch.zeros(self.num_nodes + 1, dtype=torch.int64, device=dev)
+            ptr[1:] = torch.cumsum(cnt, 0)
+            return ptr.to(torch.int32).contiguous(), order
+        self.in_ptr, self.in_edge = csr(ei[1])
+        self.out_ptr, self.out_edge = csr(ei[0])
+
+
+def graph_csr(edge_index, num_nodes):
+    """Cached GraphCSR: keyed by the index tensor's address, layout and in-place version; the
+    cache holds the tensor itself, so its storage (and address) cannot be reused meanwhile."""
+    key = (edge_index.data_ptr(), tuple(edge_index.shape), tuple(edge_index.stride()), edge_index._version,
+           int(num_nodes), str(edge_index.device))
+    hit = _CSR_CACHE.get(key)
+    if hit is not None:
+        _CSR_CACHE.move_to_end(key)
+        return hit[1]
+    g = GraphCSR(edge_index, num_nodes)
+    _CSR_CACHE[key] = (edge_index, g)
+    while len(_CSR_CACHE) > _CSR_KEEP:
+        _CSR_CACHE.popitem(last=False)
+    return g
+
+
+def _mlp_layers(seq):
+    """make_mlp Sequential -> [(Linear, activation module or None)]; None if unsupported."""
+    layers = []
+    for m in seq:
+        if isinstance(m, nn.Linear):
+            layers.append([m, None])
+        elif isinstance(m, nn.Dropout):
+            if m.p > 0 and m.training:
+                return None
+        elif isinstance(m, nn.LayerNorm):
+            return None
+        elif layers:
+            layers[-1][1] = m
+        else:
+            return None
+    if not 1 <= len(layers) <= L.MAX_MLP_LAYERS:
+        return None
+    for lin, act in layers:
+        try:
+            _act_of(act)
+        except NotImplementedError:
+            return None
+    return layers
+
+
+def supported(layer, x_s, x_d, edge_attr):
+    """The HIP training path implements this layer call (else the torch path runs)."""
+    if not (x_d.is_cuda and x_s.is_cuda) or x_d.dtype != torch.float32 or x_s.dtype != torch.float32:
+        return False
+    if layer.K < 1 or layer.K > L.MAX_HOPS or _mlp_layers(layer.edge_mlp) is None:
+        return False
+    if layer.edge_features > 0 and (edge_attr is None or edge_attr.dtype != torch.float32):
+        return False
+    return all(p.dtype == torch.float32 and p.is_cuda for p in layer.parameters())
+
+
+class _Meta:
+    """Everything but the tensors autograd tracks: the descriptor template of one call."""
+
+    def __init__(self, layer, layers, csr, F, ef):
+        self.layer, self.layers, self.csr, self.F, self.ef = layer, layers, csr, F, ef
+        d = L.MswSwegnnTrainDesc()
+        d.num_nodes, d.num_edges = csr.num_nodes, csr.num_edges
+        d.F, d.edge_features, d.K, d.n_layers = F, ef, layer.K, len(layers)
+        d.width[0] = layers[0][0].in_features
+        for i, (lin, act) in enumerate(layers):
+            d.width[i + 1] = lin.out_features
+            d.act[i] = _act_of(act)[0]
+        d.normalize = int(bool(layer.normalize))
+        d.with_filter_matrix = int(bool(layer.with_filter_matrix))
+        d.with_gradient = int(bool(layer.with_gradient))
+        d.upwind_mode = int(bool(layer.upwind_mode))
+        for name in ("row", "col", "in_ptr", "in_edge", "out_ptr", "out_edge"):
+            setattr(d, name, getattr(csr, name).data_ptr())
+        self.desc = d
+        # parameter list order = the Function's *params
+        self.params = []
+        for lin, act in layers:
+            self.params.append(lin.weight)
+            if lin.bias is not None:
+                self.params.append(lin.bias)
+            if isinstance(act, nn.PReLU):
+                self.params.append(act.weight)
+        if layer.with_filter_matrix:
+            self.params += [f.weight for f in layer.filter_matrix]
+
+    def bind(self, params):
+        """Point the descriptor at the (contiguous) parameter tensors of this call."""
+        d, it = self.desc, iter(params)
+        for i, (lin, act) in enumerate(self.layers):
+            d.weight[i] = next(it).data_ptr()
+            d.bias[i] = next(it).data_ptr() if lin.bias is not None else None
+            d.slope[i] = next(it).data_ptr() if isinstance(act, nn.PReLU) else None
+        if self.layer.with_filter_matrix:
+            for k in range(self.layer.K + 1):
+                d.filter[k] = next(it).data_ptr()
+        return d
+
+
+def _ws(meta):
+    s, t = C.c_int64(), C.c_int64()
+    L.check(L.lib().msw_swegnn_train_workspace(C.byref(meta.desc), C.byref(s), C.byref(t)))
+    return int(s.value), int(t.value)
+
+
+class _SwegnnFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, x_s, x_d, edge_attr, *params):
+        dev = x_d.device
+        x_s, x_d = x_s.contiguous(), x_d.contiguous()
+        ea = edge_attr.contiguous() if meta.ef > 0 else None
+        params = [p.contiguous() for p in params]
+        d = meta.bind(params)
+        n_saved, _ = _ws(meta)
+        saved = torch.empty(n_saved, device=dev, dtype=torch.float32)
+        out = torch.empty(meta.csr.num_nodes, meta.F, device=dev, dtype=torch.float32)
+        L.check(L.lib().msw_swegnn_train_forward(C.byref(d), x_s.data_ptr(), x_d.data_ptr(),
+                                                 ea.data_ptr() if ea is not None else None,
+                                                 saved.data_ptr(), out.data_ptr(),
+                                                 C.c_void_p(_raw_stream(dev.index or 0))))
+        ctx.meta = meta
+        ctx.has_ea = edge_attr is not None
+        ctx.save_for_backward(x_s, x_d, ea if ea is not None else torch.empty(0, device=dev), saved, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        meta = ctx.meta
+        x_s, x_d, ea, saved, *params = ctx.saved_tensors
+        dev = x_d.device
+        gout = gout.contiguous().to(torch.float32)
+        d = meta.bind(params)
+        _, n_scratch = _ws(meta)
+        scratch = torch.empty(n_scratch, device=dev, dtype=torch.float32)
+        g = L.MswSwegnnGrads()
+        dxs = torch.empty_like(x_s) if ctx.needs_input_grad[1] else None
+        dxd = torch.empty_like(x_d)
+        dea = torch.empty_like(ea) if meta.ef > 0 and ctx.needs_input_grad[3] else None
+        g.d_x_s = dxs.data_ptr() if dxs is not None else None
+        g.d_x_d = dxd.data_ptr()
+        g.d_edge_attr = dea.data_ptr() if dea is not None else None
+        dps = [torch.empty_like(p) if ctx.needs_input_grad[4 + i] else None for i, p in enumerate(params)]
+        it = iter(dps)
+        for i, (lin, act) in enumerate(meta.layers):
+            w = next(it)
+            g.d_weight[i] = w.data_ptr() if w is not None else None
+            if lin.bias is not None:
+                b = next(it)
+                g.d_bias[i] = b.data_ptr() if b is not None else None
+            if isinstance(act, nn.PReLU):
+                a = next(it)
+                g.d_slope[i] = a.data_ptr() if a is not None else None
+        if meta.layer.with_filter_matrix:
+            for k in range(meta.layer.K + 1):
+                f = next(it)
+                g.d_filter[k] = f.data_ptr() if f is not None else None
+        L.check(L.lib().msw_swegnn_train_backward(C.byref(d), x_s.data_ptr(), x_d.data_ptr(),
+                                                  ea.data_ptr() if meta.ef > 0 else None, saved.data_ptr(),
+                                                  gout.data_ptr(), C.byref(g), scratch.data_ptr(),
+                                                  C.c_void_p(_raw_stream(dev.index or 0))))
+        return (None, dxs, dxd, dea if ctx.has_ea else None, *dps)
+
+
+def swegnn_apply(layer, x_s, x_d, edge_index, edge_attr=None):
+    """SWEGNN.forward of `layer` on the HIP training kernels (differentiable)."""
+    layers = _mlp_layers(layer.edge_mlp)
+    F = int(x_d.shape[1])
+    ef = int(layer.edge_features) if layer.edge_features > 0 else 0
+    csr = graph_csr(edge_index, x_d.shape[0])
+    meta = _Meta(layer, layers, csr, F, ef)
+    if ef > 0 and edge_attr.dim() == 1:
+        edge_attr = edge_attr.unsqueeze(1)
+    return _SwegnnFunction.apply(meta, x_s, x_d, edge_attr if ef > 0 else None, *meta.params)

@@ -222,6 +222,11 @@ class EnginePlan:
             raise ValueError(f"x has shape {tuple(x.shape)}, plan expects {(self.num_nodes, self.nnf)}")
         return x.contiguous()
 
+    def accepts(self, x):
+        """x can be fed to forward() as is (right device, dtype, shape, contiguous)."""
+        return (x.is_cuda and x.device == self.device and x.dtype == torch.float32
+                and x.shape == (self.num_nodes, self.nnf) and x.is_contiguous())
+
     def forward(self, x):
         """MSGNN.forward / GNN.forward on the GPU: x [N, nnf] -> y [N, 2].  The plan replays
         its captured forward graph (msw_forward): two device copies + one graph launch."""

@@ -1,0 +1,123 @@
+"""Autograd through the HIP SWEGNN kernels (first slice; mswegnn/autograd.py,
+csrc/train.hip) against the drop-in's torch autograd of the same layer, which restates the
+reference's SWEGNN.forward (models/gnn.py:387-445) op for op.
+
+The reference trains through this layer in training_step (training/train.py:125-145).  The
+bar: every parameter and input gradient within 1e-4 relative (max |ours - torch| / max |torch|)
+of torch's fp32 autograd on the same inputs.
+"""
+import pytest
+import torch
+
+from conftest import build_msgnn, rel_err, weights
+from mswegnn.mesh import make_multiscale_mesh, mesh_config, wet_state
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _encoded_inputs(m, g, scale):
+    """x_s, x_d (encoders of the model, torch) and the encoded edge features of `scale`'s
+    edges, as MSGNN.forward feeds gnn_processor[scale] (gnn.py:281-304)."""
+    with torch.no_grad():
+        x = g.x.clone()
+        nst = m.static_node_features - m.with_WL
+        x_s, x_d = x[:, :nst], x[:, nst:]
+        x_s = torch.cat((x_s, (x_s[:, -1] + x_d[:, -m.out_dim]).unsqueeze(-1)), 1)
+        x_s = m.static_node_encoder(x_s)
+        x_d = m.dynamic_node_encoder(x_d)
+        ea = m.edge_encoder(g.edge_attr)
+    ep = g.edge_ptr
+    ei = g.edge_index[:, ep[scale]:ep[scale + 1]]
+    return x_s, x_d, ei, ea[ep[scale]:ep[scale + 1]]
+
+
+def _grads(layer, x_s, x_d, ei, ea, wout, engine):
+    layer.train_engine = engine
+    layer.zero_grad(set_to_none=True)
+    xs = x_s.clone().requires_grad_(True)
+    xd = x_d.clone().requires_grad_(True)
+    e = ea.clone().requires_grad_(True) if ea is not None else None
+    out = layer(xs, xd, ei, e)
+    (out * wout).sum().backward()
+    g = {"out": out.detach(), "x_s": xs.grad, "x_d": xd.grad}
+    if e is not None:
+        g["edge_attr"] = e.grad
+    for n, p in layer.named_parameters():
+        g[n] = p.grad
+    layer.train_engine = "auto"
+    return g
+
+
+def _compare(ours, ref, label):
+    assert ours.keys() == ref.keys()
+    worst = {}
+    for k in ref:
+        assert ours[k] is not None and ref[k] is not None, (label, k)
+        worst[k] = rel_err(ours[k], ref[k])
+    bad = {k: v for k, v in worst.items() if not v <= TOL}
+    assert not bad, (label, bad)
+    return max(worst.values())
+
+
+@pytest.mark.parametrize("scale", [0, 2])
+def test_processor_gradients_vs_torch_autograd(cuda, scale):
+    """One K4_F32 processor (gnn_processor[scale]: K = 4 hops, 3-layer PReLU edge MLP with the
+    encoded edge features, filter matrices) on the tiny mesh with a partly wet state (dry rows
+    make inactive edges): output, d x_s, d x_d, d edge_attr and every parameter gradient."""
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=4), seed=1).to(cuda)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+    x_s, x_d, ei, ea = _encoded_inputs(m, g, scale)
+    layer = m.gnn_processor[scale]
+    wout = torch.randn(x_d.shape, device=cuda, generator=torch.Generator(cuda).manual_seed(3))
+    ref = _grads(layer, x_s, x_d, ei, ea, wout, "torch")
+    ours = _grads(layer, x_s, x_d, ei, ea, wout, "auto")
+    e = _compare(ours, ref, f"scale {scale}")
+    print(f"gnn_processor[{scale}]: worst rel err {e:.2e} over {len(ref)} tensors")
+
+
+def test_intra_scale_and_variant_gradients(cuda):
+    """The other SWEGNN shapes: intra_scale_gnn (K = 1, no edge features, no filter, s * out[row]
+    messages), upwind_mode, no normalisation, a 2-layer ReLU MLP, K = 2."""
+    from models.gnn import SWEGNN
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=4), seed=2).to(cuda)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+    x_s, x_d, ei, ea = _encoded_inputs(m, g, 0)
+    gen = torch.Generator(cuda).manual_seed(5)
+    wout = torch.randn(x_d.shape, device=cuda, generator=gen)
+    iei = g.intra_mesh_edge_index[:, g.intra_edge_ptr[0]:g.intra_edge_ptr[1]]
+    _compare(_grads(m.intra_scale_gnn[2], x_s, x_d, iei, None, wout, "auto"),
+             _grads(m.intra_scale_gnn[2], x_s, x_d, iei, None, wout, "torch"), "intra")
+    torch.manual_seed(0)
+    for kw in (dict(upwind_mode=True), dict(normalize=False), dict(K=2, n_layers=2, activation="relu"),
+               dict(with_gradient=False, with_filter_matrix=False, K=3)):
+        args = dict(K=kw.pop("K", 4), n_layers=kw.pop("n_layers", 3), activation=kw.pop("activation", "prelu"),
+                    bias=True)
+        layer = SWEGNN(32, 32, 32, device=cuda, **args, **kw).to(cuda)
+        _compare(_grads(layer, x_s, x_d, ei, ea, wout, "auto"), _grads(layer, x_s, x_d, ei, ea, wout, "torch"),
+                 str(kw or args))
+
+
+def test_msgnn_training_step_gradients(cuda):
+    """A whole MSGNN loss backward with every SWEGNN layer (7 processors + 3 unpooling) on the
+    HIP training kernels vs the all-torch model: the gradient of every parameter (the
+    reference's training_step back-propagates a per-step loss through MSGNN.forward)."""
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=4), seed=1).to(cuda)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+    m.train()
+    tgt = torch.rand(g.num_nodes, 2, device=cuda, generator=torch.Generator(cuda).manual_seed(7))
+
+    def step(engine):
+        m.zero_grad(set_to_none=True)
+        m.engine = engine
+        y = m(g)
+        loss = ((y - tgt) ** 2).mean()
+        loss.backward()
+        return {"y": y.detach(), **{n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}}
+    ref = step("torch")
+    ours = step("auto")
+    from mswegnn.autograd import _CSR_CACHE
+    assert len(_CSR_CACHE) > 0  # the HIP training path ran
+    e = _compare(ours, ref, "MSGNN")
+    print(f"MSGNN: worst rel err {e:.2e} over {len(ref)} gradients")

@@ -598,3 +598,43 @@ def test_strong_scaling_section_two_ranks_gloo():
         assert k in s3, k
     assert len(s3["rank_ms"]) == 2 and s3["tW_ms"] >= max(s3["rank_ms"]) - 1e-9
     assert s3["gathered_vs_single_gpu_max_rel"] <= 1e-5
+
+
+def test_speculative_forward_replans_on_weight_change(monkeypatch):
+    """models.gnn _engine_forward launches the previous call's plan before consulting the plan
+    cache (the reference's step loop syncs the host every step); when the cache names another
+    plan -- weights modified in place, another graph -- the forward is redone with it and the
+    speculative output is dropped.  EnginePlan is a recorder (no GPU)."""
+    from mswegnn import engine as E
+    calls = []
+
+    class FakePlan:
+        _h = 1
+
+        def __init__(self, model, graph, device):
+            self.tag = float(len(calls))
+            calls.append(("build", self.tag))
+
+        def accepts(self, x):
+            return True
+
+        def forward(self, x):
+            calls.append(("fwd", self.tag))
+            return torch.full((x.shape[0], 2), self.tag)
+
+        def close(self):
+            self._h = None
+
+    monkeypatch.setattr(E, "EnginePlan", FakePlan)
+    g = make_multiscale_mesh(**mesh_config("tiny"), T=2)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32"))
+    y0 = m._engine_forward(g)
+    y1 = m._engine_forward(g)
+    assert torch.equal(y0, y1) and [c[0] for c in calls] == ["build", "fwd", "fwd"]
+    with torch.no_grad():
+        m.node_decoder[0].weight.mul_(1.0)  # in-place: version bump -> new plan
+    y2 = m._engine_forward(g)
+    assert calls[-3:] == [("fwd", 0.0), ("build", 4.0), ("fwd", 4.0)]  # speculative, rebuild, redo
+    assert float(y2[0, 0]) == 4.0
+    y3 = m._engine_forward(g.clone())  # same content: cache adopts it, speculation stands
+    assert float(y3[0, 0]) == 4.0 and calls[-1] == ("fwd", 4.0)
