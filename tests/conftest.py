@@ -161,4 +161,43 @@ def assert_rollout_parity(ours, ref, P, cfg, g, T, label=""):
           f"ours vs fp64 {e_ours:.2e} (mask-threshold flip)")
     assert e_ref > REL_TOL, f"{label}: {e:.2e} > {REL_TOL} on a well-conditioned rollout"
     assert e_ours <= 1.5 * e_ref, f"{label}: ours {e_ours:.2e} vs fp64, reference {e_ref:.2e}"
+    t, cells = flip_localisation(ours, ref, r64)
+    print(f"{label}: divergence starts at step {t}, cells {cells} (the reference's own mask flip)")
     return e, e_ref
+
+
+def flip_localisation(ours, ref, r64, thr=1e-4):
+    """Proof that a rollout divergence from the fp32 reference is the reference's own
+    _mask_small_WD flip (models/models.py:79-91) and nothing else.  ours / ref / r64:
+    [N, 2, T] (ours, the fp32 reference, exact fp64 arithmetic).  Asserts that
+      * the first step where ours leaves the fp32 reference (rel > REL_TOL) is the first step
+        where the fp32 reference leaves fp64 arithmetic;
+      * at that step every cell where ours differs from the reference is a cell where the
+        reference differs from fp64, and at each of them one side's depth is exactly 0 and the
+        other's lies within rounding above the 1e-4 threshold (the mask flipped), and ours
+        took the fp64 side;
+    returns (that step, those cells)."""
+    ours, ref, r64 = (torch.as_tensor(a).double().cpu() for a in (ours, ref, r64))
+    T = ref.shape[-1]
+
+    def first_step(a, b):
+        for t in range(T):
+            if rel_err(a[..., t], b[..., t]) > REL_TOL:
+                return t
+        return None
+    t_ref, t_ours = first_step(ref, r64), first_step(ours, ref)
+    assert t_ref is not None and t_ours == t_ref, f"ours diverges at step {t_ours}, the reference's flip is at {t_ref}"
+    t = t_ref
+    den = ref[..., t].abs().max().item()
+    d_ours = (ours[..., t] - ref[..., t]).abs().amax(1) > REL_TOL * den
+    d_flip = (ref[..., t] - r64[..., t]).abs().amax(1) > REL_TOL * den
+    cells = torch.nonzero(d_ours).flatten().tolist()
+    assert cells, "no cell diverges at the first divergent step"
+    assert not bool((d_ours & ~d_flip).any()), \
+        f"cells {torch.nonzero(d_ours & ~d_flip).flatten().tolist()} diverge where the reference did not flip"
+    for n in cells:
+        h32, h64 = ref[n, 0, t].item(), r64[n, 0, t].item()
+        lo, hi = sorted((abs(h32), abs(h64)))
+        assert lo == 0.0 and thr < hi <= thr * (1 + 1e-3), f"cell {n}: depths {h32!r} / {h64!r} are not a mask flip"
+        assert (ours[n, :, t] - r64[n, :, t]).abs().max().item() <= REL_TOL * den, f"cell {n}: ours not on the fp64 side"
+    return t, cells

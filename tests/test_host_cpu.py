@@ -638,3 +638,28 @@ def test_speculative_forward_replans_on_weight_change(monkeypatch):
     assert float(y2[0, 0]) == 4.0
     y3 = m._engine_forward(g.clone())  # same content: cache adopts it, speculation stands
     assert float(y3[0, 0]) == 4.0 and calls[-1] == ("fwd", 4.0)
+
+
+def test_flip_localisation_rules():
+    """conftest.flip_localisation (the config-3 mask-flip exception, verdict r2): accepts a
+    divergence that starts at the reference's own flip cell, rejects one elsewhere."""
+    from conftest import flip_localisation
+    N, T = 50, 6
+    g = torch.Generator().manual_seed(0)
+    r64 = torch.rand(N, 2, T, generator=g, dtype=torch.float64) + 0.5
+    r64[7, 0, 3] = 1.00002e-4          # fp64: just above the threshold -> kept
+    ref = r64.clone().float().double()
+    ref[7, :, 3] = 0.0                 # fp32 reference: masked (h and v)
+    ref[:, :, 4:] += 0.01              # the flip propagates
+    ours = r64.clone()
+    ours[:, :, 4:] += 0.02             # ours stays on the fp64 side, diverges later
+    t, cells = flip_localisation(ours, ref, r64)
+    assert (t, cells) == (3, [7])
+    bad = ours.clone()
+    bad[11, 1, 3] += 0.5               # another cell diverging at the same step
+    with pytest.raises(AssertionError):
+        flip_localisation(bad, ref, r64)
+    early = ours.clone()
+    early[2, 0, 1] += 0.5              # divergence before the flip
+    with pytest.raises(AssertionError):
+        flip_localisation(early, ref, r64)
