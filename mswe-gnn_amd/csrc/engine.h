@@ -208,6 +208,12 @@ struct HopArgs {
   Epilogue epi;
   int coop;          // last hop: waves per tile (k_hop_coop), 0 = one
   int split;         // middle hop: features split over two waves per tile (k_hop_split)
+  // middle hop in the row layout (k_hop_rows, large meshes): 16 consecutive destinations per
+  // wave, each lane row pulling its in-edges from the scale's CSR by destination
+  int rows;
+  int nrows;         // destinations of the scale (local rows [0, nrows) = internal n0 + k)
+  const int* rptr;   // [nrows + 1] CSR offsets (local destination order)
+  const int2* redge; // [E] {internal source row, tile-padded s slot}, reference edge order
 };
 
 // Hop chain: M = 2 or 3 consecutive hops (k .. k+M-1) in one launch, the last of them

@@ -1676,6 +1676,92 @@ __global__ __launch_bounds__((64 * hop_waves<NT, LOOP>())) void k_hop(HopArgs a)
   MSW_MARK(c, 9);
 }
 
+// ---------------------------------------------------------------------------- row-layout middle hop
+// Large meshes (grid-stride regime, HBM-bound): a wave owns 16 CONSECUTIVE destination rows of
+// the scale; lane row j pulls its own in-edges from the scale's CSR by destination (reference
+// edge order: {source row, tile-padded s slot} per edge) -- no lane records, no LDS slab, and
+// all 16 rows of the filter MFMA are live (an edge tile holds ~5 destinations of its 16 rows).
+// A lane keeps DC edges' source and s rows in flight at once (DC = 4 at F <= 32, 2 at F = 64).
+// The arithmetic is k_hop's operation for operation -- the activity predicate's sums, the
+// message, agg = ((0 + m_0) + m_1) + ... in edge order, the filter -- so it is bit-identical.
+constexpr int kRowHopWaves = 8;
+#ifndef MSW_ROW_DC
+#define MSW_ROW_DC 4  // edges in flight per lane (F <= 32)
+#endif
+template <int NT>
+__global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  constexpr int DC = NT >= 4 ? 2 : MSW_ROW_DC;
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int stride = gridDim.x * kRowHopWaves;
+  const int ntile = (a.nrows + kRowsPerWave - 1) / kRowsPerWave;
+  f32x4 wf[NT][NT];
+  load_filter<NT>(wf, a.c.W, a.filt_a, lane);
+  for (int tile = blockIdx.x * kRowHopWaves + w; tile < ntile; tile += stride) {
+    const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+    const int k = tile * kRowsPerWave + j;
+    const bool valid = k < a.nrows;
+    const int kc = valid ? k : 0;
+    const int q0 = a.rptr[kc], q1 = valid ? a.rptr[kc + 1] : q0;
+    const size_t n = (size_t)a.n0 + kc;
+    f32x4 od[NT];
+    load_row<NT>(od, a.in + n * F, g);
+    const int deg = q1 - q0;
+    int dmax = deg;  // wave-uniform trip count
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) dmax = max(dmax, __shfl_xor(dmax, o));
+    float rd = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) rd += hsum(od[t]);
+    const bool zd = row_sum(rd) != 0.f;
+    f32x4 agg[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) agg[t] = zero4();
+    for (int q = 0; q < dmax; q += DC) {
+      int2 e[DC];
+#pragma unroll
+      for (int u = 0; u < DC; ++u)  // absent edges read the row's own entries (never used)
+        e[u] = q + u < deg ? a.redge[q0 + q + u] : int2{(int)n, 0};
+      f32x4 os[DC][NT], sv[DC][NT];
+#pragma unroll
+      for (int u = 0; u < DC; ++u) {
+        load_row<NT>(os[u], a.in + (size_t)e[u].x * F, g);
+        load_row<NT>(sv[u], a.s + (size_t)e[u].y * F, g);
+      }
+#pragma unroll
+      for (int u = 0; u < DC; ++u) {
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) rs += hsum(os[u][t]);
+        const bool act = (row_sum(rs) != 0.f) || zd;  // gnn.py:408-411
+        const bool has = q + u < deg;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x4 gv;
+          if (a.grad) {
+            gv = od[t] - os[u][t];
+            if (a.upwind) {
+              gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
+              gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
+            }
+          } else {
+            gv = os[u][t];
+          }
+          const f32x4 m = act ? gv * sv[u][t] : zero4();
+          const f32x4 sum = agg[t] + m;
+          agg[t] = has ? sum : agg[t];
+        }
+      }
+    }
+    f32x4 res[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = od[t];
+    apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+    if (valid) store_row<NT>(a.out + n * F, res, NT, g);
+  }
+}
+
 // ---------------------------------------------------------------------------- feature-split middle hop
 // A middle hop (no epilogue) with each edge tile's features split over two waves: rank r
 // gathers, messages and sums features [F r / 2, F (r + 1) / 2) only (half the loads per wave,
@@ -2579,6 +2665,12 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
     void* args[] = {&b};
     return hipLaunchKernel(f, grid, dim3(kBlock), args, lds_bytes<NT>(a.reg.len), st);
   }
+  if (a.rows && !a.last) {  // row-layout middle hop (large meshes)
+    const int nt = cdiv(a.nrows, kRowsPerWave);
+    const int grid = a.max_blocks > 0 ? std::min(a.max_blocks, cdiv(nt, kRowHopWaves)) : cdiv(nt, kRowHopWaves);
+    hipLaunchKernelGGL((k_hop_rows<NT>), dim3(grid), dim3(64 * kRowHopWaves), 0, st, a);
+    return hipGetLastError();
+  }
   if constexpr (NT >= 2) {
     if (a.split && !a.last) {  // feature-split middle hop: two waves per tile
       HopArgs b = a;
@@ -2698,6 +2790,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 12: return edge_coop_kernel<NT>(prelu, last, 2);
     case 9: return hop_coop_kernel<NT>(prelu);
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
+    case 14: return (const void*)k_hop_rows<NT>;
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }
@@ -2713,6 +2806,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
                     : kind == 13 ? 64 * 2 * NT
+                    : kind == 14 ? 64 * kRowHopWaves
                     : kind == 2 ? 64 * (loop ? hop_waves<NT, true>() : kWaves)
                     : 64 * (loop && (kind == 3 || kind == 6) ? waves_of<NT, true>() : kWaves);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, dyn) != hipSuccess)

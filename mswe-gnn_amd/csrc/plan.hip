@@ -194,6 +194,9 @@ struct ScaleCSR {
   int ntiles = 0;
   EdgeChunk* chunks = nullptr;  // [nchunks][16] dense edge chunks (k_edge_mlp)
   int nchunks = 0;
+  int* rptr = nullptr;          // row-layout middle hops (k_hop_rows, large scales): CSR by
+  int2* redge = nullptr;        // destination, {source row, s slot} per edge
+
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
   // hop chains of m = 2, 3 hops (engine.h HopMArgs), indexed by m; ok = false -> not built
   struct Chain {
@@ -622,6 +625,7 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
     HopArgs& h = H.hop;
     h.c = c;
     h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
+    h.nrows = g.ns; h.rptr = g.rptr; h.redge = g.redge;
     h.s = P->s; h.xs = P->xs;
     h.in = P->O[pr.par]; h.out = P->T[0];
     h.filt_a = eh.filt_a;
@@ -672,6 +676,7 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
       HopArgs& h = L.hop;
       h.c = c;
       h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles;
+      h.nrows = g.ns; h.rptr = g.rptr; h.redge = g.redge;
       h.s = P->s; h.xs = P->xs;
       h.in = cur; h.out = split ? (cur == P->T[0] ? P->T[1] : P->T[0]) : nxt;
       h.filt_a = pr.filt.empty() ? -1 : pr.filt[k - 1];
@@ -993,6 +998,14 @@ void caps(msw_plan* P, A& a, int kind, int prelu, int last, int floats) {
 // A/B measurements: MSW_NO_LOOP=eh,hop,epi,all keeps those launches one tile per wave at
 // any size (no grid-stride loop).
 constexpr int kHopLoopTiles = 65536;
+// middle hops of scales with at least this many edge tiles run in the row layout
+// (k_hop_rows; MSW_HOP_ROWS=0 keeps the edge tiles)
+constexpr int kRowHopMinTiles = kHopLoopTiles;
+// MSW_HOP_ROWS=2: every middle hop in the row layout, at any size (parity tests)
+bool row_hops_forced() {
+  const char* e = getenv("MSW_HOP_ROWS");
+  return e && atoi(e) == 2;
+}
 constexpr long kEncCoopWaves = 4096;
 bool no_loop(const char* kind) {
   const char* e = getenv("MSW_NO_LOOP");
@@ -1058,6 +1071,18 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         bool sp = P->NT == 4 && L.hop.max_blocks == 0;
         if (const char* hs = getenv("MSW_HOP_SPLIT")) sp = atoi(hs) != 0;
         L.hop.split = (sp && P->NT >= 2 && !L.hop.last) ? 1 : 0;
+      }
+      {  // row layout for the grid-stride middle hops of large scales (k_hop_rows)
+        HopArgs& h = L.hop;
+        const bool loop = h.fit_blocks > 0 && h.max_blocks > 0 && (h.ntiles + kWaves - 1) / kWaves > h.fit_blocks;
+        const char* hr = getenv("MSW_HOP_ROWS");
+        const bool want = hr ? atoi(hr) != 0 : true;
+        h.rows = 0;
+        if (want && !h.last && (loop || row_hops_forced()) && h.rptr && h.redge) {
+          h.rows = 1;
+          h.split = 0;
+          h.max_blocks = resident_of(P->NT, 14, 0, 0, 0, 1);
+        }
       }
       {  // a last hop with an epilogue on few tiles: P = F / 16 waves per tile (k_hop_coop)
         HopArgs& h = L.hop;
@@ -1409,6 +1434,14 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     }
     for (int m = 2; P->hop_pairs && c.ntiles <= P->chain_max_tiles && m <= P->chain_max; ++m)
       if ((rc = build_chain(P, c, rowptr, so, tl, pcsr, m))) return rc;
+    if (c.ntiles >= kRowHopMinTiles || row_hops_forced()) {  // row-layout middle hops: CSR + s slots
+      std::vector<int> slot_of_csr(c.E, -1);
+      for (size_t q = 0; q < pcsr.size(); ++q)
+        if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
+      std::vector<int2> re(std::max(c.E, 1));
+      for (int i = 0; i < c.E; ++i) re[i] = int2{so[i], slot_of_csr[i]};
+      if ((rc = pupload(P, &c.rptr, rowptr)) || (rc = pupload(P, &c.redge, re))) return rc;
+    }
   }
   // intra-scale levels
   P->lv.assign(S > 1 ? S - 1 : 0, LevelMaps{});

@@ -670,3 +670,21 @@ def test_wide_pool_matches_default(cuda, F, monkeypatch):
     m = build_msgnn(4, F, 4)
     ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), ga)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
+
+
+@pytest.mark.parametrize("S,F,K,ck", [(4, 32, 4, "K4_F32"), (4, 16, 2, "K2_F16"), (4, 64, 4, None), (3, 32, 4, None)])
+def test_row_layout_hops_match_edge_tiles(cuda, monkeypatch, S, F, K, ck):
+    """k_hop_rows (the row-layout middle hop of large meshes, forced on every scale here with
+    MSW_HOP_ROWS=2) == the edge-tile k_hop bit for bit over a rollout (wet start: every
+    branch of the activity predicate)."""
+    from mswegnn.engine import EnginePlan
+    T = 6
+    g = wet_state(make_multiscale_mesh(**mesh_config("small" if S == 4 else "small3"), T=T), seed=4).to(cuda)
+    m = build_msgnn(S, F, K, state=weights(ck) if ck else None).to(cuda)
+    outs = []
+    for v in ("0", "2"):
+        monkeypatch.setenv("MSW_HOP_ROWS", v)
+        plan = EnginePlan(m, g, cuda)
+        outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
+        plan.close()
+    assert torch.equal(outs[0], outs[1])
