@@ -1686,18 +1686,27 @@ __global__ __launch_bounds__((64 * hop_waves<NT, LOOP>())) void k_hop(HopArgs a)
 // message, agg = ((0 + m_0) + m_1) + ... in edge order, the filter -- so it is bit-identical.
 constexpr int kRowHopWaves = 8;
 #ifndef MSW_ROW_DC
-#define MSW_ROW_DC 4  // edges in flight per lane (F <= 32)
+#define MSW_ROW_DC 3  // edges in flight per lane (F <= 32): 113 VGPRs, 4 waves per SIMD
 #endif
 template <int NT>
 __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
   constexpr int DC = NT >= 4 ? 2 : MSW_ROW_DC;
-  const int lane = threadIdx.x & 63, w = wave_id();
+  [[maybe_unused]] const int lane = threadIdx.x & 63;
+  const int w = wave_id();
   const int stride = gridDim.x * kRowHopWaves;
   const int ntile = (a.nrows + kRowsPerWave - 1) / kRowsPerWave;
+#ifdef MSW_ROW_FILT_LDS
+  // the filter operand in LDS (ds_read per use) instead of 4 NT^2 VGPRs
+  __shared__ __attribute__((aligned(16))) float wl[NT * NT * 256];
+  for (int i = threadIdx.x; i < NT * NT * 64; i += 64 * kRowHopWaves)
+    st4(wl + 4 * i, ld4(a.c.W + (a.filt_a >= 0 ? a.filt_a : 0) + 4 * i));
+  __syncthreads();
+#else
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
+#endif
   for (int tile = blockIdx.x * kRowHopWaves + w; tile < ntile; tile += stride) {
     const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
     const int k = tile * kRowsPerWave + j;
@@ -1757,7 +1766,11 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
     f32x4 res[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) res[t] = od[t];
+#ifdef MSW_ROW_FILT_LDS
+    apply_filter<NT>(res, agg, a.filt_a >= 0 ? 0 : -1, wl, ln);
+#else
     apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+#endif
     if (valid) store_row<NT>(a.out + n * F, res, NT, g);
   }
 }

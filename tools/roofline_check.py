@@ -1,16 +1,23 @@
 """Cross-check bench.py's live roofline timing against the rocprofv3 kernel trace of the
-same command: bench.py times `iters` back-to-back launches of one kernel with HIP events
+same command: bench.py times back-to-back launches of one kernel with HIP events
 (msw_bench_kernel); this finds those runs in the trace (>= 20 consecutive launches of one
 kernel name) and reports their average duration and their launch-to-launch period (what
 the HIP events measure: duration + boundary).
 
-    python tools/roofline_check.py gpurun_out/prof/run_kernel_trace.csv
+    python tools/roofline_check.py gpurun_out/prof/run_kernel_trace.csv [--json out.json]
+
+--json: the runs in bench.py's order (default workload: finest middle hop, fused edge MLP +
+hop, pooling; then the ~1M-node mesh's middle hop and edge MLP + hop), named by role -- the
+file bench.py reads into `roofline.rocprof` (profiles/roofline_rocprof.json).
 """
 import csv
+import json
 import sys
 
+ROLES = ["hop", "edge_hop", "pool", "hop_large", "edge_hop_large"]
 
-def main(path):
+
+def runs_of(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     runs, i = [], 0
     while i < len(rows):
@@ -20,13 +27,28 @@ def main(path):
         if j - i + 1 >= 20:
             runs.append(rows[i:j + 1])
         i = j + 1
+    out = []
     for run in runs:
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in run]
         span = (int(run[-1]["End_Timestamp"]) - int(run[0]["Start_Timestamp"])) / 1e3
         grid = run[0].get("Grid_Size", run[0].get("Grid_Size_X", "?"))
-        print(f"{run[0]['Kernel_Name'][:60]:60s} grid={grid:>8} launches={len(run):4d} "
-              f"avg duration {sum(d) / len(d):9.2f} us  period {span / len(run):9.2f} us")
+        out.append({"kernel": run[0]["Kernel_Name"].split("(")[0].replace("void msw::", ""), "grid": grid,
+                    "launches": len(run), "avg_duration_us": sum(d) / len(d), "period_us": span / len(run)})
+    return out
+
+
+def main(argv):
+    path = argv[1]
+    runs = runs_of(path)
+    for r in runs:
+        print(f"{r['kernel'][:60]:60s} grid={r['grid']:>8} launches={r['launches']:4d} "
+              f"avg duration {r['avg_duration_us']:9.2f} us  period {r['period_us']:9.2f} us")
+    if "--json" in argv:
+        out = argv[argv.index("--json") + 1]
+        with open(out, "w") as f:
+            json.dump({"source": path, "runs": runs,
+                       "by_role": {ROLES[i]: r for i, r in enumerate(runs[:len(ROLES)])}}, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv)
