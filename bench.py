@@ -443,14 +443,14 @@ def main():
         from mswegnn.rollout import apply_boundary_condition, use_prediction
         dyn = model.previous_t * model.NUM_WATER_VARS
 
-        def rollout():  # training/train.py:87-95 verbatim semantics, model(temp) -> msw_forward
+        def rollout(fwd=model):  # training/train.py:87-95 verbatim semantics, model(temp) -> msw_forward
             temp = g.clone()
             preds = []
             with torch.no_grad():
                 for t in range(T):
                     temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, t],
                                                                 temp.node_BC, type_BC=temp.type_BC)
-                    pred = model(temp)
+                    pred = fwd(temp)
                     temp.x = use_prediction(temp.x, pred, model.previous_t)
                     preds.append(pred)
             return torch.stack(preds, -1)
@@ -484,6 +484,24 @@ def main():
         dist.all_reduce(tn, op=dist.ReduceOp.SUM)
         nodes_all = float(tn.item())
     value = nodes_all * T * args.steps / dt
+
+    caller_overhead = None
+    if args.caller == "reference-loop" and world == 1:
+        # the caller's own cost: the same loop with the model replaced by a stub that returns a
+        # fresh [N, 2] tensor (no GPU work): its index_put / slice copy / cat kernels and its
+        # per-step host synchronisation (check_type_BC reads the GPU tensor type_BC)
+        def stub(temp):
+            return torch.zeros(temp.x.shape[0], 2, device=temp.x.device)
+        rollout(stub)
+        torch.cuda.synchronize()
+        c0 = time.perf_counter()
+        for _ in range(3):
+            rollout(stub)
+        torch.cuda.synchronize()
+        tc = (time.perf_counter() - c0) / 3
+        caller_overhead = {"ms_per_rollout": tc * 1e3, "us_per_step": tc / T * 1e6,
+                           "note": "the reference loop with a no-op model (stub returning zeros): "
+                                   "what the caller itself costs per step"}
 
     strong = part_check = None
     if world > 1:
@@ -688,6 +706,8 @@ def main():
                                             "edge-encoder inputs / outputs kept for the per-rollout "
                                             "recompute of the edge terms"},
         }
+        if caller_overhead is not None:
+            result["caller_overhead"] = caller_overhead
         if world > 1:
             result["strong_scaling"] = strong
             result["partitioned_rollout_rccl"] = part_check

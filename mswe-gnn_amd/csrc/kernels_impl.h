@@ -1707,12 +1707,33 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
 #endif
+#ifdef MSW_ROW_PIPE
+  // the next tile's CSR offsets are loaded while this tile computes: per tile the dependent
+  // chain is edge records -> rows instead of offsets -> edge records -> rows
+  int pq0, pq1;
+  {
+    const int k = (blockIdx.x * kRowHopWaves + w) * kRowsPerWave + (threadIdx.x & 15);
+    const int kc = k < a.nrows ? k : 0;
+    pq0 = a.rptr[kc];
+    pq1 = k < a.nrows ? a.rptr[kc + 1] : pq0;
+  }
+#endif
   for (int tile = blockIdx.x * kRowHopWaves + w; tile < ntile; tile += stride) {
     const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
     const int k = tile * kRowsPerWave + j;
     const bool valid = k < a.nrows;
     const int kc = valid ? k : 0;
+#ifdef MSW_ROW_PIPE
+    const int q0 = pq0, q1 = pq1;
+    {
+      const int kn = (tile + stride) * kRowsPerWave + j;
+      const int knc = kn < a.nrows ? kn : 0;
+      pq0 = a.rptr[knc];
+      pq1 = kn < a.nrows ? a.rptr[knc + 1] : pq0;
+    }
+#else
     const int q0 = a.rptr[kc], q1 = valid ? a.rptr[kc + 1] : q0;
+#endif
     const size_t n = (size_t)a.n0 + kc;
     f32x4 od[NT];
     load_row<NT>(od, a.in + n * F, g);

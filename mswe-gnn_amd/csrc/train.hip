@@ -91,6 +91,7 @@ struct GemmArgs {
 __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
   __shared__ float As[kBK][kBM + 4];
   __shared__ float Bs[kBK][kBN + 4];
+  constexpr int UA = (kBM * kBK) / kGemmThreads, UB = (kBN * kBK) / kGemmThreads;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int m0 = blockIdx.x * kBM, n0 = blockIdx.y * kBN;
   const int kb = a.part ? blockIdx.z * a.kchunk : 0;
@@ -103,22 +104,42 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool a_mfast = a.lam == 1 && a.lak != 1;  // A stored m-contiguous (transposed operand)
   const bool b_kfast = a.lbk == 1 && a.lbn != 1;  // B stored k-contiguous
+  // per thread: its UA + UB tile elements (fixed positions), the next slice's values in
+  // registers while the current slice is multiplied out of LDS (global latency hidden)
+  int am[UA], ak[UA], bn[UB], bk[UB];
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int idx = tid + u * kGemmThreads;
+    am[u] = a_mfast ? idx % kBM : idx / kBK;
+    ak[u] = a_mfast ? idx / kBM : idx % kBK;
+  }
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    const int idx = tid + u * kGemmThreads;
+    bn[u] = b_kfast ? idx / kBK : idx % kBN;
+    bk[u] = b_kfast ? idx % kBK : idx / kBN;
+  }
+  float ra[UA], rb[UB];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < UA; ++u) {
+      const int m = m0 + am[u], k = k0 + ak[u];
+      ra[u] = (m < a.M && k < ke) ? a.A[(long)m * a.lam + (long)k * a.lak] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int n = n0 + bn[u], k = k0 + bk[u];
+      rb[u] = (n < a.N && k < ke) ? a.B[(long)k * a.lbk + (long)n * a.lbn] : 0.f;
+    }
+  };
+  if (kb < ke) fetch(kb);
   for (int k0 = kb; k0 < ke; k0 += kBK) {
 #pragma unroll
-    for (int u = 0; u < (kBM * kBK) / kGemmThreads; ++u) {
-      const int idx = tid + u * kGemmThreads;
-      const int mm = a_mfast ? idx % kBM : idx / kBK, kk = a_mfast ? idx / kBM : idx % kBK;
-      const int m = m0 + mm, k = k0 + kk;
-      As[kk][mm] = (m < a.M && k < ke) ? a.A[(long)m * a.lam + (long)k * a.lak] : 0.f;
-    }
+    for (int u = 0; u < UA; ++u) As[ak[u]][am[u]] = ra[u];
 #pragma unroll
-    for (int u = 0; u < (kBN * kBK) / kGemmThreads; ++u) {
-      const int idx = tid + u * kGemmThreads;
-      const int nn = b_kfast ? idx / kBK : idx % kBN, kk = b_kfast ? idx % kBK : idx / kBN;
-      const int n = n0 + nn, k = k0 + kk;
-      Bs[kk][nn] = (n < a.N && k < ke) ? a.B[(long)k * a.lbk + (long)n * a.lbn] : 0.f;
-    }
+    for (int u = 0; u < UB; ++u) Bs[bk[u]][bn[u]] = rb[u];
     __syncthreads();
+    if (k0 + kBK < ke) fetch(k0 + kBK);
 #pragma unroll
     for (int k4 = 0; k4 < kBK; k4 += 4) {
       const int kr = k4 + (lane >> 4);
@@ -155,12 +176,24 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
       }
 }
 
-// out[i] = sum_{s < splits} part[s][i] (in order), i < count
-__global__ void k_sum_splits(const float* __restrict__ part, int splits, long count, float* __restrict__ out) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+// out[i] = sum_{s < splits} part[s][i], i < count.  A 256-thread workgroup owns 64 outputs;
+// row group p (of 4) adds splits p, p + 4, ... in order, then the 4 partials are added in
+// order through LDS (fixed order: deterministic)
+__global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ part, int splits, long count,
+                                                    float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
+  for (long i0 = blockIdx.x * 64L; i0 < count; i0 += gridDim.x * 64L) {
+    const long i = i0 + c;
     float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += part[(long)s * count + i];
-    out[i] = v;
+    if (i < count) {
+#pragma unroll 8
+      for (int s = p; s < splits; s += 4) v += part[(long)s * count + i];
+    }
+    red[p][c] = v;
+    __syncthreads();
+    if (p == 0 && i < count) out[i] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    __syncthreads();
   }
 }
 
@@ -333,13 +366,28 @@ __global__ __launch_bounds__(256) void k_act_bwd(const float* __restrict__ pre, 
   if (threadIdx.x == 0 && spart) spart[blockIdx.x] = red[0];
 }
 
-// column sums of X [R][W] over row slice blockIdx.x -> part[blockIdx.x][W]
-__global__ void k_colsum(const float* __restrict__ X, long R, int W, long rchunk, float* __restrict__ part) {
+// column sums of X [R][W] over row slice blockIdx.x -> part[blockIdx.x][W]: thread t sums
+// column t % W over rows t / W, t / W + P, ... (P = 256 / W row lanes), then the P partials
+// are added in order through LDS (deterministic)
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ X, long R, int W, long rchunk,
+                                                float* __restrict__ part) {
+  __shared__ float red[256];
   const long r0 = blockIdx.x * rchunk, r1 = min(R, r0 + rchunk);
-  for (int c = threadIdx.x; c < W; c += blockDim.x) {
+  for (int c0 = 0; c0 < W; c0 += 256) {
+    const int wc = min(256, W - c0);
+    const int P = 256 / wc;
+    const int c = threadIdx.x % wc, rl = threadIdx.x / wc;
     float v = 0.f;
-    for (long r = r0; r < r1; ++r) v += X[r * W + c];
-    part[(long)blockIdx.x * W + c] = v;
+    if (rl < P)
+      for (long r = r0 + rl; r < r1; r += P) v += X[r * W + c0 + c];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    if ((int)threadIdx.x < wc) {
+      float sacc = 0.f;
+      for (int p = 0; p < P; ++p) sacc += red[p * wc + threadIdx.x];
+      part[(long)blockIdx.x * W + c0 + threadIdx.x] = sacc;
+    }
+    __syncthreads();
   }
 }
 
@@ -455,12 +503,12 @@ hipError_t weight_grad(const float* A, int lda, const float* B, int ldb, long R,
   g.A = A; g.lam = 1; g.lak = lda;
   g.B = B; g.lbk = ldb; g.lbn = 1;
   g.part = part;
-  const int splits = (int)std::min<long>(kMaxSplits, std::max<long>(1, R / 1024));
+  const int splits = (int)std::min<long>(kMaxSplits, std::max<long>(1, R / (8 * kBK)));
   hipError_t e = gemm(g, st, splits);
   if (e != hipSuccess) return e;
   const int kchunk = ((g.K + splits - 1) / splits + kBK - 1) / kBK * kBK;
   const int used = std::max(1, (g.K + kchunk - 1) / kchunk);
-  hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N)), dim3(256), 0, st, part, used, (long)M * N, dW);
+  hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N, 64)), dim3(256), 0, st, part, used, (long)M * N, dW);
   return hipGetLastError();
 }
 
@@ -529,7 +577,7 @@ int msw_swegnn_train_forward(const msw_swegnn_train_desc* d, const float* xs, co
   }
   for (int k = 0; k < d->K; ++k) {
     const float* ok = saved + y.outk + (long)k * N * F;
-    float* on = saved + y.outk + (long)(k + 1) * N * F;
+    float* on = k + 1 == d->K ? out : saved + y.outk + (long)(k + 1) * N * F;  // out_K is not needed later
     float* agg = saved + y.agg + (long)k * N * F;
     int* nz = reinterpret_cast<int*>(saved + y.nz + (long)k * N);
     hipLaunchKernelGGL(k_node_nz, dim3(blocks_for(N)), dim3(256), 0, st, ok, F, N, nz);
@@ -549,7 +597,6 @@ int msw_swegnn_train_forward(const msw_swegnn_train_desc* d, const float* xs, co
       TRY(hipGetLastError());
     }
   }
-  TRY(hipMemcpyAsync(out, saved + y.outk + (long)d->K * N * F, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
   return MSW_OK;
 }
 
@@ -565,13 +612,13 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, c
   hipStream_t st = (hipStream_t)stream;
   const long E = d->num_edges, N = d->num_nodes;
   const int F = d->F;
-  float* G = scratch + y.G0;
-  float* Gn = scratch + y.G1;
+  const float* G = grad_out;  // read-only: the first hop's transpose writes G1
+  float* Gbuf[2] = {scratch + y.G0, scratch + y.G1};
+  int gi = 0;
   float* dagg = scratch + y.dagg;
   float* t = scratch + y.t;
   float* ds = scratch + y.ds;
   float* part = scratch + y.part;
-  TRY(hipMemcpyAsync(G, grad_out, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
   if (E > 0) TRY(hipMemsetAsync(ds, 0, sizeof(float) * E * F, st));
   for (int k = d->K - 1; k >= 0; --k) {
     const float* ok = saved + y.outk + (long)k * N * F;
@@ -585,18 +632,19 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, c
       g.B = d->filter[k + 1]; g.lbk = F; g.lbn = 1;
       g.C = dagg; g.ldc = F;
       TRY(gemm(g, st));
-    } else {
-      TRY(hipMemcpyAsync(dagg, G, sizeof(float) * N * F, hipMemcpyDeviceToDevice, st));
     }
+    const float* dg = d->with_filter_matrix ? dagg : G;  // no filter: dagg = G
     if (E > 0) {
       hipLaunchKernelGGL(k_edge_bwd, dim3(blocks_for(E * F)), dim3(256), 0, st, d->row, d->col, ok, saved + y.s, nz,
-                         dagg, F, E, d->with_gradient, d->upwind_mode, ds, t);
+                         dg, F, E, d->with_gradient, d->upwind_mode, ds, t);
       TRY(hipGetLastError());
     }
+    float* Gn = Gbuf[gi];
+    gi ^= 1;
     hipLaunchKernelGGL(k_node_bwd, dim3(blocks_for(N * F)), dim3(256), 0, st, d->in_ptr, d->in_edge, d->out_ptr,
                        d->out_edge, G, t, F, N, d->with_gradient, Gn);
     TRY(hipGetLastError());
-    std::swap(G, Gn);
+    G = Gn;
   }
   // out_0 = W_0 x_d
   if (d->with_filter_matrix) {
@@ -625,7 +673,7 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, c
   hipLaunchKernelGGL(k_normalize_bwd, dim3(blocks_for(E)), dim3(256), 0, st, saved + y.s, saved + y.nrm, ds, F, E,
                      d->normalize, dcur);
   TRY(hipGetLastError());
-  const long rchunk = std::max<long>(1024, (E + kMaxSplits - 1) / kMaxSplits);
+  const long rchunk = std::max<long>(256, (E + kMaxSplits - 1) / kMaxSplits);
   const int nrs = (int)((E + rchunk - 1) / rchunk);
   for (int l = y.L - 1; l >= 0; --l) {
     const int wi = y.w[l], wo = y.w[l + 1];
@@ -634,12 +682,12 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, c
                        d->slope[l], dpre, scratch + y.spart);
     TRY(hipGetLastError());
     if (gr->d_slope[l]) {
-      hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(64), 0, st, scratch + y.spart, ab, 1L, gr->d_slope[l]);
+      hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, st, scratch + y.spart, ab, 1L, gr->d_slope[l]);
       TRY(hipGetLastError());
     }
     if (gr->d_bias[l]) {
       hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, E, wo, rchunk, part);
-      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo)), dim3(256), 0, st, part, nrs, (long)wo, gr->d_bias[l]);
+      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo, 64)), dim3(256), 0, st, part, nrs, (long)wo, gr->d_bias[l]);
       TRY(hipGetLastError());
     }
     const float* Xl = l == 0 ? saved + y.X0 : saved + y.post[l - 1];
