@@ -642,24 +642,30 @@ def test_speculative_forward_replans_on_weight_change(monkeypatch):
 
 def test_flip_localisation_rules():
     """conftest.flip_localisation (the config-3 mask-flip exception, verdict r2): accepts a
-    divergence that starts at the reference's own flip cell, rejects one elsewhere."""
+    divergence that is a depth-mask flip at or after the reference's own flip, rejects one
+    that is not a flip or that starts earlier."""
     from conftest import flip_localisation
-    N, T = 50, 6
+    N, T = 50, 7
     g = torch.Generator().manual_seed(0)
     r64 = torch.rand(N, 2, T, generator=g, dtype=torch.float64) + 0.5
     r64[7, 0, 3] = 1.00002e-4          # fp64: just above the threshold -> kept
     ref = r64.clone().float().double()
-    ref[7, :, 3] = 0.0                 # fp32 reference: masked (h and v)
-    ref[:, :, 4:] += 0.01              # the flip propagates
-    ours = r64.clone()
-    ours[:, :, 4:] += 0.02             # ours stays on the fp64 side, diverges later
+    ref[7, :, 3] = 0.0                 # fp32 reference: masked (h and v) at step 3
+    ref[:, :, 5:] += 0.01              # the flip propagates
+    ours = ref.clone()                 # ours flips like the reference at step 3 ...
+    ref[9, 0, 4] = 1.00001e-4          # ... and a second near-threshold cell at step 4:
+    ours[9, :, 4] = 0.0                # ours masks it, the reference does not
+    ours[:, :, 5:] += 0.02
     t, cells = flip_localisation(ours, ref, r64)
-    assert (t, cells) == (3, [7])
+    assert (t, cells) == (4, [9])
+    ours_fp64 = r64.clone()            # ours on the fp64 side of the first flip
+    ours_fp64[:, :, 5:] += 0.5
+    assert flip_localisation(ours_fp64, ref, r64) == (3, [7])
     bad = ours.clone()
-    bad[11, 1, 3] += 0.5               # another cell diverging at the same step
+    bad[11, 1, 4] += 0.5               # another cell diverging without a mask flip
     with pytest.raises(AssertionError):
         flip_localisation(bad, ref, r64)
     early = ours.clone()
-    early[2, 0, 1] += 0.5              # divergence before the flip
+    early[2, 0, 1] = 0.0               # divergence before the reference's flip
     with pytest.raises(AssertionError):
         flip_localisation(early, ref, r64)

@@ -50,7 +50,12 @@ def main():
         # bench.py's large-mesh roofline (config 5): the middle hop (LAST = false, the third
         # template argument) moving the most bytes per launch (grid-stride launches have
         # capped grids, so the grid size does not identify it)
-        mids = [(kk, vv) for kk, vv in hops if kk.split("<")[1].split(",")[2].strip() == "false"]
+        def middle(kk):  # k_hop_rows (row layout) is a middle hop; k_hop<NT, ACT, LAST, LOOP>
+            if kk.startswith("k_hop_rows"):
+                return True
+            args = kk.split("<")[1].split(">")[0].split(",")
+            return kk.startswith("k_hop<") and len(args) >= 3 and args[2].strip() == "false"
+        mids = [(kk, vv) for kk, vv in hops if middle(kk)]
         kl, vl = max(mids or hops, key=lambda kv: kv[1]["hbm_bytes_per_launch"] or 0)
         res["k_hop_large"] = dict(vl, kernel=kl)
     # bench.py's large-mesh edge-MLP roofline: the grid-stride fused edge MLP + hop without an

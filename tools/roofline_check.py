@@ -32,7 +32,8 @@ def runs_of(path):
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in run]
         span = (int(run[-1]["End_Timestamp"]) - int(run[0]["Start_Timestamp"])) / 1e3
         grid = run[0].get("Grid_Size", run[0].get("Grid_Size_X", "?"))
-        out.append({"kernel": run[0]["Kernel_Name"].split("(")[0].replace("void msw::", ""), "grid": grid,
+        out.append({"kernel": run[0]["Kernel_Name"].split("(")[0].replace("void msw::", "").replace("msw::", ""),
+                    "grid": grid,
                     "launches": len(run), "avg_duration_us": sum(d) / len(d), "period_us": span / len(run)})
     return out
 
@@ -45,9 +46,10 @@ def main(argv):
               f"avg duration {r['avg_duration_us']:9.2f} us  period {r['period_us']:9.2f} us")
     if "--json" in argv:
         out = argv[argv.index("--json") + 1]
+        ours = [r for r in runs if r["kernel"].startswith("k_")]  # engine kernels only
         with open(out, "w") as f:
             json.dump({"source": path, "runs": runs,
-                       "by_role": {ROLES[i]: r for i, r in enumerate(runs[:len(ROLES)])}}, f, indent=1)
+                       "by_role": {ROLES[i]: r for i, r in enumerate(ours[:len(ROLES)])}}, f, indent=1)
 
 
 if __name__ == "__main__":
