@@ -172,7 +172,9 @@ def flip_localisation(ours, ref, r64, thr=1e-4):
     the fp32 reference, exact fp64 arithmetic).  Asserts that
       * the fp32 reference itself leaves fp64 arithmetic (rel > REL_TOL) at some step t_ref,
         by a mask flip: at its first divergent step every cell where it differs from fp64 has
-        one depth exactly 0 and the other within rounding above the 1e-4 threshold;
+        one depth exactly 0 and the other within rounding above the 1e-4 threshold, or both
+        depths 0 and one velocity exactly 0 (v * (h != 0) on the unmasked depth: ReLU gave
+        exactly 0 on one side, a positive sub-threshold depth on the other);
       * ours does not leave the fp32 reference before t_ref;
       * at the first step where ours leaves the fp32 reference, every cell where they differ
         is such a flip between ours and the reference (their inputs still agree to 1e-4, so
@@ -194,10 +196,17 @@ def flip_localisation(ours, ref, r64, thr=1e-4):
         assert cells, f"{what}: no cell diverges at step {t}"
         for n in cells:
             ha, hb = a[n, 0, t].item(), b[n, 0, t].item()
+            va, vb = a[n, 1, t].item(), b[n, 1, t].item()
             lo, hi = sorted((abs(ha), abs(hb)))
-            assert lo == 0.0 and thr < hi <= thr * (1 + 1e-3), \
-                f"{what}: cell {n} at step {t}: depths {ha!r} / {hb!r}, velocities " \
-                f"{a[n, 1, t].item()!r} / {b[n, 1, t].item()!r} are not a mask flip"
+            # (a) the depth mask h * (|h| > 1e-4) flipped: one depth exactly 0, the other within
+            #     rounding above the threshold; (b) the velocity mask v * (h != 0) flipped on the
+            #     UNMASKED depth: both depths come out 0 (ReLU gave exactly 0 on one side, a
+            #     sub-threshold positive depth on the other), one velocity exactly 0
+            depth_flip = lo == 0.0 and thr < hi <= thr * (1 + 1e-3)
+            vel_flip = ha == 0.0 and hb == 0.0 and min(abs(va), abs(vb)) == 0.0 and max(abs(va), abs(vb)) > 0.0
+            assert depth_flip or vel_flip, \
+                f"{what}: cell {n} at step {t}: depths {ha!r} / {hb!r}, velocities {va!r} / {vb!r} " \
+                f"are not a mask flip"
         return cells
     t_ref, t_ours = first_step(ref, r64), first_step(ours, ref)
     assert t_ref is not None, "the fp32 reference does not leave fp64 arithmetic"

@@ -669,3 +669,8 @@ def test_flip_localisation_rules():
     early[2, 0, 1] = 0.0               # divergence before the reference's flip
     with pytest.raises(AssertionError):
         flip_localisation(early, ref, r64)
+    # the velocity mask v * (h != 0) on the unmasked depth (config-3 member 0, step 44): both
+    # depths 0, the fp32 velocity 0, the fp64 one 0.011
+    r64v = r64.clone()
+    r64v[7, :, 3] = torch.tensor([0.0, 0.011], dtype=torch.float64)
+    assert flip_localisation(r64v, ref, r64v) == (3, [7])
