@@ -10,11 +10,23 @@ import torch
 
 
 class Data:
-    """Attribute bag standing in for torch_geometric.data.Data."""
+    """Attribute bag standing in for torch_geometric.data.Data.  As in PyG, the standard
+    attributes (x, edge_index, edge_attr, y, pos, ...) read as None when absent, and
+    ``data['key']`` is attribute access."""
+
+    _PYG_ATTRS = ("x", "edge_index", "edge_attr", "edge_weight", "y", "pos", "batch", "face", "normal")
 
     def __init__(self, **kwargs):
         for k, v in kwargs.items():
             setattr(self, k, v)
+
+    def __getattr__(self, key):  # only called for missing attributes
+        if key in Data._PYG_ATTRS:
+            return None
+        raise AttributeError(f"'{type(self).__name__}' object has no attribute '{key}'")
+
+    def __getitem__(self, key):
+        return getattr(self, key)
 
     def keys(self):
         return [k for k in self.__dict__.keys() if not k.startswith('_')]
@@ -67,6 +79,8 @@ class Batch(Data):
         return len(self._data_list)
 
     def __getitem__(self, i):
+        if isinstance(i, str):
+            return getattr(self, i)
         return self._data_list[i]
 
     def clone(self):

@@ -132,6 +132,25 @@ def batch_model(spec):
             orc.msgnn_config(num_scales=spec["S"], hid_features=spec["F"], K=spec["K"]))
 
 
+def ingest_samples():
+    """The samples of fx_ingest (oracle/gen_golden_ingest.py): raw simulations in the pickled
+    dataset layout, prepared by the REFERENCE's own get_scalers / create_data_attr /
+    to_temporal_dataset -> [(Graph, T, reference rollout)], plus the reference's rollout of
+    the 2-graph Batch."""
+    from mswegnn.mesh import Graph
+    fx = golden("fx_ingest")
+    out = []
+    for i in range(int(fx["num_samples"])):
+        g = {k: torch.from_numpy(fx[f"s{i}_{k}"]) for k in ("x", "edge_index", "edge_attr", "edge_ptr", "node_ptr",
+                                                             "intra_mesh_edge_index", "intra_edge_ptr", "BC",
+                                                             "node_BC")}
+        T = int(fx[f"s{i}_T"])
+        gr = Graph(**g, type_BC=torch.tensor(int(fx[f"s{i}_type_BC"])), y=torch.zeros(g["x"].shape[0], 2, T),
+                   temporal_res=torch.tensor(120), previous_t=torch.tensor(3))
+        out.append((gr, T, torch.from_numpy(fx[f"s{i}_rollout"])))
+    return out, torch.from_numpy(fx["batch_rollout"])
+
+
 def oracle_fp64_rollout(P, cfg, g, T):
     """The oracle in float64 (weights, inputs and arithmetic): the exact-arithmetic yardstick
     for rollouts whose fp32 result is itself sensitive to rounding."""

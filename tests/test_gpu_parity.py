@@ -688,3 +688,39 @@ def test_row_layout_hops_match_edge_tiles(cuda, monkeypatch, S, F, K, ck):
         outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
         plan.close()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("mode", ["fused", "stepped"])
+def test_ingested_dataset_vs_reference(cuda, mode):
+    """§8 f4 ingest: the reference's own dataset pipeline (get_scalers -> create_data_attr ->
+    to_temporal_dataset, config.yaml settings; oracle/gen_golden_ingest.py) prepared
+    simulations in its pickled-dataset layout; the HIP engine's rollout of those arrays -- each
+    sample and the 2-graph batch, through rollout_test (fused) or the reference's step loop
+    (one graph-replayed msw_forward per step) -- matches the reference's rollouts."""
+    from conftest import ingest_samples
+    from mswegnn.batch import collate
+    from mswegnn.rollout import (adapt_batch_training, apply_boundary_condition, rollout_test, split_rollout,
+                                 use_prediction)
+    samples, rb = ingest_samples()
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+
+    def run(graph):
+        if mode == "fused":
+            return rollout_test(m, graph)
+        temp = adapt_batch_training(graph).clone() if hasattr(graph, "num_graphs") else graph.clone()
+        preds = []
+        with torch.no_grad():
+            for t in range(graph.y.shape[-1]):
+                temp.x[:, -6:] = apply_boundary_condition(temp.x[:, -6:], temp.BC[:, :, t], temp.node_BC,
+                                                          type_BC=temp.type_BC)
+                p = m(temp)
+                temp.x = use_prediction(temp.x, p, 3)
+                preds.append(p)
+        return torch.stack(preds, -1)
+    for g, T, ref in samples:
+        r = run(g.to(cuda)).cpu()
+        assert per_step_rel(r, ref) <= REL_TOL, per_step_rel(r, ref)
+    b = collate([g for g, _, _ in samples])
+    r = run(b.to(cuda)).cpu()
+    for p, q in zip(split_rollout(r, b), split_rollout(rb, b)):
+        assert per_step_rel(p, q) <= REL_TOL

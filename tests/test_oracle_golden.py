@@ -131,3 +131,22 @@ def test_oracle_upwind_mode_and_seeded_init():
     m = build_msgnn(3, 32, 2)
     r = orc.rollout(state_dict_of(m), cfg, g)
     assert_pinned(r, torch.from_numpy(fx["rollout"]))
+
+
+def test_oracle_on_reference_ingested_dataset():
+    """fx_ingest: simulations in the reference's pickled-dataset layout prepared by the
+    REFERENCE's own ingest (get_scalers, create_data_attr, to_temporal_dataset with config.yaml's
+    dataset settings) and rolled out by its rollout_test (K4_F32, full 48-step test horizon);
+    the oracle on the ingested arrays reproduces it, single graphs and the 2-graph batch."""
+    from conftest import ingest_samples
+    from mswegnn.batch import collate
+    from mswegnn.rollout import adapt_batch_training
+    samples, rb = ingest_samples()
+    P = weights("K4_F32")
+    cfg = orc.msgnn_config(num_scales=4, hid_features=32, K=4)
+    for g, T, ref in samples:
+        assert T == 48 and g.x.shape[1] == 8
+        assert_pinned(orc.rollout(P, cfg, g, T), ref)
+    b = adapt_batch_training(collate([g for g, _, _ in samples]))
+    r = orc.rollout(P, cfg, b, samples[0][1])
+    assert per_step_rel(r, rb) <= 1e-5  # batched CPU GEMMs block rows differently
