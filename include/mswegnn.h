@@ -294,6 +294,36 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* desc, const float* x_
                               const float* edge_attr, const float* saved, const float* grad_out,
                               const msw_swegnn_grads* grads, float* scratch, void* stream);
 
+/* ---- Training: autograd through one make_mlp stack --------------------------
+ * Replaces the autograd of a make_mlp Sequential (models/models.py:121-146: Linear + activation
+ * after every layer, no dropout / layer norm) -- the model's edge / node encoders and node
+ * decoder (models/gnn.py:204-215, 239-240) -- in training_step (training/train.py:125-145). */
+typedef struct {
+  int64_t rows;
+  int32_t n_layers;                      /* 1..MSW_MAX_MLP_LAYERS */
+  int32_t width[MSW_MAX_MLP_LAYERS + 1]; /* width[0] = input features, width[n_layers] = output */
+  int32_t act[MSW_MAX_MLP_LAYERS];       /* enum msw_activation after each layer */
+  const float* weight[MSW_MAX_MLP_LAYERS]; /* [width[l+1]][width[l]] */
+  const float* bias[MSW_MAX_MLP_LAYERS];   /* NULL = bias=False */
+  const float* slope[MSW_MAX_MLP_LAYERS];  /* device scalar (PReLU) or NULL */
+} msw_mlp_train_desc;
+
+/* Gradient outputs (device; written, not accumulated); NULL skips that gradient. */
+typedef struct {
+  float* d_x;
+  float* d_weight[MSW_MAX_MLP_LAYERS];
+  float* d_bias[MSW_MAX_MLP_LAYERS];
+  float* d_slope[MSW_MAX_MLP_LAYERS];
+} msw_mlp_grads;
+
+int msw_mlp_train_workspace(const msw_mlp_train_desc* desc, int64_t* saved_floats, int64_t* scratch_floats);
+/* out [rows][width[n_layers]] = MLP(x [rows][width[0]]); `saved` receives every layer's
+ * pre-activation and the hidden layers' outputs. */
+int msw_mlp_train_forward(const msw_mlp_train_desc* desc, const float* x, float* saved, float* out, void* stream);
+/* Gradients of the input and the parameters given grad_out and the forward's `saved`. */
+int msw_mlp_train_backward(const msw_mlp_train_desc* desc, const float* x, const float* saved,
+                           const float* grad_out, const msw_mlp_grads* grads, float* scratch, void* stream);
+
 /* Diagnostics: route per-phase timestamps of wave 0 of workgroup 0 of every launch to the
  * device buffer `buf` (uint64[20]: {shader clock, 100 MHz clock} for phase marks 0..9).
  * Only builds compiled with -DMSW_TRACE record anything; NULL disables. */

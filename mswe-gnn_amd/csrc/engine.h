@@ -185,6 +185,9 @@ struct EdgeHopArgs {
   Epilogue epi;
   int coop;                        // waves per tile (k_edge_coop: MFMA output tiles split
                                    // across them), 0/1 = one wave per tile
+  int pipe;                        // k_edge_mlp: software-pipelined variant (k_edge_mlp_pipe)
+  int wdirect;                     // k_edge_coop4: read the MLP region from its blob copy
+                                   // (c.W + reg.off) instead of staging it in LDS
   int* step_inc;                   // rollout mode, first edge-MLP launch of a step:
                                    // &RolloutIO::step, advanced once (workgroup 0, lane 0)
   const EdgeChunk* chunks; int nchunks;  // k_edge_mlp: dense 16-edge chunks [nchunks][16]

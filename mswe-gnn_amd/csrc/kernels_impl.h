@@ -1016,6 +1016,92 @@ void k_edge_mlp(EdgeHopArgs a) {
   }
 }
 
+// k_edge_mlp software-pipelined (F = 64, MSW_MLP_PIPE): one wave per SIMD, each wave walks
+// ~2 chunks and issues the next chunk's U / V / Pe gathers (1.5 KB per edge) before the
+// current chunk's MLP (384 MFMAs), so the gathers of chunk n+1 run under the MFMA chain of
+// chunk n instead of every wave of the launch gathering, then multiplying, in lockstep.  Same
+// operations on the same operands as k_edge_mlp: s is bit-identical.
+constexpr int kMlpPipeWaves = 4;
+template <int NT>
+struct MlpFetch {
+  f32x4 u[2 * NT], v[2 * NT], p[2 * NT];
+  int4 e;
+};
+template <int NT>
+__device__ __forceinline__ void mlp_fetch(MlpFetch<NT>& f, const EdgeHopArgs& a, int ch, int j, int g) {
+  constexpr int T2 = 2 * NT;
+  const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  f.e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+  const bool ev = f.e.z >= 0;
+  const float* Ub = a.U + (size_t)(ev ? f.e.x : a.n0) * hs;
+  const float* Vb = a.V + (size_t)(ev ? f.e.y : a.n0) * hs;
+  const float* Pb = a.Pe && ev ? a.Pe + (size_t)f.e.z * hs : z;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    const bool on = t < a.h1t;
+    f.u[t] = ld4((on ? Ub : z) + off);
+    f.v[t] = ld4((on ? Vb : z) + off);
+    f.p[t] = ld4((on ? Pb : z) + off);
+  }
+}
+template <int NT, int ACT>
+__global__ __launch_bounds__(64 * kMlpPipeWaves) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_edge_mlp_pipe(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = wave_id();
+  const int stride = gridDim.x * kMlpPipeWaves;
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
+  const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+  int ch = blockIdx.x * kMlpPipeWaves + w;
+  MlpFetch<NT> f;
+  if (ch < a.nchunks) mlp_fetch<NT>(f, a, ch, j, g);  // in flight during the weight staging
+  const float* Wm = a.c.W;
+  if (a.reg.len > 0) {
+    stage_glds<kMlpPipeWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
+    __syncthreads();
+    Wm = smem;
+  }
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  for (; ch < a.nchunks; ch += stride) {
+    f32x4 H[T2];
+#pragma unroll
+    for (int t = 0; t < T2; ++t) {
+      const f32x4 p = a.Pe ? f.p[t] : ld4(Wm + b1 + 16 * t + 4 * g);
+      H[t] = t < a.h1t ? (f.u[t] + f.v[t]) + p : zero4();
+    }
+    const int4 e = f.e;
+    if (ch + stride < a.nchunks) mlp_fetch<NT>(f, a, ch + stride, j, g);
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 q = sv[t] / nrm;
+        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+        q.y = (q.y == q.y) ? q.y : 0.f;
+        q.z = (q.z == q.z) ? q.z : 0.f;
+        q.w = (q.w == q.w) ? q.w : 0.f;
+        sv[t] = q;
+      }
+    }
+    if (e.z >= 0) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  }
+}
+
 // ---------------------------------------------------------------------------- cooperative edge hop
 // The fused edge MLP + hop with P waves per tile, for scales whose tiles are far fewer than
 // the chip's SIMDs (the MLP chain of one wave is then the launch's critical path): every
@@ -1280,8 +1366,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   EdgeHopRows<NT> q;
   edge_hop_load<NT, LST>(q, a, tile, j, g);
   const Lanes& L = q.L;
-  if (a.reg.len > 0) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
-  const float* Wm = a.reg.len > 0 ? (const float*)smem : c.W;
+  // the MLP region: staged in LDS, or (wdirect: two workgroups per CU) read from its blob copy
+  if (a.reg.len > 0 && !a.wdirect) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
+  const float* Wm = a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W;
   float* my = &slab[j][0];
   if (r == 0) {
     store_row<T2>(my, q.Vn, T2, g);
@@ -2658,6 +2745,15 @@ static const void* edge_hop_kernel(int prelu, bool loop, int last) {
 template <int NT>
 hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st) {
   if (a.nchunks <= 0) return hipSuccess;
+  if (a.pipe) {
+    const int n = cdiv(a.nchunks, kMlpPipeWaves);
+    const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(64 * kMlpPipeWaves);
+    if (a.c.prelu)
+      hipLaunchKernelGGL((k_edge_mlp_pipe<NT, 1>), grid, block, eh_lds_bytes(a.reg.len), st, a);
+    else
+      hipLaunchKernelGGL((k_edge_mlp_pipe<NT, -1>), grid, block, eh_lds_bytes(a.reg.len), st, a);
+    return hipGetLastError();
+  }
   const int n = cdiv(a.nchunks, kMlpWaves);
   const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(64 * kMlpWaves);
   if (a.c.prelu)
@@ -2675,7 +2771,7 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
     EdgeHopArgs b = a;
     const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
     void* args[] = {&b};
-    return hipLaunchKernel(f, grid, dim3(kBlock), args, eh_lds_bytes(a.reg_nf), st);
+    return hipLaunchKernel(f, grid, dim3(kBlock), args, a.wdirect ? 0 : eh_lds_bytes(a.reg_nf), st);
   }
   const bool loop = tile_loop(a);
   EdgeHopArgs b = a;
@@ -2825,6 +2921,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 9: return hop_coop_kernel<NT>(prelu);
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
     case 14: return (const void*)k_hop_rows<NT>;
+    case 15: return prelu ? (const void*)k_edge_mlp_pipe<NT, 1> : (const void*)k_edge_mlp_pipe<NT, -1>;
     default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
   }
 }
@@ -2834,11 +2931,12 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
                  : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
-  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7 || kind == 10 || kind == 12) ? eh_lds_bytes((int)(dyn_bytes / 4))
+  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
   const int block = kind == 4 ? 64 * chain_waves<NT>()
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
+                    : kind == 15 ? 64 * kMlpPipeWaves
                     : kind == 13 ? 64 * 2 * NT
                     : kind == 14 ? 64 * kRowHopWaves
                     : kind == 2 ? 64 * (loop ? hop_waves<NT, true>() : kWaves)

@@ -1007,6 +1007,12 @@ bool row_hops_forced() {
   return e && atoi(e) == 2;
 }
 constexpr long kEncCoopWaves = 4096;
+// MSW_COOP2_DIRECT: 0 never read the two-wave cooperative edge hop's MLP region from the
+// blob, 1 (default) when staging it would cost a second round, 2 always (parity tests)
+int wdirect_mode() {
+  const char* e = getenv("MSW_COOP2_DIRECT");
+  return e ? atoi(e) : 1;
+}
 bool no_loop(const char* kind) {
   const char* e = getenv("MSW_NO_LOOP");
   return e && (strstr(e, kind) || strstr(e, "all"));
@@ -1030,9 +1036,14 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       L.enc.coop = coop ? P->NT : 0;
       break;
     }
-    case L_EDGE_MLP:
-      L.eh.max_blocks = resident_of(P->NT, 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
+    case L_EDGE_MLP: {
+      // MSW_MLP_PIPE=1: one wave per SIMD walking ~2 chunks, the next chunk's gathers in
+      // flight under the current chunk's MLP (k_edge_mlp_pipe)
+      const char* pp = getenv("MSW_MLP_PIPE");
+      L.eh.pipe = pp && atoi(pp) != 0;
+      L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
+    }
     case L_EDGE_HOP: {
       EdgeHopArgs& a = L.eh;
       caps(P, a, 1, a.c.prelu, a.last, a.reg.len);
@@ -1054,9 +1065,21 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // place of four, for tests)
       const int c2 = getenv("MSW_COOP2_F64") ? atoi(getenv("MSW_COOP2_F64")) : 1;
       if (c2 == 2 && a.coop == 4) a.coop = 0;
-      if (P->NT == 4 && !a.coop && !loop && epi_ok && P->coop_w[0] > 0 && 2L * a.ntiles <= P->coop_w[0] && c2 &&
-          (2 * a.ntiles + kWaves - 1) / kWaves <= resident_of(P->NT, 12, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0))
-        a.coop = 2;
+      a.wdirect = 0;
+      if (P->NT == 4 && !a.coop && !loop && epi_ok && P->coop_w[0] > 0 && 2L * a.ntiles <= P->coop_w[0] && c2) {
+        const int need = (2 * a.ntiles + kWaves - 1) / kWaves;
+        const int wd = wdirect_mode();
+        if (need <= resident_of(P->NT, 12, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0)) {
+          a.coop = 2;
+          a.wdirect = wd == 2 && a.reg.len > 0;
+        } else if (wd != 0 && a.reg.len > 0 && need <= resident_of(P->NT, 12, a.c.prelu, a.last, 0, 0)) {
+          // the staged MLP region (96 KB) holds one workgroup per CU: read it from its blob
+          // copy instead, two workgroups per CU, and the grid fits one round (the finest
+          // unpooling of zenodo4_f64: 652 tiles; MSW_COOP2_DIRECT=0 off)
+          a.coop = 2;
+          a.wdirect = 1;
+        }
+      }
       break;
     }
     case L_HOP:
@@ -1556,6 +1579,8 @@ int64_t msw_struct_size(const char* name) {
   if (!strcmp(name, "msw_exchange_desc")) return sizeof(msw_exchange_desc);
   if (!strcmp(name, "msw_swegnn_train_desc")) return sizeof(msw_swegnn_train_desc);
   if (!strcmp(name, "msw_swegnn_grads")) return sizeof(msw_swegnn_grads);
+  if (!strcmp(name, "msw_mlp_train_desc")) return sizeof(msw_mlp_train_desc);
+  if (!strcmp(name, "msw_mlp_grads")) return sizeof(msw_mlp_grads);
   return -1;
 }
 

@@ -1,6 +1,7 @@
-// Autograd through one SWEGNN processor on gfx950 (first slice): the training
-// forward (saving what the backward needs) and the backward of
-//   SWEGNN.forward  models/gnn.py:387-445
+// Autograd through the model's layers on gfx950: the training forward (saving
+// what the backward needs) and the backward of
+//   SWEGNN.forward  models/gnn.py:387-445   (msw_swegnn_train_*)
+//   make_mlp        models/models.py:121-146 (msw_mlp_train_*: encoders gnn.py:204-215, decoder :239-240)
 // as the reference trains it (training_step, training/train.py:125-145).  The reference
 // recomputes s_ij from the active edges of every hop; s_ij depends on the hop only through
 // the mask, so by linearity of the backward ONE MLP backward of ds = sum_k [active_k] ds_k
@@ -482,6 +483,52 @@ bool layout_of(const msw_swegnn_train_desc* d, Layout& y) {
   return true;
 }
 
+struct MlpRun {
+  long R;
+  int L;
+  const int* w;    // widths [L + 1]
+  const int* act;  // [L]
+  const float* const* W;
+  const float* const* b;
+  const float* const* slope;
+};
+
+struct MlpLayout {  // float offsets: saved = pre[0..L-1], post[0..L-2]; scratch = A, B, partials
+  long pre[4], post[4], saved;
+  long A, B, part, spart, scratch;
+  int L, w[5], wmax;
+};
+
+bool mlp_layout_of(const msw_mlp_train_desc* d, MlpLayout& y) {
+  if (!d || d->n_layers < 1 || d->n_layers > 4 || d->rows < 0) return false;
+  const long R = d->rows;
+  y.L = d->n_layers;
+  y.wmax = 0;
+  for (int l = 0; l <= y.L; ++l) {
+    y.w[l] = d->width[l];
+    if (y.w[l] <= 0) return false;
+    y.wmax = std::max(y.wmax, y.w[l]);
+  }
+  for (int l = 0; l < y.L; ++l)
+    if (!d->weight[l]) return false;
+  auto al = [](long n) { return (n + 63) / 64 * 64; };
+  long o = 0;
+  for (int l = 0; l < y.L; ++l) { y.pre[l] = o; o += al(R * y.w[l + 1]); }
+  for (int l = 0; l + 1 < y.L; ++l) { y.post[l] = o; o += al(R * y.w[l + 1]); }
+  y.saved = o;
+  o = 0;
+  y.A = o; o += al(R * y.wmax);
+  y.B = o; o += al(R * y.wmax);
+  y.part = o; o += al((long)kMaxSplits * y.wmax * y.wmax);
+  y.spart = o; o += al(kMaxSplits * 4L);
+  y.scratch = o;
+  return true;
+}
+
+MlpRun mlp_of(const msw_swegnn_train_desc* d, const Layout& y, long rows) {
+  return MlpRun{rows, y.L, y.w, d->act, d->weight, d->bias, d->slope};
+}
+
 hipError_t gemm(const GemmArgs& a0, hipStream_t st, int splits = 1) {
   GemmArgs a = a0;
   dim3 grid((a.M + kBM - 1) / kBM, (a.N + kBN - 1) / kBN, 1);
@@ -510,6 +557,67 @@ hipError_t weight_grad(const float* A, int lda, const float* B, int ldb, long R,
   const int used = std::max(1, (g.K + kchunk - 1) / kchunk);
   hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N, 64)), dim3(256), 0, st, part, used, (long)M * N, dW);
   return hipGetLastError();
+}
+
+// One make_mlp stack (models/models.py:121-146: Linear + activation after every layer) over R
+// rows: the forward saves every layer's pre-activation (and output: the next layer's input),
+// the backward walks the layers in reverse -- activation / PReLU-slope, bias (column sums),
+// weight (split-K) and input gradients.  Shared by the SWEGNN edge MLP and msw_mlp_train_*.
+
+hipError_t mlp_forward(const MlpRun& m, const float* X, float* const* pre, float* const* post, hipStream_t st) {
+  const float* in = X;
+  for (int l = 0; l < m.L; ++l) {
+    GemmArgs g{};
+    g.M = (int)m.R; g.N = m.w[l + 1]; g.K = m.w[l];
+    g.A = in; g.lam = m.w[l]; g.lak = 1;
+    g.B = m.W[l]; g.lbk = 1; g.lbn = m.w[l];  // B(k, n) = W[n][k]
+    g.C = post[l]; g.ldc = m.w[l + 1];
+    g.bias = m.b[l];
+    g.pre = pre[l]; g.ldp = m.w[l + 1];
+    g.act = m.act[l]; g.slope = m.slope[l];
+    hipError_t e = gemm(g, st);
+    if (e != hipSuccess) return e;
+    in = post[l];
+  }
+  return hipSuccess;
+}
+
+// dY [R][w_L] (read-only; may be bufA) -> dX [R][w_0] (null: not needed; may be bufA);
+// bufA / bufB: [R][max width] each; part: split partials; spart: [kMaxSplits]
+hipError_t mlp_backward(const MlpRun& m, const float* X, const float* const* pre, const float* const* post,
+                        const float* dY, float* dX, float* const* dW, float* const* db, float* const* dslope,
+                        float* bufA, float* bufB, float* part, float* spart, hipStream_t st) {
+  const long R = m.R;
+  const long rchunk = std::max<long>(256, (R + kMaxSplits - 1) / kMaxSplits);
+  const int nrs = (int)((R + rchunk - 1) / rchunk);
+  const float* dcur = dY;
+  float* dpre = bufB;
+  for (int l = m.L - 1; l >= 0; --l) {
+    const int wi = m.w[l], wo = m.w[l + 1];
+    const int ab = blocks_for(R * wo) < kMaxSplits ? blocks_for(R * wo) : kMaxSplits;
+    hipLaunchKernelGGL(k_act_bwd, dim3(ab), dim3(256), 0, st, pre[l], dcur, R * wo, m.act[l], m.slope[l], dpre, spart);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (dslope[l]) hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, st, spart, ab, 1L, dslope[l]);
+    if (db[l]) {
+      hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, R, wo, rchunk, part);
+      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo, 64)), dim3(256), 0, st, part, nrs, (long)wo, db[l]);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const float* Xl = l == 0 ? X : post[l - 1];
+    if (dW[l] && (e = weight_grad(dpre, wo, Xl, wi, R, wo, wi, part, dW[l], st)) != hipSuccess) return e;
+    float* tgt = l == 0 ? dX : bufA;
+    if (tgt) {
+      GemmArgs g{};  // d X_l = dpre W_l
+      g.M = (int)R; g.N = wi; g.K = wo;
+      g.A = dpre; g.lam = wo; g.lak = 1;
+      g.B = m.W[l]; g.lbk = wi; g.lbn = 1;
+      g.C = tgt; g.ldc = wi;
+      if ((e = gemm(g, st)) != hipSuccess) return e;
+    }
+    dcur = bufA;
+  }
+  return hipSuccess;
 }
 
 #define TRY(x)                                                                     \
@@ -546,19 +654,13 @@ int msw_swegnn_train_forward(const msw_swegnn_train_desc* d, const float* xs, co
     hipLaunchKernelGGL(k_gather_cat, dim3(blocks_for(E * y.w[0])), dim3(256), 0, st, d->row, d->col, xs, xd, ea, F,
                        d->edge_features, E, X0);
     TRY(hipGetLastError());
-    const float* in = X0;
-    for (int l = 0; l < y.L; ++l) {  // make_mlp: Linear + activation after every layer
-      GemmArgs g{};
-      g.M = (int)E; g.N = y.w[l + 1]; g.K = y.w[l];
-      g.A = in; g.lam = y.w[l]; g.lak = 1;
-      g.B = d->weight[l]; g.lbk = 1; g.lbn = y.w[l];  // B(k, n) = W[n][k]
-      g.C = saved + y.post[l]; g.ldc = y.w[l + 1];
-      g.bias = d->bias[l];
-      g.pre = saved + y.pre[l]; g.ldp = y.w[l + 1];
-      g.act = d->act[l]; g.slope = d->slope[l];
-      TRY(gemm(g, st));
-      in = saved + y.post[l];
+    float* pre[4];
+    float* post[4];
+    for (int l = 0; l < y.L; ++l) {
+      pre[l] = saved + y.pre[l];
+      post[l] = saved + y.post[l];
     }
+    TRY(mlp_forward(mlp_of(d, y, E), X0, pre, post, st));
     hipLaunchKernelGGL(k_normalize, dim3(blocks_for(E)), dim3(256), 0, st, saved + y.post[y.L - 1], F, E, d->normalize,
                        saved + y.s, saved + y.nrm);
     TRY(hipGetLastError());
@@ -673,31 +775,18 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, c
   hipLaunchKernelGGL(k_normalize_bwd, dim3(blocks_for(E)), dim3(256), 0, st, saved + y.s, saved + y.nrm, ds, F, E,
                      d->normalize, dcur);
   TRY(hipGetLastError());
-  const long rchunk = std::max<long>(256, (E + kMaxSplits - 1) / kMaxSplits);
-  const int nrs = (int)((E + rchunk - 1) / rchunk);
-  for (int l = y.L - 1; l >= 0; --l) {
-    const int wi = y.w[l], wo = y.w[l + 1];
-    const int ab = blocks_for(E * wo) < kMaxSplits ? blocks_for(E * wo) : kMaxSplits;
-    hipLaunchKernelGGL(k_act_bwd, dim3(ab), dim3(256), 0, st, saved + y.pre[l], dcur, E * wo, d->act[l],
-                       d->slope[l], dpre, scratch + y.spart);
-    TRY(hipGetLastError());
-    if (gr->d_slope[l]) {
-      hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, st, scratch + y.spart, ab, 1L, gr->d_slope[l]);
-      TRY(hipGetLastError());
+  {
+    const float* pre[4];
+    const float* post[4];
+    for (int l = 0; l < y.L; ++l) {
+      pre[l] = saved + y.pre[l];
+      post[l] = saved + y.post[l];
     }
-    if (gr->d_bias[l]) {
-      hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, E, wo, rchunk, part);
-      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo, 64)), dim3(256), 0, st, part, nrs, (long)wo, gr->d_bias[l]);
-      TRY(hipGetLastError());
-    }
-    const float* Xl = l == 0 ? saved + y.X0 : saved + y.post[l - 1];
-    if (gr->d_weight[l]) TRY(weight_grad(dpre, wo, Xl, wi, E, wo, wi, part, gr->d_weight[l], st));
-    GemmArgs g{};  // d X_l = dpre W_l
-    g.M = (int)E; g.N = wi; g.K = wo;
-    g.A = dpre; g.lam = wo; g.lak = 1;
-    g.B = d->weight[l]; g.lbk = wi; g.lbn = 1;
-    g.C = dcur; g.ldc = wi;
-    TRY(gemm(g, st));
+    float* dW[4] = {gr->d_weight[0], gr->d_weight[1], gr->d_weight[2], gr->d_weight[3]};
+    float* db[4] = {gr->d_bias[0], gr->d_bias[1], gr->d_bias[2], gr->d_bias[3]};
+    float* dsl[4] = {gr->d_slope[0], gr->d_slope[1], gr->d_slope[2], gr->d_slope[3]};
+    TRY(mlp_backward(mlp_of(d, y, E), saved + y.X0, pre, post, dcur, dcur, dW, db, dsl, dcur, dpre, part,
+                     scratch + y.spart, st));
   }
   // dcur = dX0 [E][4F + ef]
   hipLaunchKernelGGL(k_scatter_inputs, dim3(blocks_for(N * F)), dim3(256), 0, st, d->in_ptr, d->in_edge, d->out_ptr,
@@ -708,6 +797,59 @@ int msw_swegnn_train_backward(const msw_swegnn_train_desc* d, const float* xs, c
                        d->edge_features, gr->d_edge_attr);
     TRY(hipGetLastError());
   }
+  return MSW_OK;
+}
+
+int msw_mlp_train_workspace(const msw_mlp_train_desc* d, int64_t* saved_floats, int64_t* scratch_floats) {
+  MlpLayout y;
+  if (!mlp_layout_of(d, y)) return set_error(MSW_ERR_INVALID, "inconsistent MLP training descriptor");
+  if (saved_floats) *saved_floats = y.saved;
+  if (scratch_floats) *scratch_floats = y.scratch;
+  return MSW_OK;
+}
+
+int msw_mlp_train_forward(const msw_mlp_train_desc* d, const float* x, float* saved, float* out, void* stream) {
+  MlpLayout y;
+  if (!mlp_layout_of(d, y)) return set_error(MSW_ERR_INVALID, "inconsistent MLP training descriptor");
+  if (d->rows == 0) return MSW_OK;
+  if (!x || !saved || !out) return set_error(MSW_ERR_INVALID, "null argument");
+  float* pre[4];
+  float* post[4];
+  for (int l = 0; l < y.L; ++l) {
+    pre[l] = saved + y.pre[l];
+    post[l] = l + 1 < y.L ? saved + y.post[l] : out;
+  }
+  TRY(mlp_forward(MlpRun{d->rows, y.L, y.w, d->act, d->weight, d->bias, d->slope}, x, pre, post,
+                  (hipStream_t)stream));
+  return MSW_OK;
+}
+
+int msw_mlp_train_backward(const msw_mlp_train_desc* d, const float* x, const float* saved, const float* grad_out,
+                           const msw_mlp_grads* gr, float* scratch, void* stream) {
+  MlpLayout y;
+  if (!mlp_layout_of(d, y)) return set_error(MSW_ERR_INVALID, "inconsistent MLP training descriptor");
+  if (!gr) return set_error(MSW_ERR_INVALID, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  float* dW[4] = {gr->d_weight[0], gr->d_weight[1], gr->d_weight[2], gr->d_weight[3]};
+  float* db[4] = {gr->d_bias[0], gr->d_bias[1], gr->d_bias[2], gr->d_bias[3]};
+  float* dsl[4] = {gr->d_slope[0], gr->d_slope[1], gr->d_slope[2], gr->d_slope[3]};
+  if (d->rows == 0) {  // no rows: every gradient is zero
+    for (int l = 0; l < y.L; ++l) {
+      if (dW[l]) TRY(hipMemsetAsync(dW[l], 0, sizeof(float) * y.w[l] * y.w[l + 1], st));
+      if (db[l]) TRY(hipMemsetAsync(db[l], 0, sizeof(float) * y.w[l + 1], st));
+      if (dsl[l]) TRY(hipMemsetAsync(dsl[l], 0, sizeof(float), st));
+    }
+    return MSW_OK;
+  }
+  if (!x || !saved || !grad_out || !scratch) return set_error(MSW_ERR_INVALID, "null argument");
+  const float* pre[4];
+  const float* post[4];
+  for (int l = 0; l < y.L; ++l) {
+    pre[l] = saved + y.pre[l];
+    post[l] = l + 1 < y.L ? saved + y.post[l] : nullptr;  // the output is not needed
+  }
+  TRY(mlp_backward(MlpRun{d->rows, y.L, y.w, d->act, d->weight, d->bias, d->slope}, x, pre, post, grad_out,
+                   gr->d_x, dW, db, dsl, scratch + y.A, scratch + y.B, scratch + y.part, scratch + y.spart, st));
   return MSW_OK;
 }
 

@@ -153,10 +153,24 @@ _LAST_PLAN = weakref.WeakKeyDictionary()  # model -> plan of its previous engine
 _TORCH_ONLY = contextvars.ContextVar("mswegnn_torch_only", default=False)
 
 
+def _mlp_call(owner, seq, x):
+    """make_mlp ``seq`` on x: with autograd on a GPU the HIP training kernels run it
+    (mswegnn/autograd.py mlp_apply), else the module itself."""
+    if (getattr(owner, "train_engine", "auto") != "torch" and not _TORCH_ONLY.get() and torch.is_grad_enabled()
+            and x.is_cuda):
+        from mswegnn import autograd as _ag
+        if _ag.mlp_supported(seq, x):
+            return _ag.mlp_apply(seq, x)
+    return seq(x)
+
+
 class _EngineMixin:
     """Binds a model to the HIP engine (one cached plan per graph topology + weights)."""
 
     engine = "auto"
+    # 'auto': with autograd on a GPU, the encoders / decoder (and every SWEGNN layer, see
+    # SWEGNN.train_engine) run on the HIP training kernels; 'torch': the modules themselves
+    train_engine = "auto"
 
     def _engine_for(self, graph):
         """The cached plan for this graph, or None when engine='auto' and the engine does
@@ -269,16 +283,16 @@ class GNN(_EngineMixin, BaseFloodModel):
 
     def _torch_forward(self, graph):
         x = graph.x.clone()
-        edge_attr = self.edge_encoder(graph.edge_attr) if self.edge_mlp else graph.edge_attr
+        edge_attr = _mlp_call(self, self.edge_encoder, graph.edge_attr) if self.edge_mlp else graph.edge_attr
         x_s, x_d = self._split_inputs(x)
-        x_s = self.static_node_encoder(x_s)
-        h = x_d = self.dynamic_node_encoder(x_d)
+        x_s = _mlp_call(self, self.static_node_encoder, x_s)
+        h = x_d = _mlp_call(self, self.dynamic_node_encoder, x_d)
         for conv in self.gnn_processor:
             h = conv(x_s, x_d, graph.edge_index, edge_attr)
             if self.gnn_activation is not None:
                 h = self.gnn_activation(h)
             x_d = h
-        h = self.node_decoder(h) + self._add_residual_connection(x)
+        h = _mlp_call(self, self.node_decoder, h) + self._add_residual_connection(x)
         return self._mask_small_WD(torch.relu(h), epsilon=0.0001)
 
 
@@ -368,13 +382,13 @@ class MSGNN(_EngineMixin, BaseFloodModel):
         ei, ep = graph.edge_index, graph.edge_ptr
         iei, iep = graph.intra_mesh_edge_index, graph.intra_edge_ptr
         scale = self._create_scale_mask(graph)
-        edge_attr = self.edge_encoder(graph.edge_attr) if self.edge_mlp else graph.edge_attr
+        edge_attr = _mlp_call(self, self.edge_encoder, graph.edge_attr) if self.edge_mlp else graph.edge_attr
         nst = self.static_node_features - self.with_WL
         x_s, x_d = x[:, :nst], x[:, nst:]
         if self.with_WL:
             x_s = torch.cat((x_s, (x_s[:, -1] + x_d[:, -self.out_dim]).unsqueeze(-1)), 1)
-        x_s = self.static_node_encoder(x_s)
-        x_d = self.dynamic_node_encoder(x_d)
+        x_s = _mlp_call(self, self.static_node_encoder, x_s)
+        x_d = _mlp_call(self, self.dynamic_node_encoder, x_d)
         x_down = torch.zeros_like(x_d)
         x_up = torch.zeros_like(x_d)
         sel = lambda i: (scale == i).unsqueeze(1).to(x_d.dtype)  # noqa: E731
@@ -393,5 +407,5 @@ class MSGNN(_EngineMixin, BaseFloodModel):
                 if self.skip_connections:
                     x_d = x_d + x_down * sel(s - 1)
         h = x_up if self.gnn_activation is None else self.gnn_activation(x_up)
-        h = self.node_decoder(h) + self._add_residual_connection(x)
+        h = _mlp_call(self, self.node_decoder, h) + self._add_residual_connection(x)
         return self._mask_small_WD(torch.relu(h), epsilon=0.0001)

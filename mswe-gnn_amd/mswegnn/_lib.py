@@ -99,6 +99,18 @@ class MswSwegnnGrads(C.Structure):
                 ("d_slope", C.c_void_p * MAX_MLP_LAYERS), ("d_filter", C.c_void_p * (MAX_HOPS + 1))]
 
 
+
+class MswMlpTrainDesc(C.Structure):
+    _fields_ = [("rows", C.c_int64), ("n_layers", C.c_int32), ("width", C.c_int32 * (MAX_MLP_LAYERS + 1)),
+                ("act", C.c_int32 * MAX_MLP_LAYERS), ("weight", C.c_void_p * MAX_MLP_LAYERS),
+                ("bias", C.c_void_p * MAX_MLP_LAYERS), ("slope", C.c_void_p * MAX_MLP_LAYERS)]
+
+
+class MswMlpGrads(C.Structure):
+    _fields_ = [("d_x", C.c_void_p), ("d_weight", C.c_void_p * MAX_MLP_LAYERS),
+                ("d_bias", C.c_void_p * MAX_MLP_LAYERS), ("d_slope", C.c_void_p * MAX_MLP_LAYERS)]
+
+
 # (name, restype, argtypes) of every entry point declared in include/mswegnn.h
 SYMBOLS = [
     ("msw_plan_create", C.c_int, [C.POINTER(MswGraphDesc), C.POINTER(MswModelDesc), C.c_int,
@@ -132,12 +144,18 @@ SYMBOLS = [
     ("msw_swegnn_train_backward", C.c_int, [C.POINTER(MswSwegnnTrainDesc), C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(MswSwegnnGrads), C.c_void_p, C.c_void_p]),
+    ("msw_mlp_train_workspace", C.c_int, [C.POINTER(MswMlpTrainDesc), c_int64_p, c_int64_p]),
+    ("msw_mlp_train_forward", C.c_int, [C.POINTER(MswMlpTrainDesc), C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]),
+    ("msw_mlp_train_backward", C.c_int, [C.POINTER(MswMlpTrainDesc), C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.POINTER(MswMlpGrads), C.c_void_p, C.c_void_p]),
 ]
 
 STRUCTS = {"msw_linear": MswLinear, "msw_mlp": MswMlp, "msw_swegnn": MswSwegnn,
            "msw_model_desc": MswModelDesc, "msw_graph_desc": MswGraphDesc,
            "msw_plan_stats": MswPlanStats, "msw_exchange_desc": MswExchangeDesc,
-           "msw_swegnn_train_desc": MswSwegnnTrainDesc, "msw_swegnn_grads": MswSwegnnGrads}
+           "msw_swegnn_train_desc": MswSwegnnTrainDesc, "msw_swegnn_grads": MswSwegnnGrads,
+           "msw_mlp_train_desc": MswMlpTrainDesc, "msw_mlp_grads": MswMlpGrads}
 
 _lib = None
 

@@ -1,4 +1,4 @@
-"""Autograd through the HIP SWEGNN kernels (first slice).
+"""Autograd through the HIP training kernels.
 
 ``swegnn_apply(layer, x_s, x_d, edge_index, edge_attr)`` runs one ``SWEGNN`` processor
 (models/gnn.py:387-445) as a ``torch.autograd.Function`` whose forward and backward are the
@@ -9,8 +9,12 @@ MFMA GEMMs for the edge-MLP and filter layers (split-K weight gradients), CSR pu
 destination and by source for the hop's transpose, no atomics.  torch only allocates the
 buffers (saved state, scratch, gradients) and orders the work on its current stream.
 
-``SWEGNN.forward`` (models/gnn.py of this package) routes here on a GPU with autograd
-enabled; everything else of the model (encoders, pooling, decoder) keeps its torch path.
+``mlp_apply(seq, x)`` does the same for a make_mlp Sequential (models/models.py:121-146: the
+edge / node encoders and the node decoder) over ``msw_mlp_train_*``.
+
+``SWEGNN.forward`` and the models' encoder / decoder calls (models/gnn.py of this package)
+route here on a GPU with autograd enabled; pooling, the scale selections and the output mask
+keep their torch ops (index_add / elementwise).
 """
 from __future__ import annotations
 
@@ -21,12 +25,13 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .engine import _act_of, _raw_stream
+from .engine import _act_code, _raw_stream
 
-__all__ = ["swegnn_apply", "supported", "graph_csr"]
+__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported"]
 
 _CSR_CACHE = OrderedDict()
 _CSR_KEEP = 32
+MLP_CALLS = [0]  # mlp_apply calls (tests check that the HIP path ran)
 
 
 class GraphCSR:
@@ -86,7 +91,7 @@ def _mlp_layers(seq):
         return None
     for lin, act in layers:
         try:
-            _act_of(act)
+            _act_code(act)
         except NotImplementedError:
             return None
     return layers
@@ -114,7 +119,7 @@ class _Meta:
         d.width[0] = layers[0][0].in_features
         for i, (lin, act) in enumerate(layers):
             d.width[i + 1] = lin.out_features
-            d.act[i] = _act_of(act)[0]
+            d.act[i] = _act_code(act)
         d.normalize = int(bool(layer.normalize))
         d.with_filter_matrix = int(bool(layer.with_filter_matrix))
         d.with_gradient = int(bool(layer.with_gradient))
@@ -220,3 +225,99 @@ def swegnn_apply(layer, x_s, x_d, edge_index, edge_attr=None):
     if ef > 0 and edge_attr.dim() == 1:
         edge_attr = edge_attr.unsqueeze(1)
     return _SwegnnFunction.apply(meta, x_s, x_d, edge_attr if ef > 0 else None, *meta.params)
+
+
+def mlp_supported(seq, x):
+    """The HIP training path implements this make_mlp call (else the module runs)."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 2:
+        return False
+    layers = _mlp_layers(seq)
+    if layers is None or layers[0][0].in_features != x.shape[1]:
+        return False
+    return all(p.dtype == torch.float32 and p.is_cuda for p in seq.parameters())
+
+
+class _MlpMeta:
+    def __init__(self, layers, rows):
+        self.layers = layers
+        d = L.MswMlpTrainDesc()
+        d.rows, d.n_layers = rows, len(layers)
+        d.width[0] = layers[0][0].in_features
+        for i, (lin, act) in enumerate(layers):
+            d.width[i + 1] = lin.out_features
+            d.act[i] = _act_code(act)
+        self.desc = d
+        self.params = []
+        for lin, act in layers:
+            self.params.append(lin.weight)
+            if lin.bias is not None:
+                self.params.append(lin.bias)
+            if isinstance(act, nn.PReLU):
+                self.params.append(act.weight)
+
+    def bind(self, params):
+        d, it = self.desc, iter(params)
+        for i, (lin, act) in enumerate(self.layers):
+            d.weight[i] = next(it).data_ptr()
+            d.bias[i] = next(it).data_ptr() if lin.bias is not None else None
+            d.slope[i] = next(it).data_ptr() if isinstance(act, nn.PReLU) else None
+        return d
+
+    def workspace(self):
+        s, t = C.c_int64(), C.c_int64()
+        L.check(L.lib().msw_mlp_train_workspace(C.byref(self.desc), C.byref(s), C.byref(t)))
+        return int(s.value), int(t.value)
+
+
+class _MlpFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, x, *params):
+        dev = x.device
+        x = x.contiguous()
+        params = [p.contiguous() for p in params]
+        d = meta.bind(params)
+        n_saved, _ = meta.workspace()
+        saved = torch.empty(max(n_saved, 1), device=dev, dtype=torch.float32)
+        out = torch.empty(x.shape[0], meta.layers[-1][0].out_features, device=dev, dtype=torch.float32)
+        L.check(L.lib().msw_mlp_train_forward(C.byref(d), x.data_ptr(), saved.data_ptr(), out.data_ptr(),
+                                              C.c_void_p(_raw_stream(dev.index or 0))))
+        ctx.meta = meta
+        ctx.save_for_backward(x, saved, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        meta = ctx.meta
+        x, saved, *params = ctx.saved_tensors
+        dev = x.device
+        gout = gout.contiguous().to(torch.float32)
+        d = meta.bind(params)
+        _, n_scratch = meta.workspace()
+        scratch = torch.empty(max(n_scratch, 1), device=dev, dtype=torch.float32)
+        g = L.MswMlpGrads()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
+        g.d_x = dx.data_ptr() if dx is not None else None
+        dps = [torch.empty_like(p) if ctx.needs_input_grad[2 + i] else None for i, p in enumerate(params)]
+        it = iter(dps)
+        for i, (lin, act) in enumerate(meta.layers):
+            w = next(it)
+            g.d_weight[i] = w.data_ptr() if w is not None else None
+            if lin.bias is not None:
+                b = next(it)
+                g.d_bias[i] = b.data_ptr() if b is not None else None
+            if isinstance(act, nn.PReLU):
+                a = next(it)
+                g.d_slope[i] = a.data_ptr() if a is not None else None
+        L.check(L.lib().msw_mlp_train_backward(C.byref(d), x.data_ptr(), saved.data_ptr(), gout.data_ptr(),
+                                               C.byref(g), scratch.data_ptr(),
+                                               C.c_void_p(_raw_stream(dev.index or 0))))
+        if dx is not None and x.shape[0] == 0:
+            dx.zero_()
+        return (None, dx, *dps)
+
+
+def mlp_apply(seq, x):
+    """make_mlp `seq` applied to x [rows][in] on the HIP training kernels (differentiable)."""
+    meta = _MlpMeta(_mlp_layers(seq), int(x.shape[0]))
+    MLP_CALLS[0] += 1
+    return _MlpFunction.apply(meta, x, *meta.params)

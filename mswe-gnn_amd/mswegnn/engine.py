@@ -31,23 +31,31 @@ def _f32(keep, t):
     return a.ctypes.data_as(L.c_float_p)
 
 
-def _act_of(mod):
-    """(code, param) of an activation module."""
+def _act_code(mod):
+    """enum msw_activation code of an activation module (no device read)."""
     if mod is None:
-        return 0, 0.0
+        return 0
     if isinstance(mod, nn.PReLU):
         if mod.weight.numel() != 1:
             raise NotImplementedError("PReLU with more than one parameter")
-        return L.ACT["prelu"], float(mod.weight.detach().reshape(-1)[0])
+        return L.ACT["prelu"]
     for name, cls in (("relu", nn.ReLU), ("elu", nn.ELU), ("swish", nn.SiLU),
                       ("sigmoid", nn.Sigmoid), ("tanh", nn.Tanh)):
         if isinstance(mod, cls):
-            return L.ACT[name], 0.0
+            return L.ACT[name]
     if isinstance(mod, nn.LeakyReLU):
         if abs(mod.negative_slope - 0.1) > 1e-12:
             raise NotImplementedError("LeakyReLU slope other than 0.1")
-        return L.ACT["leakyrelu"], 0.0
+        return L.ACT["leakyrelu"]
     raise NotImplementedError(f"activation {type(mod).__name__}")
+
+
+def _act_of(mod):
+    """(code, param) of an activation module (reads a PReLU slope from the device)."""
+    code = _act_code(mod)
+    if isinstance(mod, nn.PReLU):
+        return code, float(mod.weight.detach().reshape(-1)[0])
+    return code, 0.0
 
 
 def _mlp(keep, seq):

@@ -73,6 +73,9 @@ def state_dict_of(model):
 def rel_err(a, b):
     a = torch.as_tensor(a).double().cpu()
     b = torch.as_tensor(b).double().cpu()
+    if b.numel() == 0:
+        assert a.numel() == 0
+        return 0.0
     den = b.abs().max().item()
     return (a - b).abs().max().item() / (den if den > 0 else 1.0)
 

@@ -690,6 +690,29 @@ def test_row_layout_hops_match_edge_tiles(cuda, monkeypatch, S, F, K, ck):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct"])
+def test_f64_kernel_variants_match_default(cuda, monkeypatch, variant):
+    """F = 64 kernel variants == the default bit for bit over a wet-start rollout (forced on the
+    small mesh): k_edge_mlp_pipe (the split edge MLP with the next chunk's gathers in flight,
+    MSW_MLP_PIPE) against k_edge_mlp, and the two-wave cooperative edge hop reading its MLP
+    region from the blob (MSW_COOP2_DIRECT=2) against the LDS-staged one."""
+    from mswegnn.engine import EnginePlan
+    T = 6
+    g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=4).to(cuda)
+    m = build_msgnn(4, 64, 4).to(cuda)
+    base = {"mlp_pipe": {"MSW_SPLIT_EDGE_MLP": "1"}, "coop2_direct": {"MSW_COOP2_F64": "2"}}[variant]
+    knob = {"mlp_pipe": "MSW_MLP_PIPE", "coop2_direct": "MSW_COOP2_DIRECT"}[variant]
+    for k, v in base.items():
+        monkeypatch.setenv(k, v)
+    outs = []
+    for v in ("0", "2"):
+        monkeypatch.setenv(knob, v)
+        plan = EnginePlan(m, g, cuda)
+        outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
+        plan.close()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("mode", ["fused", "stepped"])
 def test_ingested_dataset_vs_reference(cuda, mode):
     """§8 f4 ingest: the reference's own dataset pipeline (get_scalers -> create_data_attr ->

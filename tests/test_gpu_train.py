@@ -1,6 +1,6 @@
-"""Autograd through the HIP SWEGNN kernels (first slice; mswegnn/autograd.py,
-csrc/train.hip) against the drop-in's torch autograd of the same layer, which restates the
-reference's SWEGNN.forward (models/gnn.py:387-445) op for op.
+"""Autograd through the HIP training kernels (mswegnn/autograd.py, csrc/train.hip)
+against the drop-in's torch autograd of the same layers, which restate the reference's
+SWEGNN.forward (models/gnn.py:387-445) and make_mlp (models/models.py:121-146) op for op.
 
 The reference trains through this layer in training_step (training/train.py:125-145).  The
 bar: every parameter and input gradient within 1e-4 relative (max |ours - torch| / max |torch|)
@@ -117,7 +117,44 @@ def test_msgnn_training_step_gradients(cuda):
         return {"y": y.detach(), **{n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}}
     ref = step("torch")
     ours = step("auto")
-    from mswegnn.autograd import _CSR_CACHE
-    assert len(_CSR_CACHE) > 0  # the HIP training path ran
+    from mswegnn import autograd as ag
+    assert len(ag._CSR_CACHE) > 0 and ag.MLP_CALLS[0] > 0  # the HIP training path ran
     e = _compare(ours, ref, "MSGNN")
     print(f"MSGNN: worst rel err {e:.2e} over {len(ref)} gradients")
+
+
+@pytest.mark.parametrize("case", ["prelu3_bias", "relu2_nobias", "tanh1", "elu2_wide", "empty"])
+def test_mlp_gradients_vs_torch_autograd(cuda, case):
+    """make_mlp stacks (the encoders' / decoder's shapes and activations) on msw_mlp_train_*:
+    output, input gradient and every parameter gradient against torch autograd, including
+    an empty row set (zero gradients)."""
+    from models.models import make_mlp
+    from mswegnn.autograd import mlp_apply, mlp_supported
+    spec = {"prelu3_bias": (9, 32, 32, 3, True, "prelu", 700), "relu2_nobias": (1, 32, 32, 2, False, "relu", 1025),
+            "tanh1": (32, 2, 32, 1, True, "tanh", 333), "elu2_wide": (5, 64, 64, 2, True, "elu", 4099),
+            "empty": (9, 32, 32, 3, True, "prelu", 0)}[case]
+    din, dout, hid, nl, bias, act, rows = spec
+    torch.manual_seed(5)
+    seq = make_mlp(din, dout, hid, n_layers=nl, bias=bias, activation=act).to(cuda)
+    if act == "prelu":
+        with torch.no_grad():
+            for mod in seq:
+                if isinstance(mod, torch.nn.PReLU):
+                    mod.weight.fill_(0.13)
+    x = torch.randn(rows, din, device=cuda)
+    wout = torch.randn(rows, dout, device=cuda)
+    assert mlp_supported(seq, x)
+
+    def run(fn):
+        seq.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        y = fn(xx)
+        (y * wout).sum().backward()
+        out = {"y": y.detach(), "x": xx.grad}
+        for n, p in seq.named_parameters():
+            out[n] = p.grad if p.grad is not None else torch.zeros_like(p)
+        return out
+    ref = run(seq)
+    ours = run(lambda xx: mlp_apply(seq, xx))
+    e = _compare(ours, ref, case)
+    print(f"mlp {case}: worst rel err {e:.2e} over {len(ref)} tensors")
