@@ -324,6 +324,18 @@ int msw_mlp_train_forward(const msw_mlp_train_desc* desc, const float* x, float*
 int msw_mlp_train_backward(const msw_mlp_train_desc* desc, const float* x, const float* saved,
                            const float* grad_out, const msw_mlp_grads* grads, float* scratch, void* stream);
 
+/* ---- Training: autograd of the mean pooling ----------------------------------
+ * Replaces MSGNN._pooling (models/gnn.py:242-257, learnable=False, reduce='mean') and its
+ * autograd: pooling edge e maps fine[e] -> coarse[e] (intra_mesh_edge_index rows (coarse,
+ * fine), gnn.py:310); cptr / cedge = CSR of the pooling edges by coarse node, fptr / fedge by
+ * fine node ([N + 1], [E], edges in pooling-edge order).  out[c] = sum of x[fine] over c's
+ * edges / max(#edges, 1), rows without children 0; deterministic (no atomics). */
+int msw_pool_mean_forward(int64_t num_nodes, int32_t F, const int32_t* fine, const int32_t* cptr,
+                          const int32_t* cedge, const float* x, float* out, void* stream);
+int msw_pool_mean_backward(int64_t num_nodes, int32_t F, const int32_t* coarse, const int32_t* cptr,
+                           const int32_t* fptr, const int32_t* fedge, const float* grad_out, float* grad_x,
+                           void* stream);
+
 /* Diagnostics: route per-phase timestamps of wave 0 of workgroup 0 of every launch to the
  * device buffer `buf` (uint64[20]: {shader clock, 100 MHz clock} for phase marks 0..9).
  * Only builds compiled with -DMSW_TRACE record anything; NULL disables. */

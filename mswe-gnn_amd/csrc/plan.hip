@@ -1037,10 +1037,11 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     }
     case L_EDGE_MLP: {
-      // MSW_MLP_PIPE=1: one wave per SIMD walking ~2 chunks, the next chunk's gathers in
-      // flight under the current chunk's MLP (k_edge_mlp_pipe)
+      // one wave per SIMD walking ~2 chunks, the next chunk's gathers in flight under the
+      // current chunk's MLP (k_edge_mlp_pipe; zenodo4_f64: 27.8 -> 27.0 us per launch,
+      // +0.4 %; MSW_MLP_PIPE=0: k_edge_mlp, two waves per SIMD, one chunk each)
       const char* pp = getenv("MSW_MLP_PIPE");
-      L.eh.pipe = pp && atoi(pp) != 0;
+      L.eh.pipe = pp ? atoi(pp) != 0 : 1;
       L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
     }
@@ -1049,6 +1050,9 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       caps(P, a, 1, a.c.prelu, a.last, a.reg.len);
       a.fit_blocks = resident_of(P->NT, 1, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0);
       if (no_loop("eh")) a.max_blocks = 0;
+      // MSW_EH_LOOP=1: the grid-stride variant at any size (parity tests of the large-mesh path)
+      if (const char* el = getenv("MSW_EH_LOOP"))
+        if (atoi(el) != 0 && a.max_blocks > 0 && a.ntiles > kWaves) a.fit_blocks = 1;
       // two waves per tile (k_edge_coop) while the tiles leave most SIMDs idle: one tile
       // per wave at most, no grid-stride loop, an epilogue of projections only
       const bool loop = a.fit_blocks > 0 && a.max_blocks > 0 && (a.ntiles + kWaves - 1) / kWaves > a.fit_blocks;

@@ -2,6 +2,7 @@
 // what the backward needs) and the backward of
 //   SWEGNN.forward  models/gnn.py:387-445   (msw_swegnn_train_*)
 //   make_mlp        models/models.py:121-146 (msw_mlp_train_*: encoders gnn.py:204-215, decoder :239-240)
+//   _pooling        models/gnn.py:242-257     (msw_pool_mean_*: mean pooling, learnable=False)
 // as the reference trains it (training_step, training/train.py:125-145).  The reference
 // recomputes s_ij from the active edges of every hop; s_ij depends on the hop only through
 // the mask, so by linearity of the backward ONE MLP backward of ds = sum_k [active_k] ds_k
@@ -428,6 +429,37 @@ __global__ void k_copy_cols(const float* __restrict__ src, long rows, int src_ld
   }
 }
 
+// Mean pooling (gnn.py:242-257, learnable=False): out[c] = sum of x[fine] over c's children in
+// pooling-edge order / max(#children, 1) -- a pull over the CSR by coarse node, no atomics;
+// backward dx[f] = sum over f's pooling edges of dout[c] / max(#children of c, 1).
+__global__ void k_pool_fwd(const int* __restrict__ cptr, const int* __restrict__ cedge, const int* __restrict__ fine,
+                           const float* __restrict__ x, int F, long N, float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < N * F; i += (long)gridDim.x * blockDim.x) {
+    const long c = i / F;
+    const int f = (int)(i - c * F);
+    const int b = cptr[c], e = cptr[c + 1];
+    float acc = 0.f;
+    for (int q = b; q < e; ++q) acc += x[(long)fine[cedge[q]] * F + f];
+    const int cnt = e - b;
+    out[i] = acc / (float)(cnt > 1 ? cnt : 1);
+  }
+}
+__global__ void k_pool_bwd(const int* __restrict__ fptr, const int* __restrict__ fedge, const int* __restrict__ coarse,
+                           const int* __restrict__ cptr, const float* __restrict__ dout, int F, long N,
+                           float* __restrict__ dx) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < N * F; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / F;
+    const int f = (int)(i - n * F);
+    float acc = 0.f;
+    for (int q = fptr[n]; q < fptr[n + 1]; ++q) {
+      const int c = coarse[fedge[q]];
+      const int cnt = cptr[c + 1] - cptr[c];
+      acc += dout[(long)c * F + f] / (float)(cnt > 1 ? cnt : 1);
+    }
+    dx[i] = acc;
+  }
+}
+
 __global__ void k_add(const float* __restrict__ a, const float* __restrict__ b, long n, float* __restrict__ c) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     c[i] = a[i] + b[i];
@@ -850,6 +882,29 @@ int msw_mlp_train_backward(const msw_mlp_train_desc* d, const float* x, const fl
   }
   TRY(mlp_backward(MlpRun{d->rows, y.L, y.w, d->act, d->weight, d->bias, d->slope}, x, pre, post, grad_out,
                    gr->d_x, dW, db, dsl, scratch + y.A, scratch + y.B, scratch + y.part, scratch + y.spart, st));
+  return MSW_OK;
+}
+
+int msw_pool_mean_forward(int64_t num_nodes, int32_t F, const int32_t* fine, const int32_t* cptr,
+                          const int32_t* cedge, const float* x, float* out, void* stream) {
+  if (num_nodes < 0 || F < 1) return set_error(MSW_ERR_INVALID, "bad pooling sizes");
+  if (num_nodes == 0) return MSW_OK;
+  if (!fine || !cptr || !cedge || !x || !out) return set_error(MSW_ERR_INVALID, "null argument");
+  hipLaunchKernelGGL(k_pool_fwd, dim3(blocks_for(num_nodes * F)), dim3(256), 0, (hipStream_t)stream, cptr, cedge,
+                     fine, x, F, (long)num_nodes, out);
+  TRY(hipGetLastError());
+  return MSW_OK;
+}
+
+int msw_pool_mean_backward(int64_t num_nodes, int32_t F, const int32_t* coarse, const int32_t* cptr,
+                           const int32_t* fptr, const int32_t* fedge, const float* grad_out, float* grad_x,
+                           void* stream) {
+  if (num_nodes < 0 || F < 1) return set_error(MSW_ERR_INVALID, "bad pooling sizes");
+  if (num_nodes == 0) return MSW_OK;
+  if (!coarse || !cptr || !fptr || !fedge || !grad_out || !grad_x) return set_error(MSW_ERR_INVALID, "null argument");
+  hipLaunchKernelGGL(k_pool_bwd, dim3(blocks_for(num_nodes * F)), dim3(256), 0, (hipStream_t)stream, fptr, fedge,
+                     coarse, cptr, grad_out, F, (long)num_nodes, grad_x);
+  TRY(hipGetLastError());
   return MSW_OK;
 }
 

@@ -366,6 +366,18 @@ class MSGNN(_EngineMixin, BaseFloodModel):
             out = out / cnt.clamp(min=1).unsqueeze(1)
         return out
 
+    def _pool(self, x, pool_edges):
+        """Mean pooling over one level's intra-scale edges (rows (coarse, fine)): with autograd
+        on a GPU the deterministic HIP kernels (mswegnn/autograd.py pool_apply), else
+        _pooling."""
+        if (not self.learned_pooling and self.train_engine != "torch" and not _TORCH_ONLY.get()
+                and torch.is_grad_enabled() and x.is_cuda):
+            from mswegnn import autograd as _ag
+            if _ag.pool_supported(x, pool_edges):
+                return _ag.pool_apply(x, pool_edges)
+        coarse, fine = pool_edges
+        return self._pooling(x, fine, coarse, 'mean', self.learned_pooling)
+
     def forward(self, graph):
         y = self._engine_forward(graph) if _engine_wanted(self, graph.x) else None
         if y is not None:
@@ -395,8 +407,7 @@ class MSGNN(_EngineMixin, BaseFloodModel):
         for i in range(S - 1):                                  # fine -> coarse
             x_d = self.gnn_processor[i](x_s, x_d, ei[:, ep[i]:ep[i + 1]], edge_attr[ep[i]:ep[i + 1]])
             x_down = x_down + x_d * sel(i)
-            coarse, fine = iei[:, iep[i]:iep[i + 1]]
-            x_d = self._pooling(x_d, fine, coarse, 'mean', self.learned_pooling)
+            x_d = self._pool(x_d, iei[:, iep[i]:iep[i + 1]])
         x_down = x_down + x_d
         for i in range(S):                                      # coarse -> fine
             s = S - 1 - i

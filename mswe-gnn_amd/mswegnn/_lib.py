@@ -144,6 +144,10 @@ SYMBOLS = [
     ("msw_swegnn_train_backward", C.c_int, [C.POINTER(MswSwegnnTrainDesc), C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.POINTER(MswSwegnnGrads), C.c_void_p, C.c_void_p]),
+    ("msw_pool_mean_forward", C.c_int, [C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p]),
+    ("msw_pool_mean_backward", C.c_int, [C.c_int64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p]),
     ("msw_mlp_train_workspace", C.c_int, [C.POINTER(MswMlpTrainDesc), c_int64_p, c_int64_p]),
     ("msw_mlp_train_forward", C.c_int, [C.POINTER(MswMlpTrainDesc), C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p]),

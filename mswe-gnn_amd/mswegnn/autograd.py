@@ -12,9 +12,13 @@ buffers (saved state, scratch, gradients) and orders the work on its current str
 ``mlp_apply(seq, x)`` does the same for a make_mlp Sequential (models/models.py:121-146: the
 edge / node encoders and the node decoder) over ``msw_mlp_train_*``.
 
-``SWEGNN.forward`` and the models' encoder / decoder calls (models/gnn.py of this package)
-route here on a GPU with autograd enabled; pooling, the scale selections and the output mask
-keep their torch ops (index_add / elementwise).
+``pool_apply(x, pool_edges)`` is MSGNN's mean pooling (models/gnn.py:242-257) over
+``msw_pool_mean_*``: CSR pulls by coarse node (forward) and by fine node (backward), no
+atomics, so the whole training forward / backward is deterministic.
+
+``SWEGNN.forward``, the models' encoder / decoder calls and MSGNN's pooling (models/gnn.py of
+this package) route here on a GPU with autograd enabled; the scale selections, skip sums and
+the output mask stay elementwise torch ops.
 """
 from __future__ import annotations
 
@@ -27,11 +31,12 @@ import torch.nn as nn
 from . import _lib as L
 from .engine import _act_code, _raw_stream
 
-__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported"]
+__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported", "pool_apply"]
 
 _CSR_CACHE = OrderedDict()
 _CSR_KEEP = 32
-MLP_CALLS = [0]  # mlp_apply calls (tests check that the HIP path ran)
+MLP_CALLS = [0]  # mlp_apply / pool_apply calls (tests check that the HIP path ran)
+POOL_CALLS = [0]
 
 
 class GraphCSR:
@@ -321,3 +326,40 @@ def mlp_apply(seq, x):
     meta = _MlpMeta(_mlp_layers(seq), int(x.shape[0]))
     MLP_CALLS[0] += 1
     return _MlpFunction.apply(meta, x, *meta.params)
+
+
+class _PoolFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, csr, x):
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        dev = x.device
+        L.check(L.lib().msw_pool_mean_forward(csr.num_nodes, int(x.shape[1]), csr.col.data_ptr(),
+                                              csr.out_ptr.data_ptr(), csr.out_edge.data_ptr(), x.data_ptr(),
+                                              out.data_ptr(), C.c_void_p(_raw_stream(dev.index or 0))))
+        ctx.csr = csr
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        csr = ctx.csr
+        gout = gout.contiguous().to(torch.float32)
+        dx = torch.empty_like(gout)
+        dev = gout.device
+        L.check(L.lib().msw_pool_mean_backward(csr.num_nodes, int(gout.shape[1]), csr.row.data_ptr(),
+                                               csr.out_ptr.data_ptr(), csr.in_ptr.data_ptr(),
+                                               csr.in_edge.data_ptr(), gout.data_ptr(), dx.data_ptr(),
+                                               C.c_void_p(_raw_stream(dev.index or 0))))
+        return None, dx
+
+
+def pool_supported(x, pool_edges):
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and pool_edges.is_cuda
+            and pool_edges.dim() == 2 and pool_edges.shape[0] == 2)
+
+
+def pool_apply(x, pool_edges):
+    """Mean pooling of x [N][F] over pool_edges [2][E] = (coarse, fine) rows (a slice of
+    intra_mesh_edge_index, gnn.py:310) on the HIP kernels (differentiable)."""
+    POOL_CALLS[0] += 1
+    return _PoolFunction.apply(graph_csr(pool_edges, x.shape[0]), x)

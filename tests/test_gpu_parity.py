@@ -690,6 +690,24 @@ def test_row_layout_hops_match_edge_tiles(cuda, monkeypatch, S, F, K, ck):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("S,F,K,ck", [(4, 32, 4, "K4_F32"), (3, 32, 4, None), (4, 64, 4, None)])
+def test_grid_stride_edge_hops_match_one_tile_per_wave(cuda, monkeypatch, S, F, K, ck):
+    """The grid-stride fused edge MLP + hop of large meshes (staged weights once per
+    workgroup, the next tile's lane record prefetched; forced at any size with MSW_EH_LOOP=1)
+    == the one-tile-per-wave kernels bit for bit over a wet-start rollout."""
+    from mswegnn.engine import EnginePlan
+    T = 6
+    g = wet_state(make_multiscale_mesh(**mesh_config("small" if S == 4 else "small3"), T=T), seed=4).to(cuda)
+    m = build_msgnn(S, F, K, state=weights(ck) if ck else None).to(cuda)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("MSW_EH_LOOP", v)
+        plan = EnginePlan(m, g, cuda)
+        outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
+        plan.close()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct"])
 def test_f64_kernel_variants_match_default(cuda, monkeypatch, variant):
     """F = 64 kernel variants == the default bit for bit over a wet-start rollout (forced on the

@@ -118,7 +118,7 @@ def test_msgnn_training_step_gradients(cuda):
     ref = step("torch")
     ours = step("auto")
     from mswegnn import autograd as ag
-    assert len(ag._CSR_CACHE) > 0 and ag.MLP_CALLS[0] > 0  # the HIP training path ran
+    assert len(ag._CSR_CACHE) > 0 and ag.MLP_CALLS[0] > 0 and ag.POOL_CALLS[0] > 0  # the HIP path ran
     e = _compare(ours, ref, "MSGNN")
     print(f"MSGNN: worst rel err {e:.2e} over {len(ref)} gradients")
 
@@ -158,3 +158,27 @@ def test_mlp_gradients_vs_torch_autograd(cuda, case):
     ours = run(lambda xx: mlp_apply(seq, xx))
     e = _compare(ours, ref, case)
     print(f"mlp {case}: worst rel err {e:.2e} over {len(ref)} tensors")
+
+
+def test_mean_pooling_gradients_vs_torch_autograd(cuda):
+    """MSGNN's mean pooling (gnn.py:242-257) on msw_pool_mean_*: output and input gradient of
+    every pooling level of the small mesh against the drop-in's index_add path."""
+    from mswegnn.autograd import pool_apply
+    g = make_multiscale_mesh(**mesh_config("small"), T=2).to(cuda)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+    iei, iep = g.intra_mesh_edge_index, g.intra_edge_ptr
+    torch.manual_seed(2)
+    x = torch.randn(g.num_nodes, 32, device=cuda)
+    for i in range(3):
+        pe = iei[:, iep[i]:iep[i + 1]]
+        wout = torch.randn_like(x)
+
+        def run(fn):
+            xx = x.clone().requires_grad_(True)
+            y = fn(xx)
+            (y * wout).sum().backward()
+            return {"y": y.detach(), "x": xx.grad}
+        ref = run(lambda xx: m._pooling(xx, pe[1], pe[0], "mean", False))
+        ours = run(lambda xx: pool_apply(xx, pe))
+        e = _compare(ours, ref, f"pool level {i}")
+        print(f"pool level {i}: worst rel err {e:.2e}")
