@@ -26,7 +26,7 @@ def rmse_loss(pred, real, n0, velocity_scaler=1.0):
     scale (training/loss.py:76-118, get_multiscale_loss single graph)."""
     diff = pred[:n0] - real[:n0]
     per_var = torch.sqrt(torch.mean(diff ** 2, 0))
-    sc = torch.tensor([1.0, velocity_scaler], device=pred.device)
+    sc = torch.tensor([1.0, velocity_scaler], device=pred.device, dtype=pred.dtype)
     return torch.dot(per_var, sc) / sc.sum()
 
 
@@ -37,7 +37,19 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--only", choices=["hip", "torch"], default=None)
+    ap.add_argument("--fp64-ref", action="store_true",
+                    help="also the first-step gradients of the torch path in float64 (the yardstick)")
+    ap.add_argument("--parts", default="swegnn,mlp,pool",
+                    help="diagnostics: which layer kinds run on the HIP training kernels")
     a = ap.parse_args()
+    from mswegnn import autograd as ag
+    parts = set(a.parts.split(","))
+    if "mlp" not in parts:
+        ag.mlp_supported = lambda *args: False
+    if "pool" not in parts:
+        ag.pool_supported = lambda *args: False
+    if "swegnn" not in parts:
+        ag.supported = lambda *args: False
     from mswegnn.rollout import apply_boundary_condition, use_prediction
     dev = torch.device("cuda", 0)
     R = a.rollout_steps
@@ -85,25 +97,68 @@ def main():
             step()
             opt.step()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / a.steps, float(first), grads
+        return (time.perf_counter() - t0) / max(a.steps, 1), float(first.detach()), grads
     if a.only:
         t, l, _ = run("auto" if a.only == "hip" else "torch")
         print(json.dumps({"only": a.only, "ms_per_training_step": t * 1e3, "first_loss": l}), flush=True)
         return
     t_hip, l_hip, g_hip = run("auto")
     t_torch, l_torch, g_torch = run("torch")
-    worst = max(((g_hip[k] - g_torch[k]).abs().max() / g_torch[k].abs().max().clamp(min=1e-30)).item()
-                for k in g_torch)
+    _, _, g_hip2 = run("auto")      # run-to-run: the HIP path is deterministic (no atomics)
+    _, _, g_torch2 = run("torch")   # torch's index_add / scatter use atomics on the GPU
+
+    def per_tensor(a, b):
+        return {k: ((a[k] - b[k]).abs().max() / b[k].abs().max().clamp(min=1e-30)).item() for k in b}
+
+    def global_rel(a, b):
+        num = sum(((a[k] - b[k]) ** 2).sum() for k in b).sqrt()
+        den = sum((b[k] ** 2).sum() for k in b).sqrt()
+        return (num / den).item()
+    fp64 = None
+    if a.fp64_ref:  # exact-arithmetic yardstick: the same first step, torch path, float64
+        import copy
+        m64 = copy.deepcopy(m0).double()
+        m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in state0.items()})
+        m64.train()
+        m64.engine = "torch"
+        g64 = g.clone()
+        for k in ("x", "edge_attr", "BC"):
+            setattr(g64, k, getattr(g, k).double())
+        y64 = y.double()
+        dyn = m64.previous_t * m64.NUM_WATER_VARS
+        temp = g64.clone()
+        losses = []
+        for i in range(R):
+            temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, i], temp.node_BC,
+                                                        type_BC=temp.type_BC)
+            preds = m64(temp)
+            temp.x = use_prediction(temp.x, preds, m64.previous_t)
+            losses.append(rmse_loss(preds, y64[:, :, i], n0))
+        torch.stack(losses).mean().backward()
+        torch.nn.utils.clip_grad_norm_(m64.parameters(), 1.0)
+        g64s = {n: p.grad.detach().float() for n, p in m64.named_parameters() if p.grad is not None}
+        fp64 = {"hip_vs_fp64_global_rel": global_rel(g_hip, g64s), "torch_vs_fp64_global_rel": global_rel(g_torch, g64s),
+                "hip_vs_fp64_worst_tensor_rel": max(per_tensor(g_hip, g64s).values()),
+                "torch_vs_fp64_worst_tensor_rel": max(per_tensor(g_torch, g64s).values())}
+    pt = per_tensor(g_hip, g_torch)
+    worst_k = max(pt, key=pt.get)
     print(json.dumps({"workload": a.workload, "fine_nodes": n0, "all_nodes": desc["all_nodes"],
-                      "rollout_steps_per_training_step": R,
+                      "rollout_steps_per_training_step": R, "hip_parts": sorted(parts),
                       "hip_ms_per_training_step": t_hip * 1e3, "torch_ms_per_training_step": t_torch * 1e3,
                       "speedup": t_torch / t_hip,
                       "fine_node_steps_per_s_hip": n0 * R / t_hip,
                       "fine_node_steps_per_s_torch": n0 * R / t_torch,
                       "first_loss_hip": l_hip, "first_loss_torch": l_torch,
-                      "first_step_grad_max_rel_diff": worst,
-                      "note": "SWEGNN layers (7 processors + 3 unpooling) on HIP training kernels; "
-                              "encoders, pooling, decoder, loss, optimizer: torch on the same GPU"}),
+                      "first_step_grad": {
+                          "hip_vs_torch_global_rel": global_rel(g_hip, g_torch),
+                          "hip_vs_torch_worst_tensor": [worst_k, pt[worst_k]],
+                          "torch_vs_torch_global_rel": global_rel(g_torch2, g_torch),
+                          "torch_vs_torch_worst_tensor_rel": max(per_tensor(g_torch2, g_torch).values()),
+                          "hip_vs_hip_max_abs": max((g_hip2[k] - g_hip[k]).abs().max().item() for k in g_hip),
+                          "fp64": fp64},
+                      "note": "SWEGNN layers (7 processors + 3 unpooling), encoders, decoder and mean pooling on "
+                              "HIP training kernels; scale selections, loss, clipping, AdamW: torch on the same "
+                              "GPU. Gradients after clip_grad_norm_(1.0) of the first training step."}),
           flush=True)
 
 
