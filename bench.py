@@ -324,16 +324,18 @@ def strong_scaling_section(dist, rank, world, dev, engine, sets, T, steps, warmu
     return rec
 
 
-def partitioned_rollout_check(rank, world, barrier, timeout=300):
+def partitioned_rollout_check(rank, world, barrier, timeout=300, parts=2, mesh="zenodo4", steps=5):
     """Single-mesh domain decomposition over RCCL: rank 0 runs
-    tools/rccl_partition_check.py (two fresh processes on GPUs 0 and 1, DistributedRollout
-    with the RCCL halo exchange, gather_owned over RCCL, compared with the undivided plan) as
-    a child with a time limit -- recorded, never fatal, and a hang cannot stall the bench."""
+    tools/rccl_partition_check.py (`parts` fresh processes on GPUs 0..parts-1,
+    DistributedRollout with the RCCL halo exchange, gather_owned over RCCL, compared with the
+    undivided plan) as a child with a time limit -- recorded, never fatal, and a hang cannot
+    stall the bench."""
     res = None
     if rank == 0:
         import signal
         import subprocess
-        cmd = [sys.executable, os.path.join(ROOT, "tools", "rccl_partition_check.py"), "2", "--mesh", "zenodo4"]
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "rccl_partition_check.py"), str(parts), "--mesh", mesh,
+               "--steps", str(steps), "--wait", str(max(30, timeout - 30))]
         env = {k: v for k, v in os.environ.items()
                if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
                             "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
@@ -388,6 +390,8 @@ def main():
                     help="N > 1: fixed config-3 sets (G simulations each) of the strong_scaling "
                          "record; '' = none")
     ap.add_argument("--strong-steps", type=int, default=3)
+    ap.add_argument("--no-partition-large", action="store_true",
+                    help="N > 1: skip the ~1.3M-node mesh in the RCCL single-mesh decomposition record")
     ap.add_argument("--no-partition-check", action="store_true",
                     help="N > 1: skip the RCCL single-mesh decomposition check")
     args = ap.parse_args()
@@ -518,7 +522,13 @@ def main():
             except Exception as e:  # noqa: BLE001
                 strong = {"error": repr(e)}
         if not args.no_partition_check and backend == "nccl" and torch.cuda.device_count() >= 2:
-            part_check = partitioned_rollout_check(rank, world, cpu_barrier)
+            # zenodo4 over two GPUs (transport check), then config 5's ~1.3M-node mesh over
+            # every rank's GPU: the single-mesh strong scaling of SURVEY §8 f2
+            part_check = {"zenodo4_2_parts": partitioned_rollout_check(rank, world, cpu_barrier)}
+            if not args.no_partition_large:
+                W = min(world, torch.cuda.device_count())
+                part_check[f"hbm1m_{W}_parts"] = partitioned_rollout_check(
+                    rank, world, cpu_barrier, timeout=420, parts=W, mesh="hbm1m", steps=2)
 
     result = None
     if rank == 0:

@@ -1,0 +1,14 @@
+# round-3 session C (after the training / F = 64 changes): smoke, full GPU tests, default bench, rocprofv3 kernel trace of the bench
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r03c; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 3
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+echo "tests rc=$?" >> $O/steps.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 5
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/$O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_prof.json 2> $O/bench_prof.err || exit 6
+echo ok >> $O/steps.log
+# the RCCL partition check on the ~1M-node mesh, one rank (nccl world of 1: the tool's path, no peers)
+timeout -k 10 420 python tools/rccl_partition_check.py 1 --mesh hbm1m --steps 2 --wait 360 > $O/partition_hbm1m_w1.json 2> $O/partition_hbm1m_w1.err
+echo "partition rc=$?" >> $O/steps.log

@@ -5,7 +5,12 @@ all-gather over RCCL (gather_owned), compared with the undivided rollout of the 
 Prints one JSON line.  Needs W GPUs (RCCL refuses two ranks on one device); bench.py runs it
 at N > 1 with a time limit.
 
-    python tools/rccl_partition_check.py [W] [--mesh zenodo4|small] [--steps 5]
+    python tools/rccl_partition_check.py [W] [--mesh zenodo4|hbm1m|small] [--steps 5] [--T 48]
+
+--mesh names a bench.py workload (its mesh, model and weights: zenodo4 = K4_F32 on the
+4-scale Zenodo-size mesh, hbm1m = config 5's ~1.3M-node 3-scale mesh, fully wet) or `small`
+(K4_F32 on the small test mesh).  The record holds both times, so on the ~1M-node mesh it is
+the single-mesh strong-scaling number of SURVEY §8 f2 (undivided / distributed).
 """
 import argparse
 import json
@@ -21,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "mswe-gnn_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
 
 
-def worker(rank, world, port, q, mesh, steps):
+def worker(rank, world, port, q, mesh, steps, T):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     dev = torch.device(f"cuda:{rank}")
@@ -31,9 +36,14 @@ def worker(rank, world, port, q, mesh, steps):
         from conftest import build_msgnn, weights, per_step_rel
         from mswegnn.mesh import make_multiscale_mesh, mesh_config
         from mswegnn.partition import DistributedRollout
-        T = 48
-        g = make_multiscale_mesh(**mesh_config(mesh), T=T)
-        m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(dev)
+        if mesh == "small":
+            g = make_multiscale_mesh(**mesh_config(mesh), T=T)
+            m = build_msgnn(4, 32, 4, state=weights("K4_F32"))
+        else:
+            sys.path.insert(0, ROOT)
+            import bench
+            g, m, _, _ = bench.build_workload(mesh, seed=0, T=T)
+        m = m.to(dev)
         m.engine = "hip"
         dr = DistributedRollout(m, g, device=dev)
         x0 = g.x.to(dev)
@@ -64,6 +74,7 @@ def worker(rank, world, port, q, mesh, steps):
                    "bit_identical": bool(torch.equal(full, whole)),
                    "distributed_ms_per_rollout": float(dt.item()) * 1e3,
                    "undivided_ms_per_rollout": t_whole * 1e3,
+                   "speedup_vs_undivided": t_whole / float(dt.item()),
                    "transport": "RCCL (msw_plan_set_comm: grouped ncclSend/ncclRecv halo exchange; "
                                 "gather_owned: torch.distributed all_gather on nccl)"})
         dr.close()
@@ -79,6 +90,8 @@ def main():
     ap.add_argument("W", nargs="?", type=int, default=2)
     ap.add_argument("--mesh", default="small")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--T", type=int, default=48)
+    ap.add_argument("--wait", type=float, default=240.0, help="seconds to wait for rank 0's record")
     a = ap.parse_args()
     if torch.cuda.device_count() < a.W:
         print(json.dumps({"error": f"needs {a.W} GPUs, {torch.cuda.device_count()} visible"}))
@@ -88,14 +101,14 @@ def main():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=worker, args=(r, a.W, port, q, a.mesh, a.steps), daemon=True)
+    procs = [ctx.Process(target=worker, args=(r, a.W, port, q, a.mesh, a.steps, a.T), daemon=True)
              for r in range(a.W)]
     for p in procs:
         p.start()
     try:
-        res = q.get(timeout=240)
+        res = q.get(timeout=a.wait)
     except Exception:  # noqa: BLE001  (queue.Empty: a rank hung)
-        res = {"error": "no result within 240 s"}
+        res = {"error": f"no result within {a.wait:.0f} s"}
     for p in procs:
         p.join(60)
         if p.is_alive():
