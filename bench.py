@@ -524,11 +524,12 @@ def main():
         if not args.no_partition_check and backend == "nccl" and torch.cuda.device_count() >= 2:
             # zenodo4 over two GPUs (transport check), then config 5's ~1.3M-node mesh over
             # every rank's GPU: the single-mesh strong scaling of SURVEY §8 f2
-            part_check = {"zenodo4_2_parts": partitioned_rollout_check(rank, world, cpu_barrier)}
-            if not args.no_partition_large:
-                W = min(world, torch.cuda.device_count())
+            # (the large mesh at N >= 4 only, to bound the driver's N = 2 / 4 / 8 sequence)
+            part_check = {"zenodo4_2_parts": partitioned_rollout_check(rank, world, cpu_barrier, timeout=180)}
+            W = min(world, torch.cuda.device_count())
+            if not args.no_partition_large and W >= 4:
                 part_check[f"hbm1m_{W}_parts"] = partitioned_rollout_check(
-                    rank, world, cpu_barrier, timeout=420, parts=W, mesh="hbm1m", steps=2)
+                    rank, world, cpu_barrier, timeout=240, parts=W, mesh="hbm1m", steps=2)
 
     result = None
     if rank == 0:

@@ -182,3 +182,23 @@ def test_mean_pooling_gradients_vs_torch_autograd(cuda):
         ours = run(lambda xx: pool_apply(xx, pe))
         e = _compare(ours, ref, f"pool level {i}")
         print(f"pool level {i}: worst rel err {e:.2e}")
+
+
+def test_ddp_training_step_two_ranks(cuda):
+    """DistributedDataParallel over the HIP training kernels (what the reference's Lightning
+    Trainer does on a multi-GPU node): two ranks (gloo, both on cuda:0 on a one-GPU box) run one
+    loss backward each; the all-reduced gradients == one process's mean of both ranks' loss
+    gradients (tools/ddp_train_check.py)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "tools", "ddp_train_check.py"), "2", "--backend", "gloo"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, p.stderr[-2000:]
+    res = json.loads(lines[-1])
+    print(res)
+    assert p.returncode == 0, res
