@@ -88,6 +88,7 @@ struct GemmArgs {
   float* pre; long ldp;           // pre-activation store (nullable)
   int act; const float* slope;    // activation of the stored C (device scalar slope)
   float* part; int kchunk;        // split-K partials
+  int bones;                      // B(k, N - 1) = 1: an implicit ones column (bias gradient)
 };
 
 __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int n = n0 + bn[u], k = k0 + bk[u];
-      rb[u] = (n < a.N && k < ke) ? a.B[(long)k * a.lbk + (long)n * a.lbn] : 0.f;
+      rb[u] = (n < a.N && k < ke) ? ((a.bones && n == a.N - 1) ? 1.f : a.B[(long)k * a.lbk + (long)n * a.lbn]) : 0.f;
     }
   };
   if (kb < ke) fetch(kb);
@@ -195,6 +196,33 @@ __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ pa
     red[p][c] = v;
     __syncthreads();
     if (p == 0 && i < count) out[i] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    __syncthreads();
+  }
+}
+
+// k_sum_splits over [M][N1] partials whose last column is the bias gradient: columns < N1 - 1
+// go to dW [M][N1 - 1], the last to db [M]
+__global__ __launch_bounds__(256) void k_sum_splits_wb(const float* __restrict__ part, int splits, int M, int N1,
+                                                       float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
+  const long count = (long)M * N1;
+  for (long i0 = blockIdx.x * 64L; i0 < count; i0 += gridDim.x * 64L) {
+    const long i = i0 + c;
+    float v = 0.f;
+    if (i < count) {
+#pragma unroll 8
+      for (int s = p; s < splits; s += 4) v += part[(long)s * count + i];
+    }
+    red[p][c] = v;
+    __syncthreads();
+    if (p == 0 && i < count) {
+      const float t = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+      const long m = i / N1;
+      const int n = (int)(i - m * N1);
+      if (n < N1 - 1) dW[m * (N1 - 1) + n] = t;
+      else db[m] = t;
+    }
     __syncthreads();
   }
 }
@@ -509,7 +537,7 @@ bool layout_of(const msw_swegnn_train_desc* d, Layout& y) {
   y.ds = o; o += al(E * F);
   y.dA = o; o += al(E * y.wmax);
   y.dB = o; o += al(E * y.wmax);
-  y.part = o; o += al((long)kMaxSplits * y.wmax * y.wmax);
+  y.part = o; o += al((long)kMaxSplits * y.wmax * (y.wmax + 1));
   y.spart = o; o += al(kMaxSplits * 4L);
   y.scratch = o;
   return true;
@@ -551,7 +579,7 @@ bool mlp_layout_of(const msw_mlp_train_desc* d, MlpLayout& y) {
   o = 0;
   y.A = o; o += al(R * y.wmax);
   y.B = o; o += al(R * y.wmax);
-  y.part = o; o += al((long)kMaxSplits * y.wmax * y.wmax);
+  y.part = o; o += al((long)kMaxSplits * y.wmax * (y.wmax + 1));
   y.spart = o; o += al(kMaxSplits * 4L);
   y.scratch = o;
   return true;
@@ -575,19 +603,27 @@ hipError_t gemm(const GemmArgs& a0, hipStream_t st, int splits = 1) {
 }
 
 // dW [M][N] = sum_rows A(row, m) B(row, n): split-K over the rows, partials summed in order
+// db (nullable) [M] = sum_rows A(row, m): the same GEMM against an implicit ones column of B
+// (part: [splits][M][N + 1] floats then)
 hipError_t weight_grad(const float* A, int lda, const float* B, int ldb, long R, int M, int N, float* part,
-                       float* dW, hipStream_t st) {
+                       float* dW, hipStream_t st, float* db = nullptr) {
   GemmArgs g{};
-  g.M = M; g.N = N; g.K = (int)R;
+  g.M = M; g.N = db ? N + 1 : N; g.K = (int)R;
   g.A = A; g.lam = 1; g.lak = lda;
   g.B = B; g.lbk = ldb; g.lbn = 1;
   g.part = part;
+  g.bones = db ? 1 : 0;
   const int splits = (int)std::min<long>(kMaxSplits, std::max<long>(1, R / (8 * kBK)));
   hipError_t e = gemm(g, st, splits);
   if (e != hipSuccess) return e;
   const int kchunk = ((g.K + splits - 1) / splits + kBK - 1) / kBK * kBK;
   const int used = std::max(1, (g.K + kchunk - 1) / kchunk);
-  hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N, 64)), dim3(256), 0, st, part, used, (long)M * N, dW);
+  if (db)
+    hipLaunchKernelGGL(k_sum_splits_wb, dim3(blocks_for((long)M * g.N, 64)), dim3(256), 0, st, part, used, M, g.N, dW,
+                       db);
+  else
+    hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N, 64)), dim3(256), 0, st, part, used, (long)M * N,
+                       dW);
   return hipGetLastError();
 }
 
@@ -631,13 +667,17 @@ hipError_t mlp_backward(const MlpRun& m, const float* X, const float* const* pre
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (dslope[l]) hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, st, spart, ab, 1L, dslope[l]);
-    if (db[l]) {
+    // the bias gradient rides on the weight-gradient GEMM as an extra ones column of X where
+    // that column fits the last 64-wide output tile; else its own column sums
+    const bool fuse_db = db[l] && dW[l] && wi % kBN != 0;
+    if (db[l] && !fuse_db) {
       hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, R, wo, rchunk, part);
       hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo, 64)), dim3(256), 0, st, part, nrs, (long)wo, db[l]);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const float* Xl = l == 0 ? X : post[l - 1];
-    if (dW[l] && (e = weight_grad(dpre, wo, Xl, wi, R, wo, wi, part, dW[l], st)) != hipSuccess) return e;
+    if (dW[l] && (e = weight_grad(dpre, wo, Xl, wi, R, wo, wi, part, dW[l], st, fuse_db ? db[l] : nullptr)) != hipSuccess)
+      return e;
     float* tgt = l == 0 ? dX : bufA;
     if (tgt) {
       GemmArgs g{};  // d X_l = dpre W_l
