@@ -173,10 +173,11 @@ class _SwegnnFunction(torch.autograd.Function):
         n_saved, _ = _ws(meta)
         saved = torch.empty(n_saved, device=dev, dtype=torch.float32)
         out = torch.empty(meta.csr.num_nodes, meta.F, device=dev, dtype=torch.float32)
-        L.check(L.lib().msw_swegnn_train_forward(C.byref(d), x_s.data_ptr(), x_d.data_ptr(),
-                                                 ea.data_ptr() if ea is not None else None,
-                                                 saved.data_ptr(), out.data_ptr(),
-                                                 C.c_void_p(_raw_stream(dev.index or 0))))
+        with torch.cuda.device(dev):  # the kernels launch on the current device
+            L.check(L.lib().msw_swegnn_train_forward(C.byref(d), x_s.data_ptr(), x_d.data_ptr(),
+                                                     ea.data_ptr() if ea is not None else None,
+                                                     saved.data_ptr(), out.data_ptr(),
+                                                     C.c_void_p(_raw_stream(dev.index or 0))))
         ctx.meta = meta
         ctx.has_ea = edge_attr is not None
         ctx.save_for_backward(x_s, x_d, ea if ea is not None else torch.empty(0, device=dev), saved, *params)
@@ -213,10 +214,11 @@ class _SwegnnFunction(torch.autograd.Function):
             for k in range(meta.layer.K + 1):
                 f = next(it)
                 g.d_filter[k] = f.data_ptr() if f is not None else None
-        L.check(L.lib().msw_swegnn_train_backward(C.byref(d), x_s.data_ptr(), x_d.data_ptr(),
-                                                  ea.data_ptr() if meta.ef > 0 else None, saved.data_ptr(),
-                                                  gout.data_ptr(), C.byref(g), scratch.data_ptr(),
-                                                  C.c_void_p(_raw_stream(dev.index or 0))))
+        with torch.cuda.device(dev):  # the kernels launch on the current device
+            L.check(L.lib().msw_swegnn_train_backward(C.byref(d), x_s.data_ptr(), x_d.data_ptr(),
+                                                      ea.data_ptr() if meta.ef > 0 else None, saved.data_ptr(),
+                                                      gout.data_ptr(), C.byref(g), scratch.data_ptr(),
+                                                      C.c_void_p(_raw_stream(dev.index or 0))))
         return (None, dxs, dxd, dea if ctx.has_ea else None, *dps)
 
 
@@ -284,8 +286,9 @@ class _MlpFunction(torch.autograd.Function):
         n_saved, _ = meta.workspace()
         saved = torch.empty(max(n_saved, 1), device=dev, dtype=torch.float32)
         out = torch.empty(x.shape[0], meta.layers[-1][0].out_features, device=dev, dtype=torch.float32)
-        L.check(L.lib().msw_mlp_train_forward(C.byref(d), x.data_ptr(), saved.data_ptr(), out.data_ptr(),
-                                              C.c_void_p(_raw_stream(dev.index or 0))))
+        with torch.cuda.device(dev):  # the kernels launch on the current device
+            L.check(L.lib().msw_mlp_train_forward(C.byref(d), x.data_ptr(), saved.data_ptr(), out.data_ptr(),
+                                                  C.c_void_p(_raw_stream(dev.index or 0))))
         ctx.meta = meta
         ctx.save_for_backward(x, saved, *params)
         return out
@@ -313,9 +316,10 @@ class _MlpFunction(torch.autograd.Function):
             if isinstance(act, nn.PReLU):
                 a = next(it)
                 g.d_slope[i] = a.data_ptr() if a is not None else None
-        L.check(L.lib().msw_mlp_train_backward(C.byref(d), x.data_ptr(), saved.data_ptr(), gout.data_ptr(),
-                                               C.byref(g), scratch.data_ptr(),
-                                               C.c_void_p(_raw_stream(dev.index or 0))))
+        with torch.cuda.device(dev):  # the kernels launch on the current device
+            L.check(L.lib().msw_mlp_train_backward(C.byref(d), x.data_ptr(), saved.data_ptr(), gout.data_ptr(),
+                                                   C.byref(g), scratch.data_ptr(),
+                                                   C.c_void_p(_raw_stream(dev.index or 0))))
         if dx is not None and x.shape[0] == 0:
             dx.zero_()
         return (None, dx, *dps)
@@ -334,9 +338,10 @@ class _PoolFunction(torch.autograd.Function):
         x = x.contiguous()
         out = torch.empty_like(x)
         dev = x.device
-        L.check(L.lib().msw_pool_mean_forward(csr.num_nodes, int(x.shape[1]), csr.col.data_ptr(),
-                                              csr.out_ptr.data_ptr(), csr.out_edge.data_ptr(), x.data_ptr(),
-                                              out.data_ptr(), C.c_void_p(_raw_stream(dev.index or 0))))
+        with torch.cuda.device(dev):  # the kernels launch on the current device
+            L.check(L.lib().msw_pool_mean_forward(csr.num_nodes, int(x.shape[1]), csr.col.data_ptr(),
+                                                  csr.out_ptr.data_ptr(), csr.out_edge.data_ptr(), x.data_ptr(),
+                                                  out.data_ptr(), C.c_void_p(_raw_stream(dev.index or 0))))
         ctx.csr = csr
         return out
 
@@ -346,10 +351,11 @@ class _PoolFunction(torch.autograd.Function):
         gout = gout.contiguous().to(torch.float32)
         dx = torch.empty_like(gout)
         dev = gout.device
-        L.check(L.lib().msw_pool_mean_backward(csr.num_nodes, int(gout.shape[1]), csr.row.data_ptr(),
-                                               csr.out_ptr.data_ptr(), csr.in_ptr.data_ptr(),
-                                               csr.in_edge.data_ptr(), gout.data_ptr(), dx.data_ptr(),
-                                               C.c_void_p(_raw_stream(dev.index or 0))))
+        with torch.cuda.device(dev):  # the kernels launch on the current device
+            L.check(L.lib().msw_pool_mean_backward(csr.num_nodes, int(gout.shape[1]), csr.row.data_ptr(),
+                                                   csr.out_ptr.data_ptr(), csr.in_ptr.data_ptr(),
+                                                   csr.in_edge.data_ptr(), gout.data_ptr(), dx.data_ptr(),
+                                                   C.c_void_p(_raw_stream(dev.index or 0))))
         return None, dx
 
 

@@ -202,3 +202,36 @@ def test_ddp_training_step_two_ranks(cuda):
     res = json.loads(lines[-1])
     print(res)
     assert p.returncode == 0, res
+
+
+def test_batched_training_step_gradients(cuda):
+    """The reference's training_step on a 2-graph batch (adapt_batch_training regrouping,
+    training/train.py:125-145, 2 rollout steps with the prediction fed back): every gradient
+    with all layers on the HIP training kernels vs the all-torch model."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import adapt_batch_training, apply_boundary_condition, use_prediction
+    ga = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=1, T=3), seed=2)
+    gb = wet_state(make_multiscale_mesh(n_coarse=3, num_scales=4, seed=2, T=3), seed=3)
+    batch = collate([ga, gb]).to(cuda)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+    m.train()
+    tgt = torch.rand(batch.x.shape[0], 2, 2, device=cuda, generator=torch.Generator(cuda).manual_seed(9))
+
+    def step(engine):
+        m.zero_grad(set_to_none=True)
+        m.engine = engine
+        temp = adapt_batch_training(batch)
+        dyn = m.previous_t * m.NUM_WATER_VARS
+        losses = []
+        for i in range(2):
+            temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, i], temp.node_BC,
+                                                        type_BC=temp.type_BC)
+            preds = m(temp)
+            temp.x = use_prediction(temp.x, preds, m.previous_t)
+            losses.append(((preds - tgt[:, :, i]) ** 2).mean())
+        torch.stack(losses).mean().backward()
+        return {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    ref = step("torch")
+    ours = step("auto")
+    e = _compare(ours, ref, "batched MSGNN")
+    print(f"batched MSGNN training step: worst rel err {e:.2e} over {len(ref)} gradients")
