@@ -2635,6 +2635,13 @@ hipError_t prepare_kernels() {
       if (e != hipSuccess) return e;
     }
   }
+  if constexpr (NT == 4) {  // F = 64 cooperative encoder on two waves per row tile
+    for (const void* f : {(const void*)k_encode_coop<NT, 1, false, 2>, (const void*)k_encode_coop<NT, -1, false, 2>,
+                          (const void*)k_encode_coop<NT, 1, true, 2>, (const void*)k_encode_coop<NT, -1, true, 2>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx(enc_coop_waves<NT>()));
+      if (e != hipSuccess) return e;
+    }
+  }
   if constexpr (NT >= 2) {  // cooperative last hops (F = 32, 64)
     for (int prelu = 0; prelu < 2; ++prelu) {
       hipError_t e = hipFuncSetAttribute(hop_coop_kernel<NT>(prelu), hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
@@ -2676,6 +2683,24 @@ hipError_t prepare_kernels() {
 template <int NT>
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   if (a.Npad <= 0) return hipSuccess;
+  if constexpr (NT == 4) {
+    if (a.coop == 2) {  // F = 64 on two waves per row tile (MSW_ENC_COOP_P=2)
+      constexpr int P = 2, WV = enc_coop_waves<NT>();
+      const dim3 grid(a.Npad / ((WV / P) * kRowsPerWave)), block(64 * WV);
+      const size_t sh = lds_bytes<NT>(a.lds_floats);
+      if (a.dec.on) {
+        if (a.c.prelu)
+          hipLaunchKernelGGL((k_encode_coop<NT, 1, true, P>), grid, block, sh, st, a);
+        else
+          hipLaunchKernelGGL((k_encode_coop<NT, -1, true, P>), grid, block, sh, st, a);
+      } else if (a.c.prelu) {
+        hipLaunchKernelGGL((k_encode_coop<NT, 1, false, P>), grid, block, sh, st, a);
+      } else {
+        hipLaunchKernelGGL((k_encode_coop<NT, -1, false, P>), grid, block, sh, st, a);
+      }
+      return hipGetLastError();
+    }
+  }
   if constexpr (NT >= 2) {
     if (a.coop == NT) {  // P = NT waves per row tile (F = 32: 2, F = 64: 4)
       constexpr int P = NT, WV = enc_coop_waves<NT>();

@@ -1034,6 +1034,9 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       bool coop = P->NT == 4 && (long)(L.enc.Npad / kRowsPerWave) * P->NT <= kEncCoopWaves;
       if (const char* ec = getenv("MSW_ENC_COOP")) coop = P->NT >= 2 && atoi(ec) != 0;
       L.enc.coop = coop ? P->NT : 0;
+      // MSW_ENC_COOP_P=2: F = 64 on two waves per row tile instead of four (A/B)
+      if (const char* cp = getenv("MSW_ENC_COOP_P"))
+        if (coop && P->NT == 4 && atoi(cp) == 2) L.enc.coop = 2;
       break;
     }
     case L_EDGE_MLP: {

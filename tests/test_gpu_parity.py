@@ -558,13 +558,15 @@ def test_split_edge_mlp_matches_fused(cuda, F, monkeypatch):
     assert per_step_rel(outs["1"][3][:ga.num_nodes], ref) <= REL_TOL
 
 
-@pytest.mark.parametrize("F", [32, 64])
-def test_coop_encoder_matches_single_wave(cuda, F, monkeypatch):
+@pytest.mark.parametrize("F,P", [(32, None), (64, None), (64, "2")])
+def test_coop_encoder_matches_single_wave(cuda, F, P, monkeypatch):
     """k_encode_coop (F / 16 waves per 16-row tile, every MFMA layer's output tiles split over
     them; the F = 64 default while that leaves <= 4 waves per SIMD) == k_encode (MSW_ENC_COOP=0), bit
     for bit: forward (encoders, projection 0, unpool V) and rollout (the previous step's
     decoder in the encoder launch, the final decode-only launch); and vs the oracle."""
     g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=7)
+    if P:  # F = 64 on two waves per row tile (MSW_ENC_COOP_P=2) instead of four
+        monkeypatch.setenv("MSW_ENC_COOP_P", P)
     outs = {}
     for sv in ("0", "1"):
         monkeypatch.setenv("MSW_ENC_COOP", sv)
