@@ -73,6 +73,40 @@ def test_abi_rejects_null_arguments_without_gpu(libso):
     assert libso.msw_plan_destroy(None) == 0
 
 
+def test_training_abi_validation_and_workspace_without_gpu(libso):
+    """The training entry points (msw_mlp_train_*, msw_swegnn_train_*, msw_pool_mean_*) size
+    their workspaces and reject inconsistent descriptors / null buffers on the host, before
+    any HIP call (no GPU here)."""
+    from mswegnn import _lib as L
+    lib = L.lib()
+    d = L.MswMlpTrainDesc()
+    d.rows, d.n_layers = 100, 3
+    for i, w in enumerate((9, 32, 32, 2)):
+        d.width[i] = w
+    s, t = C.c_int64(), C.c_int64()
+    assert lib.msw_mlp_train_workspace(C.byref(d), C.byref(s), C.byref(t)) != 0  # weights missing
+    for i in range(3):
+        d.weight[i] = 16  # any non-null address: the workspace call only validates
+    assert lib.msw_mlp_train_workspace(C.byref(d), C.byref(s), C.byref(t)) == 0
+    al = lambda n: (n + 63) // 64 * 64  # noqa: E731
+    assert s.value == al(100 * 32) + al(100 * 32) + al(100 * 2) + al(100 * 32) + al(100 * 32)
+    assert t.value == 2 * al(100 * 32) + al(256 * 32 * 33) + al(256 * 4)
+    assert lib.msw_mlp_train_forward(C.byref(d), None, None, None, None) != 0
+    assert b"null" in lib.msw_last_error()
+    d.width[3] = 0
+    assert lib.msw_mlp_train_workspace(C.byref(d), C.byref(s), C.byref(t)) != 0
+    sd = L.MswSwegnnTrainDesc()
+    sd.num_nodes, sd.num_edges, sd.F, sd.edge_features, sd.K, sd.n_layers = 10, 30, 32, 32, 4, 3
+    for i, w in enumerate((160, 64, 64, 32)):
+        sd.width[i] = w
+    assert lib.msw_swegnn_train_workspace(C.byref(sd), C.byref(s), C.byref(t)) == 0 and s.value > 0
+    sd.width[0] = 161  # != 4F + edge_features
+    assert lib.msw_swegnn_train_workspace(C.byref(sd), C.byref(s), C.byref(t)) != 0
+    assert lib.msw_pool_mean_forward(-1, 32, None, None, None, None, None, None) != 0
+    assert lib.msw_pool_mean_forward(0, 32, None, None, None, None, None, None) == 0  # nothing to do
+    assert lib.msw_pool_mean_backward(5, 32, None, None, None, None, None, None, None) != 0
+
+
 def test_mesh_generator_invariants():
     """Appendix B / SURVEY §8 sizes and the structural facts the engine relies on."""
     g = make_multiscale_mesh(**mesh_config("zenodo4"), T=4)
