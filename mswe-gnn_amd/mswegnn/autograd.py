@@ -113,11 +113,27 @@ def supported(layer, x_s, x_d, edge_attr):
     return all(p.dtype == torch.float32 and p.is_cuda for p in layer.parameters())
 
 
+def _param_list(layer=None, seq=None):
+    """The parameter objects a descriptor binds, in its order (cache validation)."""
+    out = []
+    for m in (layer.edge_mlp if layer is not None else seq):
+        if isinstance(m, nn.Linear):
+            out.append(m.weight)
+            if m.bias is not None:
+                out.append(m.bias)
+        elif isinstance(m, nn.PReLU):
+            out.append(m.weight)
+    if layer is not None and layer.with_filter_matrix:
+        out += [f.weight for f in layer.filter_matrix]
+    return out
+
+
 class _Meta:
     """Everything but the tensors autograd tracks: the descriptor template of one call."""
 
     def __init__(self, layer, layers, csr, F, ef):
         self.layer, self.layers, self.csr, self.F, self.ef = layer, layers, csr, F, ef
+        self.ws = None
         d = L.MswSwegnnTrainDesc()
         d.num_nodes, d.num_edges = csr.num_nodes, csr.num_edges
         d.F, d.edge_features, d.K, d.n_layers = F, ef, layer.K, len(layers)
@@ -157,9 +173,30 @@ class _Meta:
 
 
 def _ws(meta):
-    s, t = C.c_int64(), C.c_int64()
-    L.check(L.lib().msw_swegnn_train_workspace(C.byref(meta.desc), C.byref(s), C.byref(t)))
-    return int(s.value), int(t.value)
+    if meta.ws is None:  # depends on the descriptor's sizes only
+        s, t = C.c_int64(), C.c_int64()
+        L.check(L.lib().msw_swegnn_train_workspace(C.byref(meta.desc), C.byref(s), C.byref(t)))
+        meta.ws = int(s.value), int(t.value)
+    return meta.ws
+
+
+_META_CACHE = OrderedDict()
+_META_KEEP = 64
+
+
+def _cached_meta(key, params_now, make):
+    """Descriptor templates reused across calls (their ctypes structs cost more host time than
+    the launches): keyed by the module and graph; valid while the module holds the same
+    parameter objects (a replaced Parameter rebuilds it)."""
+    hit = _META_CACHE.get(key)
+    if hit is not None and len(hit.params) == len(params_now) and all(a is b for a, b in zip(hit.params, params_now)):
+        _META_CACHE.move_to_end(key)
+        return hit
+    meta = make()
+    _META_CACHE[key] = meta
+    while len(_META_CACHE) > _META_KEEP:
+        _META_CACHE.popitem(last=False)
+    return meta
 
 
 class _SwegnnFunction(torch.autograd.Function):
@@ -224,11 +261,13 @@ class _SwegnnFunction(torch.autograd.Function):
 
 def swegnn_apply(layer, x_s, x_d, edge_index, edge_attr=None):
     """SWEGNN.forward of `layer` on the HIP training kernels (differentiable)."""
-    layers = _mlp_layers(layer.edge_mlp)
     F = int(x_d.shape[1])
     ef = int(layer.edge_features) if layer.edge_features > 0 else 0
     csr = graph_csr(edge_index, x_d.shape[0])
-    meta = _Meta(layer, layers, csr, F, ef)
+    key = ("swegnn", id(layer), id(csr), F, ef, layer.K, bool(layer.normalize), bool(layer.with_filter_matrix),
+           bool(layer.with_gradient), bool(layer.upwind_mode))
+    meta = _cached_meta(key, _param_list(layer),
+                        lambda: _Meta(layer, _mlp_layers(layer.edge_mlp), csr, F, ef))
     if ef > 0 and edge_attr.dim() == 1:
         edge_attr = edge_attr.unsqueeze(1)
     return _SwegnnFunction.apply(meta, x_s, x_d, edge_attr if ef > 0 else None, *meta.params)
@@ -247,6 +286,7 @@ def mlp_supported(seq, x):
 class _MlpMeta:
     def __init__(self, layers, rows):
         self.layers = layers
+        self.ws = None
         d = L.MswMlpTrainDesc()
         d.rows, d.n_layers = rows, len(layers)
         d.width[0] = layers[0][0].in_features
@@ -271,9 +311,11 @@ class _MlpMeta:
         return d
 
     def workspace(self):
-        s, t = C.c_int64(), C.c_int64()
-        L.check(L.lib().msw_mlp_train_workspace(C.byref(self.desc), C.byref(s), C.byref(t)))
-        return int(s.value), int(t.value)
+        if self.ws is None:
+            s, t = C.c_int64(), C.c_int64()
+            L.check(L.lib().msw_mlp_train_workspace(C.byref(self.desc), C.byref(s), C.byref(t)))
+            self.ws = int(s.value), int(t.value)
+        return self.ws
 
 
 class _MlpFunction(torch.autograd.Function):
@@ -327,7 +369,8 @@ class _MlpFunction(torch.autograd.Function):
 
 def mlp_apply(seq, x):
     """make_mlp `seq` applied to x [rows][in] on the HIP training kernels (differentiable)."""
-    meta = _MlpMeta(_mlp_layers(seq), int(x.shape[0]))
+    rows = int(x.shape[0])
+    meta = _cached_meta(("mlp", id(seq), rows), _param_list(seq=seq), lambda: _MlpMeta(_mlp_layers(seq), rows))
     MLP_CALLS[0] += 1
     return _MlpFunction.apply(meta, x, *meta.params)
 

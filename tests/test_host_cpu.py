@@ -107,6 +107,29 @@ def test_training_abi_validation_and_workspace_without_gpu(libso):
     assert lib.msw_pool_mean_backward(5, 32, None, None, None, None, None, None, None) != 0
 
 
+def test_training_descriptor_cache_keys_follow_parameters():
+    """mswegnn/autograd.py reuses a layer's descriptor template while the layer holds the same
+    parameter objects: the validation list (_param_list) is the descriptor's own binding order
+    for every SWEGNN layer and make_mlp stack of the model, and a replaced Parameter changes it."""
+    from conftest import build_msgnn
+    from mswegnn import autograd as ag
+    m = build_msgnn(4, 32, 4)
+    g = make_multiscale_mesh(**mesh_config("tiny"), T=2)
+    csr = ag.GraphCSR(g.edge_index, g.num_nodes)
+    for layer in list(m.gnn_processor) + list(m.intra_scale_gnn):
+        ef = int(layer.edge_features) if layer.edge_features > 0 else 0
+        meta = ag._Meta(layer, ag._mlp_layers(layer.edge_mlp), csr, 32, ef)
+        assert [id(p) for p in meta.params] == [id(p) for p in ag._param_list(layer)]
+    for seq in (m.edge_encoder, m.static_node_encoder, m.dynamic_node_encoder, m.node_decoder):
+        meta = ag._MlpMeta(ag._mlp_layers(seq), 7)
+        assert [id(p) for p in meta.params] == [id(p) for p in ag._param_list(seq=seq)]
+    layer = m.gnn_processor[0]
+    before = ag._param_list(layer)
+    layer.filter_matrix[1].weight = torch.nn.Parameter(layer.filter_matrix[1].weight.detach().clone())
+    after = ag._param_list(layer)
+    assert len(before) == len(after) and any(a is not b for a, b in zip(before, after))
+
+
 def test_mesh_generator_invariants():
     """Appendix B / SURVEY §8 sizes and the structural facts the engine relies on."""
     g = make_multiscale_mesh(**mesh_config("zenodo4"), T=4)
