@@ -206,12 +206,13 @@ def test_ddp_training_step_two_ranks(cuda):
 
 def test_batched_training_step_gradients(cuda):
     """The reference's training_step on a 2-graph batch (adapt_batch_training regrouping,
-    training/train.py:125-145) with all layers on the HIP training kernels vs the all-torch
-    model: a 1-step rollout, every gradient within 1e-4 (as test_msgnn_training_step_
-    gradients); a 2-step rollout (the prediction fed back), within 1e-4 in the global relative
-    L2 norm over all gradients -- per tensor, O(1e-6) per-op rounding differences grow through
-    the autoregressive step on cancellation-heavy sums such as the PReLU-slope gradients, which
-    is why the per-tensor bar is for one step (float64 yardstick)."""
+    training/train.py:125-145; 1 and 2 rollout steps, the prediction fed back) with all layers on
+    the HIP training kernels, judged against the same step of the torch path in float64: every
+    gradient tensor of ours must be within 1e-4 of it, or -- where the fp32 torch path itself
+    is not (cancellation-heavy sums such as a bias-free encoder's weight gradient on a partly
+    dry batch) -- within 3x torch fp32's own error; over 2 steps the same rule on the global
+    relative L2 norm (float64 yardstick)."""
+    import copy
     from mswegnn.batch import collate
     from mswegnn.rollout import adapt_batch_training, apply_boundary_condition, use_prediction
     ga = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=1, T=3), seed=2)
@@ -219,29 +220,47 @@ def test_batched_training_step_gradients(cuda):
     batch = collate([ga, gb]).to(cuda)
     m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
     m.train()
+    m64 = copy.deepcopy(m).double()
+    b64 = batch.clone()
+    for k in ("x", "edge_attr", "BC"):
+        setattr(b64, k, getattr(batch, k).double())
     tgt = torch.rand(batch.x.shape[0], 2, 2, device=cuda, generator=torch.Generator(cuda).manual_seed(9))
 
-    def step(engine, R):
-        m.zero_grad(set_to_none=True)
-        m.engine = engine
-        temp = adapt_batch_training(batch)
-        dyn = m.previous_t * m.NUM_WATER_VARS
+    def step(model, bt, engine, R):
+        model.zero_grad(set_to_none=True)
+        model.engine = engine
+        temp = adapt_batch_training(bt)
+        dyn = model.previous_t * model.NUM_WATER_VARS
         losses = []
         for i in range(R):
             temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, i], temp.node_BC,
                                                         type_BC=temp.type_BC)
-            preds = m(temp)
-            temp.x = use_prediction(temp.x, preds, m.previous_t)
-            losses.append(((preds - tgt[:, :, i]) ** 2).mean())
+            preds = model(temp)
+            temp.x = use_prediction(temp.x, preds, model.previous_t)
+            losses.append(((preds - tgt[:, :, i].to(preds.dtype)) ** 2).mean())
         torch.stack(losses).mean().backward()
-        return {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
-    ref, ours = step("torch", 1), step("auto", 1)
-    e = _compare(ours, ref, "batched MSGNN, 1 step")
-    ref, ours = step("torch", 2), step("auto", 2)
-    assert ours.keys() == ref.keys()
-    num = sum(((ours[k] - ref[k]).double() ** 2).sum() for k in ref).sqrt()
-    den = sum((ref[k].double() ** 2).sum() for k in ref).sqrt()
-    e2 = (num / den).item()
-    assert e2 <= TOL, e2
-    print(f"batched MSGNN training step: 1 step worst rel err {e:.2e} over {len(ref)} gradients; "
-          f"2 steps global rel {e2:.2e}")
+        return {n: p.grad.detach().double().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    def glob(a, b):
+        return (sum(((a[k] - b[k]) ** 2).sum() for k in b).sqrt() / sum((b[k] ** 2).sum() for k in b).sqrt()).item()
+    from mswegnn import autograd as ag
+    calls = ag.MLP_CALLS[0]
+    for R in (1, 2):
+        exact = step(m64, b64, "torch", R)
+        t32 = step(m, batch, "torch", R)
+        ours = step(m, batch, "auto", R)
+        assert ours.keys() == exact.keys() == t32.keys()
+        if R == 1:
+            bad = {}
+            for k in exact:
+                e_o, e_t = rel_err(ours[k], exact[k]), rel_err(t32[k], exact[k])
+                if not e_o <= max(TOL, 3 * e_t):
+                    bad[k] = (e_o, e_t)
+            assert not bad, bad
+            worst = max(rel_err(ours[k], exact[k]) for k in exact)
+        else:
+            g_o, g_t = glob(ours, exact), glob(t32, exact)
+            assert g_o <= max(TOL, 3 * g_t), (g_o, g_t)
+    assert ag.MLP_CALLS[0] > calls
+    print(f"batched MSGNN training step vs float64: 1 step worst tensor {worst:.2e}; "
+          f"2 steps global {g_o:.2e} (torch fp32 {g_t:.2e})")
