@@ -324,37 +324,57 @@ def strong_scaling_section(dist, rank, world, dev, engine, sets, T, steps, warmu
     return rec
 
 
+def child_json_record(cmd, timeout):
+    """Run a checker as a child in its own session with a time limit and return the JSON line
+    it prints (on a time-out the child AND its rank processes are killed) -- recorded, never
+    fatal, and a hang cannot stall the bench."""
+    import signal
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                             start_new_session=True)
+        try:
+            so, se = p.communicate(timeout=timeout)
+            lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+            res = json.loads(lines[-1]) if lines else {"error": "no result line", "stderr_tail": se[-800:]}
+            res["exit_code"] = p.returncode
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            res = {"error": f"timed out after {timeout} s"}
+    except Exception as e:  # noqa: BLE001
+        res = {"error": repr(e)}
+    return res
+
+
 def partitioned_rollout_check(rank, world, barrier, timeout=300, parts=2, mesh="zenodo4", steps=5):
     """Single-mesh domain decomposition over RCCL: rank 0 runs
     tools/rccl_partition_check.py (`parts` fresh processes on GPUs 0..parts-1,
     DistributedRollout with the RCCL halo exchange, gather_owned over RCCL, compared with the
-    undivided plan) as a child with a time limit -- recorded, never fatal, and a hang cannot
-    stall the bench."""
+    undivided plan) as a child (child_json_record)."""
     res = None
     if rank == 0:
-        import signal
-        import subprocess
         cmd = [sys.executable, os.path.join(ROOT, "tools", "rccl_partition_check.py"), str(parts), "--mesh", mesh,
                "--steps", str(steps), "--wait", str(max(30, timeout - 30))]
-        env = {k: v for k, v in os.environ.items()
-               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
-                            "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
-        env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
-        try:
-            # own session: on a time-out the checker AND its rank processes are killed
-            p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
-                                 start_new_session=True)
-            try:
-                so, se = p.communicate(timeout=timeout)
-                lines = [ln for ln in so.splitlines() if ln.startswith("{")]
-                res = json.loads(lines[-1]) if lines else {"error": "no result line", "stderr_tail": se[-800:]}
-                res["exit_code"] = p.returncode
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-                p.wait()
-                res = {"error": f"timed out after {timeout} s"}
-        except Exception as e:  # noqa: BLE001
-            res = {"error": repr(e)}
+        res = child_json_record(cmd, timeout)
+    barrier()
+    return res
+
+
+def ddp_training_check(rank, world, barrier, timeout=150):
+    """Training on several GPUs over RCCL: rank 0 runs tools/ddp_train_check.py
+    (DistributedDataParallel over the HIP training kernels, one GPU per rank, nccl; gradients
+    against one process's mean of the ranks' gradients) as a child (child_json_record)."""
+    res = None
+    if rank == 0:
+        W = min(world, torch.cuda.device_count())
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "ddp_train_check.py"), str(W), "--backend", "nccl",
+               "--wait", str(max(30, timeout - 30))]
+        res = child_json_record(cmd, timeout)
     barrier()
     return res
 
@@ -507,7 +527,7 @@ def main():
                            "note": "the reference loop with a no-op model (stub returning zeros): "
                                    "what the caller itself costs per step"}
 
-    strong = part_check = None
+    strong = part_check = ddp_check = None
     if world > 1:
         # the north star's strong scaling (fixed config-3 sets, rank 0 alone vs all ranks with
         # the RCCL all-gather) and the RCCL single-mesh decomposition: after the weak line's
@@ -530,6 +550,7 @@ def main():
             if not args.no_partition_large and W >= 4:
                 part_check[f"hbm1m_{W}_parts"] = partitioned_rollout_check(
                     rank, world, cpu_barrier, timeout=240, parts=W, mesh="hbm1m", steps=2)
+            ddp_check = ddp_training_check(rank, world, cpu_barrier)
 
     result = None
     if rank == 0:
@@ -722,6 +743,8 @@ def main():
         if world > 1:
             result["strong_scaling"] = strong
             result["partitioned_rollout_rccl"] = part_check
+            if ddp_check is not None:
+                result["ddp_training_rccl"] = ddp_check
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
