@@ -31,7 +31,7 @@ import torch.nn as nn
 from . import _lib as L
 from .engine import _act_code, _raw_stream
 
-__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported", "pool_apply"]
+__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported", "pool_apply", "pool_supported"]
 
 _CSR_CACHE = OrderedDict()
 _CSR_KEEP = 32
