@@ -1044,7 +1044,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // current chunk's MLP (k_edge_mlp_pipe; zenodo4_f64: 27.8 -> 27.0 us per launch,
       // +0.4 %; MSW_MLP_PIPE=0: k_edge_mlp, two waves per SIMD, one chunk each)
       const char* pp = getenv("MSW_MLP_PIPE");
-      L.eh.pipe = pp ? atoi(pp) != 0 : 1;
+      L.eh.pipe = pp ? atoi(pp) != 0 : P->NT == 4;  // F = 32 (forced split): -11 % on config 5
       L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
     }

@@ -1,0 +1,11 @@
+# round-3 session 24: where the config-5 fused edge MLP + hop spends its wave cycles (one SQ pass,
+# one GRBM pass for the effective clock), hbm1m workload
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/s24; mkdir -p $O
+export TMPDIR=/tmp
+KRE='k_edge_hop|k_hop_rows|k_encode'
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_WAVES --kernel-include-regex "$KRE" -d $PWD/$O/pmc_sq -o run --output-format csv -- python3 bench.py --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 1 --warmup 1 --T 8 > $O/pmc_sq.log 2>&1 || exit 3
+timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex "$KRE" -d $PWD/$O/pmc_grbm -o run --output-format csv -- python3 bench.py --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 1 --warmup 1 --T 8 > $O/pmc_grbm.log 2>&1 || exit 4
+python3 tools/pmc_generic.py $O/pmc_sq $O/pmc_grbm > $O/pmc_generic.txt 2>&1
+echo ok > $O/done
