@@ -31,7 +31,7 @@ import torch.nn as nn
 from torch import Tensor
 
 from models.models import BaseFloodModel, make_mlp, activation_functions
-from mswegnn.rollout import create_scale_mask
+from mswegnn.rollout import create_scale_mask, ptr_list
 from mswegnn import hooks as _hooks
 
 
@@ -391,8 +391,10 @@ class MSGNN(_EngineMixin, BaseFloodModel):
     def _torch_forward(self, graph):
         S = self.num_scales
         x = graph.x.clone()
-        ei, ep = graph.edge_index, graph.edge_ptr
-        iei, iep = graph.intra_mesh_edge_index, graph.intra_edge_ptr
+        # pointer tensors as Python ints, read once (mswegnn.rollout.ptr_list): the reference
+        # slices with their 0-d elements, one host synchronisation per slice on a GPU
+        ei, ep = graph.edge_index, ptr_list(graph.edge_ptr)
+        iei, iep = graph.intra_mesh_edge_index, ptr_list(graph.intra_edge_ptr)
         scale = self._create_scale_mask(graph)
         edge_attr = _mlp_call(self, self.edge_encoder, graph.edge_attr) if self.edge_mlp else graph.edge_attr
         nst = self.static_node_features - self.with_WL

@@ -21,6 +21,8 @@ imported at that moment, the swap happens at the first model call, so that first
 ``rollout_test`` call still steps the reference's loop (one graph-replayed ``msw_forward``
 per step); every later call is fused.
 """
+import weakref
+
 import numpy as np
 import torch
 
@@ -68,13 +70,33 @@ def use_prediction(x, pred, previous_t):
     return out
 
 
+_PTR_LISTS = {}
+
+
+def ptr_list(t):
+    """A small index tensor (node_ptr / edge_ptr / intra_edge_ptr) as Python ints, read from
+    the device once per tensor and in-place version: slicing with its 0-d elements (as the
+    reference does) synchronises the host on every slice, which on a GPU drains the queue
+    ~50 times per forward (the training step's autograd path)."""
+    if not t.is_cuda:
+        return t.tolist()
+    hit = _PTR_LISTS.get(id(t))
+    if hit is not None and hit[0]() is t and hit[1] == t._version:
+        return hit[2]
+    lst = t.tolist()
+    if len(_PTR_LISTS) > 256:
+        _PTR_LISTS.clear()
+    _PTR_LISTS[id(t)] = (weakref.ref(t), t._version, lst)
+    return lst
+
+
 def create_scale_mask(num_nodes, num_scales, node_ptr, data_type=None, device='cpu'):
     """Scale id per node from node_ptr ([S+1], or [G, S+1] for a batch)."""
     mask = torch.zeros(num_nodes, dtype=torch.int, device=device)
-    ptr = node_ptr.reshape(-1, node_ptr.shape[-1]) if node_ptr.dim() == 2 else node_ptr.reshape(1, -1)
+    rows = ptr_list(node_ptr) if node_ptr.dim() == 2 else [ptr_list(node_ptr)]
     for i in range(num_scales):
-        for j in ptr[:, i:i + 2]:
-            mask[int(j[0]):int(j[1])] = i
+        for j in rows:
+            mask[j[i]:j[i + 1]] = i
     return mask
 
 
