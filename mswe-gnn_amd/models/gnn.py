@@ -172,6 +172,14 @@ class _EngineMixin:
     # SWEGNN.train_engine) run on the HIP training kernels; 'torch': the modules themselves
     train_engine = "auto"
 
+    def __init__(self, *args, **kwargs):
+        # MSWEGNN_FUSED_ROLLOUT with training.train half-imported when models was: the callers
+        # (main.py, test_model.py) build the model after their imports, so patching here makes
+        # the first rollout_test call fused (the forward-time patch is the fallback)
+        if _hooks.PENDING:
+            _hooks.maybe_patch()
+        super().__init__(*args, **kwargs)
+
     def _engine_for(self, graph):
         """The cached plan for this graph, or None when engine='auto' and the engine does
         not implement this model / graph (the caller then takes the torch path)."""
