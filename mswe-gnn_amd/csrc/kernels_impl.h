@@ -931,6 +931,19 @@ void k_edge_hop(EdgeHopArgs a) {
       __syncthreads();
       Wm = smem;
     }
+#if defined(MSW_EH_PRIO) || defined(MSW_EH_STAGGER)
+    // A/B (build variants): break the lockstep of the SIMD's co-resident waves, which run the
+    // same gather -> MFMA chain program -- static priority for the younger half, or a delayed
+    // start of the younger half
+    if (w >= WV / 2) {
+#ifdef MSW_EH_PRIO
+      __builtin_amdgcn_s_setprio(MSW_EH_PRIO);
+#endif
+#ifdef MSW_EH_STAGGER
+      for (int i = 0; i < MSW_EH_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
+    }
+#endif
     for (; tile < a.ntiles; tile += stride) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       EdgeHopRows<NT> q;
