@@ -156,6 +156,29 @@ struct Epilogue {
 
 // Fused: edge MLP (s_ij for every edge, stored for the later hops) + hop 1
 // (+ epilogue when the layer has K = 1; intra-scale unpooling is such a layer).
+// Children of one coarse row (32 B, one 16-B + one 8-B load): the first kPoolInline
+// internal fine rows, the count, and where the full list starts in PoolArgs::child.
+constexpr int kPoolInline = 4;
+struct alignas(16) PoolRec {
+  int c[kPoolInline];
+  int cnt, off, pad[2];
+};
+
+// Pooling fused into the coarse scale's first edge-MLP + hop launch (k_edge_coop, POOL):
+// per tile-padded edge slot of the coarse scale, the children of the slot's source (edge
+// lane) and of the lane's destination (node lane), as PoolRec (absent: cnt 0, children =
+// a safe fine row).  The launch forms the mean of the children and the projection of the
+// processor (U, V, O) itself instead of reading them from a pooling launch's output.
+struct alignas(16) PoolSlot {
+  PoolRec src, dst;
+};
+struct PoolFuse {
+  const PoolSlot* slots;           // [ntiles][16], null = not fused
+  const int* child;                // internal fine rows, reference order (PoolArgs::child)
+  const float* in;                 // x_down (fine rows)
+  NpDesc np;                       // projection of the processor (outputs not stored)
+};
+
 struct EdgeHopArgs {
   Common c;
   WReg reg;                        // [MLP | epilogue operands | filter W_1]
@@ -191,6 +214,7 @@ struct EdgeHopArgs {
   int* step_inc;                   // rollout mode, first edge-MLP launch of a step:
                                    // &RolloutIO::step, advanced once (workgroup 0, lane 0)
   const EdgeChunk* chunks; int nchunks;  // k_edge_mlp: dense 16-edge chunks [nchunks][16]
+  PoolFuse pool;                   // mean pooling + projection fused in (k_edge_coop only)
 };
 
 // Hops 2..K over the same edge tiles as the fused first hop.
@@ -266,13 +290,6 @@ struct HopMArgs {
 };
 
 // Mean pooling into the coarse rows + projection of the next processor.
-// Children of one coarse row (32 B, one 16-B + one 8-B load): the first kPoolInline
-// internal fine rows, the count, and where the full list starts in PoolArgs::child.
-constexpr int kPoolInline = 4;
-struct alignas(16) PoolRec {
-  int c[kPoolInline];
-  int cnt, off, pad[2];
-};
 
 struct PoolArgs {
   Common c;

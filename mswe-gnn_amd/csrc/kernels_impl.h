@@ -1210,7 +1210,127 @@ __device__ __forceinline__ void np_project_coop(const f32x4 (&xs)[NT], const f32
   }
 }
 
-template <int NT, int ACT, int LST, int P>
+// ---- pooling fused into the coarse scale's first edge-MLP + hop (EdgeHopArgs::pool)
+// The tile's two ranks split the pooling: rank 0 forms the SOURCE side of its edge lanes
+// (mean of the source's children, U and O = out_0 of the source), rank 1 the DESTINATION side
+// of its node lanes (V and O of the destination) -- each loads only its side's children.
+template <int NT>
+struct PoolIn {
+  f32x4 c[kPoolInline][NT];  // children rows of this rank's node (absent ones: a real row)
+  f32x4 xs[NT];              // x_s of that node
+  int cnt, off;              // child count, offset into PoolFuse::child
+};
+// edge_hop_gather with U / V / out rows replaced by the pooling inputs (issued before the
+// weight staging, like every tile load); rank r: 0 = source side, 1 = destination side
+template <int NT, int LST>
+__device__ __forceinline__ void edge_pool_load(EdgeHopRows<NT>& r, PoolIn<NT>& pi, const EdgeHopArgs& a, int tile,
+                                               int j, int g, int rank) {
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  const LaneRec rec = load_rec(a.recs, tile, j);
+  const int4* sp = reinterpret_cast<const int4*>(a.pool.slots + (size_t)tile * kRowsPerWave + j) + (rank ? 2 : 0);
+  const int4 r0 = sp[0], r1 = sp[1];
+  r.L = lanes_of(rec, tile, j, a.n0);
+  const Lanes& L = r.L;
+  const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  const float* Pb = a.Pe ? a.Pe + L.p * hs : z;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) r.Ps[t] = ld4((t < a.h1t ? Pb : z) + 16 * t + 4 * g);
+  const int ci[kPoolInline] = {r0.x, r0.y, r0.z, r0.w};
+#pragma unroll
+  for (int k = 0; k < kPoolInline; ++k) load_row<NT>(pi.c[k], a.pool.in + (size_t)ci[k] * F, g);
+  pi.cnt = r1.x; pi.off = r1.y;
+  load_row<NT>(pi.xs, a.xs + (rank ? L.n : L.sr) * F, g);
+  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
+  if (LST && a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
+}
+// mean of the children (k_pool / k_pool_edge: summed from zero in reference order, divided
+// by max(count, 1)) -- the same operations, so the same bits
+template <int NT>
+__device__ __forceinline__ void pool_mean(f32x4 (&m)[NT], const PoolIn<NT>& pi, const EdgeHopArgs& a, int g) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) m[t] = zero4();
+#pragma unroll
+  for (int k = 0; k < kPoolInline; ++k)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 s2 = m[t] + pi.c[k][t];
+      m[t] = k < pi.cnt ? s2 : m[t];
+    }
+  for (int k = kPoolInline; k < pi.cnt; ++k) {
+    f32x4 y[NT];
+    load_row<NT>(y, a.pool.in + (size_t)a.pool.child[pi.off + k] * F, g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) m[t] = m[t] + y[t];
+  }
+  const float fc = (float)(pi.cnt > 0 ? pi.cnt : 1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) m[t] = m[t] / fc;
+}
+// np_project's proj calls on the pooled row: h = U (rank 0) or V (rank 1) of [x_s; x], o = O x
+// (out_0; x itself without a filter matrix)
+template <int NT, int H1T>
+__device__ __forceinline__ void pool_project_t(f32x4 (&h)[2 * NT], f32x4 (&o)[NT], const f32x4 (&xp)[NT],
+                                               const f32x4 (&xs)[NT], const NpDesc& d, const float* W, int lane,
+                                               int rank) {
+  constexpr int T2 = 2 * NT;
+  f32x4 in[T2], acc[H1T];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    in[t] = xs[t];
+    in[NT + t] = xp[t];
+  }
+  proj<T2, H1T>(in, acc, W + (rank ? d.a_v : d.a_u), lane);
+#pragma unroll
+  for (int t = 0; t < T2; ++t) h[t] = t < H1T ? acc[t < H1T ? t : 0] : zero4();
+  if (d.a_o >= 0) {
+    proj<NT, NT>(xp, o, W + d.a_o, lane);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) o[t] = xp[t];
+  }
+}
+// rank 0 -> (q.Us, q.os) of its edge lanes, rank 1 -> (q.Vn, q.inn) of its node lanes; then
+// rank 0 publishes U | O rows in pb, rank 1 V | O rows in both ranks' slabs (XS-strided,
+// edge_hop_core's node-row layout); after the barrier each rank reads the other side back.
+template <int NT, int XS>
+__device__ __forceinline__ void edge_pool_project(EdgeHopRows<NT>& q, const PoolIn<NT>& pi, const EdgeHopArgs& a,
+                                                  const float* W, int lane, int g, int j, int rank, float* pb,
+                                                  float* slab0, float* slab1) {
+  constexpr int T2 = 2 * NT;
+  f32x4 xp[NT], h[T2], o[NT];
+  pool_mean<NT>(xp, pi, a, g);
+  if (a.pool.np.h1t == T2)
+    pool_project_t<NT, T2>(h, o, xp, pi.xs, a.pool.np, W, lane, rank);
+  else
+    pool_project_t<NT, NT>(h, o, xp, pi.xs, a.pool.np, W, lane, rank);
+  if (rank == 0) {
+    store_row<T2>(pb + j * XS, h, T2, g);
+    store_row<NT>(pb + j * XS + 16 * T2, o, NT, g);
+  } else {
+    store_row<T2>(slab0 + j * XS, h, T2, g);
+    store_row<NT>(slab0 + j * XS + 16 * T2, o, NT, g);
+    store_row<T2>(slab1 + j * XS, h, T2, g);
+    store_row<NT>(slab1 + j * XS + 16 * T2, o, NT, g);
+  }
+  __syncthreads();
+  if (rank == 0) {
+#pragma unroll
+    for (int t = 0; t < T2; ++t) q.Us[t] = h[t];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) q.os[t] = o[t];
+    load_row<NT>(q.inn, slab0 + j * XS + 16 * T2, g);
+  } else {
+    load_row<T2>(q.Us, pb + j * XS, g);
+    load_row<NT>(q.os, pb + j * XS + 16 * T2, g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) q.inn[t] = o[t];
+  }
+}
+
+template <int NT, int ACT, int LST, int P, bool POOL = false>
 __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT, T2 = 2 * NT;
@@ -1231,21 +1351,33 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
   EdgeHopRows<NT> q;
-  edge_hop_load<NT, LST>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
+  [[maybe_unused]] PoolIn<NT> pin;
+  if constexpr (POOL)
+    edge_pool_load<NT, LST>(q, pin, a, live ? tile : 0, j, g, r);
+  else
+    edge_hop_load<NT, LST>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
   const bool split = a.reg.split < a.reg_nf;
   stage_glds<kWaves>(smem, a.c.W, a.reg, 0, a.reg.split);
   __syncthreads();
   c.W = smem;
   if (split) stage_glds<kWaves>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
+  if constexpr (POOL) {
+    static_assert(P == 2, "fused pooling: a source rank and a destination rank");
+    __shared__ __attribute__((aligned(16))) float pbuf[G][kRowsPerWave][XS];
+    edge_pool_project<NT, XS>(q, pin, a, c.W, lane, g, j, r, &pbuf[grp][0][0], &slab_all[grp * P][0][0],
+                              &slab_all[grp * P + 1][0][0]);
+  }
   float* slab = &slab_all[w][0][0];
   float* b0 = &xbuf[grp][0][0][0];
   float* b1p = &xbuf[grp][1][0][0];
   const Lanes& L = q.L;
   // ---- as edge_hop_core up to the MLP (every rank)
   float* my = slab + j * XS;
-  store_row<T2>(my, q.Vn, T2, g);
-  store_row<NT>(my + 16 * T2, q.inn, NT, g);
-  wave_lds_sync();
+  if constexpr (!POOL) {  // fused pooling: the destination rank stored them (barrier above)
+    store_row<T2>(my, q.Vn, T2, g);
+    store_row<NT>(my + 16 * T2, q.inn, NT, g);
+    wave_lds_sync();
+  }
   const float* dr = slab + L.dl * XS;
   f32x4 H[T2], od[NT];
   const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
@@ -1480,8 +1612,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 }
 
 template <int NT>
-static const void* edge_coop_kernel(int prelu, int last, int pw = 0) {
+static const void* edge_coop_kernel(int prelu, int last, int pw = 0, int pool = 0) {
   if constexpr (NT == 2) {  // F = 32: each MLP layer's output tiles halve (F = 16 has one)
+    if (pool) {  // pooling fused in (EdgeHopArgs::pool)
+      if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2, true> : (const void*)k_edge_coop<NT, -1, 1, 2, true>;
+      return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2, true> : (const void*)k_edge_coop<NT, -1, 0, 2, true>;
+    }
     if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
     return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
   } else if constexpr (NT == 4) {  // F = 64: four waves per tile (pw = 2: two)
@@ -2675,11 +2811,14 @@ hipError_t prepare_kernels() {
   if constexpr (NT == 2) {  // cooperative edge hops: 160 KB minus slabs and exchange buffers
     const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
     for (int prelu = 0; prelu < 2; ++prelu)
-      for (int last = 0; last < 2; ++last) {
-        hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024 - st);
-        if (e != hipSuccess) return e;
-      }
+      for (int last = 0; last < 2; ++last)
+        for (int pool = 0; pool < 2; ++pool) {
+          // fused pooling: + the source rank's U | O exchange rows (one slab per tile)
+          const int ps = pool ? (kWaves / 2) * kRowsPerWave * (48 * NT + 4) * 4 : 0;
+          hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, 0, pool),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st - ps);
+          if (e != hipSuccess) return e;
+        }
   }
   // hop chains: 160 KB minus their own (narrower) static slabs
   constexpr int WC = chain_waves<NT>();
@@ -2804,13 +2943,14 @@ template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
-    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop);
-    if (!f) return hipErrorInvalidValue;
+    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop, a.pool.slots != nullptr);
+    if (!f || (a.pool.slots && a.coop != 2)) return hipErrorInvalidValue;
     EdgeHopArgs b = a;
     const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
     void* args[] = {&b};
     return hipLaunchKernel(f, grid, dim3(kBlock), args, a.wdirect ? 0 : eh_lds_bytes(a.reg_nf), st);
   }
+  if (a.pool.slots) return hipErrorInvalidValue;  // pooling is fused into k_edge_coop only
   const bool loop = tile_loop(a);
   EdgeHopArgs b = a;
   const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
@@ -2955,6 +3095,7 @@ static const void* kernel_of(int kind, int prelu, int last) {
       return nullptr;
     case 6: return prelu ? (const void*)k_epi<NT, 1, LOOP> : (const void*)k_epi<NT, -1, LOOP>;
     case 7: return edge_coop_kernel<NT>(prelu, last);
+    case 16: return edge_coop_kernel<NT>(prelu, last, 0, 1);
     case 12: return edge_coop_kernel<NT>(prelu, last, 2);
     case 9: return hop_coop_kernel<NT>(prelu);
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;

@@ -198,6 +198,7 @@ struct ScaleCSR {
   int2* redge = nullptr;        // destination, {source row, s slot} per edge
 
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
+  std::vector<LaneRec> hrecs;   // host copy of recs (fused pooling slots, PoolSlot)
   // hop chains of m = 2, 3 hops (engine.h HopMArgs), indexed by m; ok = false -> not built
   struct Chain {
     bool ok = false;
@@ -215,6 +216,8 @@ struct LevelMaps {              // level l: coarse scale l+1, fine scale l
   LaneRec* pool_erecs = nullptr; // edge tiles of coarse nodes and their children (<= 16 per tile)
   int pool_etiles = 0;
   int* pool_child = nullptr;    // internal fine rows, reference order
+  PoolSlot* pool_slots = nullptr; // per edge slot of the coarse scale: children of its source /
+                                  // destination (pooling fused into the coarse edge hop)
   LaneRec* un_recs = nullptr;   // fine nodes (scale l) and their coarse parents
   int un_ntiles = 0;
 };
@@ -591,7 +594,14 @@ bool chain_fits(const msw_plan* P, const ScaleCSR& g, int m, bool last, const Ep
 }
 
 constexpr int kSplitMlpTiles = 1024;  // F = 64: split edge MLP from this many edge tiles up
-void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi) {
+// the layer's edge MLP runs alone (k_edge_mlp) and hop 1 as a k_hop launch
+bool edge_mlp_split(const msw_plan* P, const Proc& pr) {
+  bool split = P->NT == 4 && pr.K > 1 && P->part_rank < 0 && P->sc[pr.scale].ntiles >= kSplitMlpTiles;
+  if (const char* sv = getenv("MSW_SPLIT_EDGE_MLP")) split = pr.K > 1 && P->part_rank < 0 && atoi(sv) != 0;
+  return split;
+}
+void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi,
+                const PoolFuse* pool = nullptr) {
   const ScaleCSR& g = P->sc[pr.scale];
   const Common c = common_of(P);
   sched_exchange(P, q, pr.scale, {{pr.par ? B_U1 : B_U0, 16 * pr.h1t}, {pr.par ? B_O1 : B_O0, P->F}});
@@ -610,11 +620,11 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   eh.last = pr.K == 1;
   eh.out = pr.K == 1 ? out : P->T[0];
   eh.epi = epi;
+  if (pool) eh.pool = *pool;  // U / V / O of this layer formed in the launch (no pooling launch)
   // F = 64 scales beyond one round of the fused kernel (one wave per SIMD): the edge MLP
   // alone over dense edge chunks (k_edge_mlp, two waves per SIMD) + hop 1 as a k_hop launch
   // (MSW_SPLIT_EDGE_MLP=0/1 overrides the size rule)
-  bool split = P->NT == 4 && pr.K > 1 && P->part_rank < 0 && g.ntiles >= kSplitMlpTiles;
-  if (const char* sv = getenv("MSW_SPLIT_EDGE_MLP")) split = pr.K > 1 && P->part_rank < 0 && atoi(sv) != 0;
+  const bool split = edge_mlp_split(P, pr);
   if (split) {
     L1.kind = L_EDGE_MLP;
     eh.chunks = g.chunks; eh.nchunks = g.nchunks;
@@ -702,6 +712,21 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   }
 }
 
+constexpr int kMaxFusedPoolBlocks = 256;  // one 4-wave workgroup (two tiles) per CU, one round
+// Mean pooling into coarse scale s fused into the first launch of the processor on s
+// (k_edge_coop with EdgeHopArgs::pool): F = 32, the scale small enough for the two-wave
+// cooperative edge hop in one round (set_grid_cap's k_edge_coop rule), not on parts (their
+// halo exchange sits between the two launches).  MSW_POOL_FUSE=0 keeps the pooling launch.
+bool pool_fusable(const msw_plan* P, int s, const Proc& pr) {
+  const int on = getenv("MSW_POOL_FUSE") ? atoi(getenv("MSW_POOL_FUSE")) : 1;
+  if (!on || P->NT != 2 || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
+  const ScaleCSR& g = P->sc[s];
+  // K > 1: the launch is not the layer's last hop (k_edge_coop runs no unpool / decoder epilogue)
+  if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s - 1].pool_slots || g.ntiles <= 0)
+    return false;
+  return P->coop_w[0] > 0 && 2L * g.ntiles <= std::min(P->coop_w[0], kWaves * kMaxFusedPoolBlocks);
+}
+
 // One forward.  Forward mode: the encoder reads graph rows of x (via perm) and the decoder
 // writes y (both patched per call); rollout mode: the internal state X is updated in place
 // by the decoder epilogue.
@@ -750,9 +775,16 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
   if (P->model_type == 0) {
     Epilogue none{};
     none.np = np_none(); none.uu_a = -1; none.dec.on = 0;
+    PoolFuse fuse{};
     for (int i = 0; i < S - 1; ++i) {  // fine -> coarse
-      sched_proc(P, q, P->procs[i], P->xdown, none);
+      sched_proc(P, q, P->procs[i], P->xdown, none, fuse.slots ? &fuse : nullptr);
       const LevelMaps& m = P->lv[i];
+      fuse = PoolFuse{};
+      if (pool_fusable(P, i + 1, P->procs[i + 1])) {  // the next processor's first launch pools
+        fuse.slots = m.pool_slots; fuse.child = m.pool_child; fuse.in = P->xdown;
+        fuse.np = np_of(P, P->procs[i + 1]);
+        continue;
+      }
       Launch L;
       L.kind = L_POOL;
       L.scale = i + 1;
@@ -775,7 +807,7 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
         e.uu_a = up.a_u; e.uu_h1t = up.h1t; e.Uu = P->Uu;
       }
       e.dec = dl;  // every scale's rows are decoded once final (gnn.py:335-348)
-      sched_proc(P, q, P->procs[j], P->xup, e);
+      sched_proc(P, q, P->procs[j], P->xup, e, i == 0 && fuse.slots ? &fuse : nullptr);
       if (s > 0) {                      // intra_scale_gnn[i] on level s-1 (+ skip) + projection
         const Proc& up = P->unpools[i];
         const ScaleCSR& fs = P->sc[s - 1];
@@ -936,6 +968,7 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       RegionBuilder R(P->blob, 0);
       a.b1_off = R.put(a.b1_off, 16 * a.h1t);
       rl.mlp(R, a.rest);
+      if (a.pool.slots) rl.np(R, a.pool.np);  // fused pooling: projected before the MLP
       const int split = R.pos();  // operands after this one stream in behind the MLP
       if (a.last) rl.epi(R, a.epi);
       // filt_a stays a blob offset (the one-tile-per-wave variant loads it into registers and
@@ -1070,6 +1103,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // F = 64 where four waves per tile do not fit one round: two, two tiles per workgroup
       // (zenodo4_f64 scale 1: 508 tiles in one round, +2.0 %; MSW_COOP2_F64=0 off, =2 also in
       // place of four, for tests)
+      if (a.pool.slots) a.coop = 2;  // fused pooling exists as k_edge_coop only (pool_fusable)
       const int c2 = getenv("MSW_COOP2_F64") ? atoi(getenv("MSW_COOP2_F64")) : 1;
       if (c2 == 2 && a.coop == 4) a.coop = 0;
       a.wdirect = 0;
@@ -1453,6 +1487,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
     for (size_t q = 0; q < pcsr.size(); ++q)
       if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
     if ((rc = pupload(P, &c.recs, recs))) return rc;
+    c.hrecs = recs;
     {
       std::vector<EdgeChunk> ck;
       for (size_t q = 0; q < recs.size(); ++q)
@@ -1515,6 +1550,22 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       if ((rc = pupload(P, &m.pool_erecs, make_recs(rp, child, cs.n0, pt, nullptr)))) return rc;
       if (child.empty()) child.push_back(0);
       if ((rc = pupload(P, &m.pool_recs, pr)) || (rc = pupload(P, &m.pool_child, child))) return rc;
+      if (!cs.hrecs.empty()) {  // fused pooling: the records of each slot's two coarse nodes
+        auto rec_of = [&](int row) {
+          PoolRec r{};
+          r.cnt = 0; r.off = 0;
+          if (row >= cs.n0 && row < cs.n0 + cs.ns) r = pr[row - cs.n0];
+          const int safe = r.cnt > 0 ? r.c[0] : fs.n0;  // absent children re-read a real row
+          for (int k = 0; k < kPoolInline; ++k) if (k >= r.cnt) r.c[k] = safe;
+          return r;
+        };
+        std::vector<PoolSlot> ps(cs.hrecs.size());
+        for (size_t q = 0; q < ps.size(); ++q) {
+          ps[q].src = rec_of(cs.hrecs[q].src);
+          ps[q].dst = rec_of(cs.hrecs[q].n);
+        }
+        if ((rc = pupload(P, &m.pool_slots, ps))) return rc;
+      }
       csr_build(fs.ns, fk, rp, order);
       std::vector<int> us(m.I);
       for (int i = 0; i < m.I; ++i) us[i] = cv[order[i]];

@@ -767,3 +767,50 @@ def test_ingested_dataset_vs_reference(cuda, mode):
     r = run(b.to(cuda)).cpu()
     for p, q in zip(split_rollout(r, b), split_rollout(rb, b)):
         assert per_step_rel(p, q) <= REL_TOL
+
+
+def _reparent(g, level=0, moves=2):
+    """A coarse node of `level` with more than kPoolInline (4) children: `moves` children of
+    the second coarse node are re-assigned to the first (intra edges stay coarse-major), so
+    the pooling's overflow path (children beyond the inline record) runs."""
+    ie = g.intra_mesh_edge_index.clone()
+    a, b = int(g.intra_edge_ptr[level]), int(g.intra_edge_ptr[level + 1])
+    co = ie[0, a:b]
+    first = int(co[0])
+    second = int(co[co != first][0])
+    idx = (co == second).nonzero().flatten()[:moves] + a
+    ie[0, idx] = first
+    seg = ie[:, a:b]
+    order = torch.argsort(seg[0] * (int(seg[1].max()) + 1) + seg[1])
+    ie[:, a:b] = seg[:, order]
+    g.intra_mesh_edge_index = ie
+    return g
+
+
+@pytest.mark.parametrize("act", ["prelu", "relu"])
+def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, act):
+    """Mean pooling + projection fused into the coarse scale's first edge-MLP + hop launch
+    (k_edge_coop<.., POOL>, MSW_POOL_FUSE=1, the default on small coarse scales) == the
+    separate pooling launch (MSW_POOL_FUSE=0), bit for bit: forward, rollout, a batch of two
+    meshes, on a mesh with a 6-child coarse node (the overflow path); 3 fewer launches per
+    step on 4 scales; and the oracle on that mesh."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import rollout_test
+    ga = _reparent(wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=21))
+    gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=22, T=6), seed=22)
+    outs, kps = {}, {}
+    for sv in ("0", "1"):
+        monkeypatch.setenv("MSW_POOL_FUSE", sv)
+        m = _hip(build_msgnn(4, 32, 4, mlp_activation=act), cuda)
+        gd = ga.to(cuda)
+        with torch.no_grad():
+            y = m(gd).cpu()
+        kps[sv] = _stats(m, gd)["kernels_per_step"]
+        outs[sv] = (y, m.rollout(gd).cpu(), rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
+    assert kps["1"] == kps["0"] - 3, kps
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b)
+    m = build_msgnn(4, 32, 4, mlp_activation=act)
+    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=32, K=4,
+                                                         mlp_activation=act), ga)
+    assert per_step_rel(outs["1"][1], ref) <= REL_TOL
