@@ -1474,12 +1474,44 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   }
 }
 
+// Fused pooling on k_edge_coop4 (F = 64): ranks [0, P/2) form the source side, [P/2, P) the
+// destination side; the P/2 ranks of a side split its U (V) and O output tiles.  dst_row: the
+// lane's row [h (16 T2) | o (16 NT)] -- the exchange rows (source) or the node slab (destination).
+template <int NT, int P, int H1T>
+__device__ __forceinline__ void pool_project_part(float* dst_row, const f32x4 (&xp)[NT], const f32x4 (&xs)[NT],
+                                                  const NpDesc& d, const float* W, int lane, int g, int side,
+                                                  int part) {
+  constexpr int NPART = P / 2, T2 = 2 * NT, TU = H1T / NPART, TO = NT / NPART;
+  static_assert(H1T % NPART == 0 && NT % NPART == 0, "whole output tiles per rank");
+  f32x4 in[T2], acc[TU];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    in[t] = xs[t];
+    in[NT + t] = xp[t];
+  }
+  proj<T2, TU>(in, acc, W + (side ? d.a_v : d.a_u) + (size_t)part * TU * T2 * 256, lane);
+#pragma unroll
+  for (int t = 0; t < TU; ++t) st4(dst_row + 16 * (part * TU + t) + 4 * g, acc[t]);
+  if (part == 0)
+#pragma unroll
+    for (int t = H1T; t < T2; ++t) st4(dst_row + 16 * t + 4 * g, zero4());  // U / V tiles past h1t
+  f32x4 o[TO];
+  if (d.a_o >= 0) {
+    proj<NT, TO>(xp, o, W + d.a_o + (size_t)part * TO * NT * 256, lane);
+  } else {
+#pragma unroll
+    for (int t = 0; t < TO; ++t) o[t] = pick<NT, TO>(xp, part, t);
+  }
+#pragma unroll
+  for (int t = 0; t < TO; ++t) st4(dst_row + 16 * T2 + 16 * (part * TO + t) + 4 * g, o[t]);
+}
+
 // F = 64 (NT = 4): the whole workgroup (4 waves) on one tile, one slab shared by the four
 // ranks (rank 0 writes the node rows and the messages) so that the 96 KB edge-MLP region
 // still fits beside it; the epilogue's operands stay in the blob (F = 64 relocation).
 // P = 2: two tiles per workgroup, two waves each (a slab and exchange buffers per tile);
 // P = 4: the whole workgroup on one tile.
-template <int ACT, int LST, int P = 4>
+template <int ACT, int LST, int P = 4, bool POOL = false>
 __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma clang fp contract(off)
   constexpr int NT = 4, F = 16 * NT, T2 = 2 * NT, G = kWaves / P, TS = NT / P;
@@ -1509,17 +1541,38 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
       for (int ti = 0; ti < NT; ++ti) wr[t][ti] = ld4(c.W + fa + ((size_t)((r * TS + t) * NT + ti) * 64 + lane) * 4);
   }
   EdgeHopRows<NT> q;
-  edge_hop_load<NT, LST>(q, a, tile, j, g);
+  [[maybe_unused]] PoolIn<NT> pin;
+  [[maybe_unused]] const int side = r >= P / 2;  // fused pooling: 0 source side, 1 destination side
+  if constexpr (POOL)
+    edge_pool_load<NT, LST>(q, pin, a, tile, j, g, side);
+  else
+    edge_hop_load<NT, LST>(q, a, tile, j, g);
   const Lanes& L = q.L;
   // the MLP region: staged in LDS, or (wdirect: two workgroups per CU) read from its blob copy
   if (a.reg.len > 0 && !a.wdirect) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
   const float* Wm = a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W;
   float* my = &slab[j][0];
-  if (r == 0) {
+  if constexpr (POOL) {
+    // source side -> exchange rows (in xbuf, free until the MLP), destination side -> the
+    // node slab; projection operands from the blob (c.W)
+    constexpr int XPB = 16 * T2 + 16 * NT + 4;
+    static_assert(kRowsPerWave * XPB <= 2 * kRowsPerWave * XW, "exchange rows fit the xbuf pair");
+    float* pb = &xbuf[0][0][0] + j * XPB;
+    f32x4 xp[NT];
+    pool_mean<NT>(xp, pin, a, g);
+    if (a.pool.np.h1t == T2)
+      pool_project_part<NT, P, T2>(side ? my : pb, xp, pin.xs, a.pool.np, c.W, lane, g, side, r % (P / 2));
+    else
+      pool_project_part<NT, P, NT>(side ? my : pb, xp, pin.xs, a.pool.np, c.W, lane, g, side, r % (P / 2));
+    __syncthreads();
+    load_row<T2>(q.Us, pb, g);
+    load_row<NT>(q.os, pb + 16 * T2, g);
+  } else if (r == 0) {
     store_row<T2>(my, q.Vn, T2, g);
     store_row<NT>(my + 16 * T2, q.inn, NT, g);
   }
-  __syncthreads();  // node rows and the MLP region have landed
+  __syncthreads();  // node rows and the MLP region have landed (fused pooling: and every rank
+                    // has read its exchange rows before the MLP's exchanges reuse xbuf)
   const float* dr = &slab[L.dl][0];
   f32x4 H[T2], od[NT];
   const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
@@ -1621,6 +1674,14 @@ static const void* edge_coop_kernel(int prelu, int last, int pw = 0, int pool = 
     if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
     return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
   } else if constexpr (NT == 4) {  // F = 64: four waves per tile (pw = 2: two)
+    if (pool) {  // pooling fused in (EdgeHopArgs::pool)
+      if (pw == 2) {
+        if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2, true> : (const void*)k_edge_coop4<-1, 1, 2, true>;
+        return prelu ? (const void*)k_edge_coop4<1, 0, 2, true> : (const void*)k_edge_coop4<-1, 0, 2, true>;
+      }
+      if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 4, true> : (const void*)k_edge_coop4<-1, 1, 4, true>;
+      return prelu ? (const void*)k_edge_coop4<1, 0, 4, true> : (const void*)k_edge_coop4<-1, 0, 4, true>;
+    }
     if (pw == 2) {
       if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2> : (const void*)k_edge_coop4<-1, 1, 2>;
       return prelu ? (const void*)k_edge_coop4<1, 0, 2> : (const void*)k_edge_coop4<-1, 0, 2>;
@@ -2801,11 +2862,12 @@ hipError_t prepare_kernels() {
     for (int pw = 2; pw <= 4; pw += 2) {
       const int st = (kWaves / pw) * (kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4);
       for (int prelu = 0; prelu < 2; ++prelu)
-        for (int last = 0; last < 2; ++last) {
-          hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, pw),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st);
-          if (e != hipSuccess) return e;
-        }
+        for (int last = 0; last < 2; ++last)
+          for (int pool = 0; pool < 2; ++pool) {
+            hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, pw, pool),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st);
+            if (e != hipSuccess) return e;
+          }
     }
   }
   if constexpr (NT == 2) {  // cooperative edge hops: 160 KB minus slabs and exchange buffers
@@ -2944,7 +3006,7 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
     const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop, a.pool.slots != nullptr);
-    if (!f || (a.pool.slots && a.coop != 2)) return hipErrorInvalidValue;
+    if (!f || (a.pool.slots && NT == 2 && a.coop != 2)) return hipErrorInvalidValue;
     EdgeHopArgs b = a;
     const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
     void* args[] = {&b};

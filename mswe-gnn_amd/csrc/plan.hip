@@ -719,11 +719,13 @@ constexpr int kMaxFusedPoolBlocks = 256;  // one 4-wave workgroup (two tiles) pe
 // halo exchange sits between the two launches).  MSW_POOL_FUSE=0 keeps the pooling launch.
 bool pool_fusable(const msw_plan* P, int s, const Proc& pr) {
   const int on = getenv("MSW_POOL_FUSE") ? atoi(getenv("MSW_POOL_FUSE")) : 1;
-  if (!on || P->NT != 2 || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
+  if (!on || (P->NT != 2 && P->NT != 4) || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
   const ScaleCSR& g = P->sc[s];
   // K > 1: the launch is not the layer's last hop (k_edge_coop runs no unpool / decoder epilogue)
   if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s - 1].pool_slots || g.ntiles <= 0)
     return false;
+  // the scales the cooperative kernels take in one round (F = 32: two waves per tile; F = 64:
+  // four, or two with two tiles per workgroup)
   return P->coop_w[0] > 0 && 2L * g.ntiles <= std::min(P->coop_w[0], kWaves * kMaxFusedPoolBlocks);
 }
 
@@ -1103,7 +1105,9 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // F = 64 where four waves per tile do not fit one round: two, two tiles per workgroup
       // (zenodo4_f64 scale 1: 508 tiles in one round, +2.0 %; MSW_COOP2_F64=0 off, =2 also in
       // place of four, for tests)
-      if (a.pool.slots) a.coop = 2;  // fused pooling exists as k_edge_coop only (pool_fusable)
+      // fused pooling exists in the cooperative kernels only (pool_fusable): F = 32 two waves
+      // per tile; F = 64 four, or two where four do not fit one round (below)
+      if (a.pool.slots && P->NT == 2) a.coop = 2;
       const int c2 = getenv("MSW_COOP2_F64") ? atoi(getenv("MSW_COOP2_F64")) : 1;
       if (c2 == 2 && a.coop == 4) a.coop = 0;
       a.wdirect = 0;
@@ -1121,6 +1125,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
           a.wdirect = 1;
         }
       }
+      if (a.pool.slots && !a.coop) a.coop = 2;  // F = 64 fused pooling: two waves per tile, any grid
       break;
     }
     case L_HOP:

@@ -787,13 +787,17 @@ def _reparent(g, level=0, moves=2):
     return g
 
 
-@pytest.mark.parametrize("act", ["prelu", "relu"])
-def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, act):
+@pytest.mark.parametrize("F,act,coop2", [(32, "prelu", None), (32, "relu", None), (64, "prelu", None),
+                                         (64, "relu", "2")])
+def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, F, act, coop2):
     """Mean pooling + projection fused into the coarse scale's first edge-MLP + hop launch
-    (k_edge_coop<.., POOL>, MSW_POOL_FUSE=1, the default on small coarse scales) == the
-    separate pooling launch (MSW_POOL_FUSE=0), bit for bit: forward, rollout, a batch of two
-    meshes, on a mesh with a 6-child coarse node (the overflow path); 3 fewer launches per
-    step on 4 scales; and the oracle on that mesh."""
+    (k_edge_coop<.., POOL> at F = 32, k_edge_coop4<.., POOL> at F = 64 -- four waves per
+    tile, or two with MSW_COOP2_F64=2; MSW_POOL_FUSE=1, the default on small coarse scales)
+    == the separate pooling launch (MSW_POOL_FUSE=0), bit for bit: forward, rollout, a batch
+    of two meshes, on a mesh with a 6-child coarse node (the overflow path); 3 fewer launches
+    per step on 4 scales; and the oracle on that mesh."""
+    if coop2:
+        monkeypatch.setenv("MSW_COOP2_F64", coop2)
     from mswegnn.batch import collate
     from mswegnn.rollout import rollout_test
     ga = _reparent(wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=21))
@@ -801,7 +805,7 @@ def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, act):
     outs, kps = {}, {}
     for sv in ("0", "1"):
         monkeypatch.setenv("MSW_POOL_FUSE", sv)
-        m = _hip(build_msgnn(4, 32, 4, mlp_activation=act), cuda)
+        m = _hip(build_msgnn(4, F, 4, mlp_activation=act), cuda)
         gd = ga.to(cuda)
         with torch.no_grad():
             y = m(gd).cpu()
@@ -810,7 +814,7 @@ def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, act):
     assert kps["1"] == kps["0"] - 3, kps
     for a, b in zip(outs["0"], outs["1"]):
         assert torch.equal(a, b)
-    m = build_msgnn(4, 32, 4, mlp_activation=act)
-    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=32, K=4,
+    m = build_msgnn(4, F, 4, mlp_activation=act)
+    ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4,
                                                          mlp_activation=act), ga)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
