@@ -177,6 +177,19 @@ struct PoolFuse {
   const int* child;                // internal fine rows, reference order (PoolArgs::child)
   const float* in;                 // x_down (fine rows)
   NpDesc np;                       // projection of the processor (outputs not stored)
+  // ... or the unpooling layer into this scale fused instead (slots null, parent set): the
+  // intra-scale SWEGNN of each slot's two nodes (one in-edge from the coarse parent, own rows
+  // zero, + skip), then the projection np -- the unpooling launch's work, in this launch
+  const int2* parent;              // [ntiles][16] {parent of the slot's source, of the lane's
+                                   // destination}: coarse internal rows, -1 = none
+  int cpad;                        // a real coarse row (absent parents load it)
+  const float* Uu; const float* Vu;  // unpool U (coarse rows) / V (fine rows) [Npad][16*h1t]
+  const float* xc;                 // x_up (coarse rows): the parent's out_0
+  const float* skip;               // + skip rows (x_down) or null
+  int b1_off, h1t, act1; float slope1;
+  MlpDev rest;                     // the unpooling layer's edge MLP layers 2..L
+  int normalize, grad, upwind;
+  int post_act; float post_slope;
 };
 
 struct EdgeHopArgs {

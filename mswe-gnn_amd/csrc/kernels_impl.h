@@ -1292,20 +1292,20 @@ __device__ __forceinline__ void pool_project_t(f32x4 (&h)[2 * NT], f32x4 (&o)[NT
     for (int t = 0; t < NT; ++t) o[t] = xp[t];
   }
 }
-// rank 0 -> (q.Us, q.os) of its edge lanes, rank 1 -> (q.Vn, q.inn) of its node lanes; then
-// rank 0 publishes U | O rows in pb, rank 1 V | O rows in both ranks' slabs (XS-strided,
-// edge_hop_core's node-row layout); after the barrier each rank reads the other side back.
+// rank 0 -> (q.Us, q.os) of its edge lanes, rank 1 -> (q.Vn, q.inn) of its node lanes, from
+// the side's row xp and its x_s; then rank 0 publishes U | O rows in pb, rank 1 V | O rows in
+// both ranks' slabs (XS-strided, edge_hop_core's node-row layout); after the barrier each
+// rank reads the other side back.
 template <int NT, int XS>
-__device__ __forceinline__ void edge_pool_project(EdgeHopRows<NT>& q, const PoolIn<NT>& pi, const EdgeHopArgs& a,
-                                                  const float* W, int lane, int g, int j, int rank, float* pb,
-                                                  float* slab0, float* slab1) {
+__device__ __forceinline__ void side_project_exchange(EdgeHopRows<NT>& q, const f32x4 (&xp)[NT], const f32x4 (&xs)[NT],
+                                                      const NpDesc& np, const float* W, int lane, int g, int j,
+                                                      int rank, float* pb, float* slab0, float* slab1) {
   constexpr int T2 = 2 * NT;
-  f32x4 xp[NT], h[T2], o[NT];
-  pool_mean<NT>(xp, pi, a, g);
-  if (a.pool.np.h1t == T2)
-    pool_project_t<NT, T2>(h, o, xp, pi.xs, a.pool.np, W, lane, rank);
+  f32x4 h[T2], o[NT];
+  if (np.h1t == T2)
+    pool_project_t<NT, T2>(h, o, xp, xs, np, W, lane, rank);
   else
-    pool_project_t<NT, NT>(h, o, xp, pi.xs, a.pool.np, W, lane, rank);
+    pool_project_t<NT, NT>(h, o, xp, xs, np, W, lane, rank);
   if (rank == 0) {
     store_row<T2>(pb + j * XS, h, T2, g);
     store_row<NT>(pb + j * XS + 16 * T2, o, NT, g);
@@ -1330,7 +1330,114 @@ __device__ __forceinline__ void edge_pool_project(EdgeHopRows<NT>& q, const Pool
   }
 }
 
-template <int NT, int ACT, int LST, int P, bool POOL = false>
+// ---- the unpooling layer into this scale fused in (PoolFuse::parent): per side node v (the
+// slot's source on rank 0, the lane's destination on rank 1) the intra-scale SWEGNN's one
+// edge parent(v) -> v (gnn.py:323-331 with own rows zero, K = 1, no filter) + skip -- the
+// unpooling launch's operations in its order (k_edge_coop / k_edge_hop, LST epilogue)
+template <int NT>
+struct UnpoolIn {
+  f32x4 uc[2 * NT], vv[2 * NT];  // unpool U of the parent, unpool V of v
+  f32x4 xc[NT], sk[NT], xs[NT];  // the parent's out_0 (x_up), v's skip row, v's x_s
+  bool ev;                       // v has a parent
+};
+template <int NT, int LST>
+__device__ __forceinline__ void edge_unpool_load(EdgeHopRows<NT>& r, UnpoolIn<NT>& u, const EdgeHopArgs& a, int tile,
+                                                 int j, int g, int rank) {
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  const PoolFuse& d = a.pool;
+  const LaneRec rec = load_rec(a.recs, tile, j);
+  const int2 pp = d.parent[(size_t)tile * kRowsPerWave + j];
+  r.L = lanes_of(rec, tile, j, a.n0);
+  const Lanes& L = r.L;
+  const float* z = a.c.zrow;
+  {
+    const int hs = 16 * a.h1t;
+    const float* Pb = a.Pe ? a.Pe + L.p * hs : z;
+#pragma unroll
+    for (int t = 0; t < T2; ++t) r.Ps[t] = ld4((t < a.h1t ? Pb : z) + 16 * t + 4 * g);
+  }
+  const size_t v = rank ? L.n : L.sr;
+  const int pc = rank ? pp.y : pp.x;
+  u.ev = pc >= 0;
+  const size_t c = (size_t)(pc >= 0 ? pc : d.cpad);
+  const int hs = 16 * d.h1t;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const bool on = t < d.h1t;
+    u.uc[t] = ld4((on ? d.Uu + c * hs : z) + 16 * t + 4 * g);
+    u.vv[t] = ld4((on ? d.Vu + v * hs : z) + 16 * t + 4 * g);
+  }
+  load_row<NT>(u.xc, d.xc + c * F, g);
+  load_row<NT>(u.sk, d.skip ? d.skip + v * F : z, g);
+  load_row<NT>(u.xs, a.xs + v * F, g);
+  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
+  if (LST && a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
+}
+template <int NT>
+__device__ __forceinline__ void unpool_row(f32x4 (&res)[NT], const UnpoolIn<NT>& u, const EdgeHopArgs& a,
+                                           const float* W, int lane, int g) {
+#pragma clang fp contract(off)
+  constexpr int T2 = 2 * NT;
+  const PoolFuse& d = a.pool;
+  f32x4 H[T2];
+  const int b1 = d.b1_off >= 0 ? d.b1_off : 0;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const f32x4 br = ld4(W + b1 + 16 * t + 4 * g);
+    H[t] = (t < d.h1t) ? (u.uc[t] + u.vv[t]) + br : zero4();
+  }
+  act_tiles<-1, T2>(H, d.act1, d.slope1);
+  f32x4 sv[NT];
+  if (d.rest.n > 0) {
+    run_mlp<T2, T2, NT, -1>(H, sv, d.rest, W, lane, g);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sv[t] = H[t];
+  }
+  if (d.normalize) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+    const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 q = sv[t] / nrm;
+      q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+      q.y = (q.y == q.y) ? q.y : 0.f;
+      q.z = (q.z == q.z) ? q.z : 0.f;
+      q.w = (q.w == q.w) ? q.w : 0.f;
+      sv[t] = q;
+    }
+  }
+  // put_message with the destination's rows zero (own_zero), then its one-edge sum
+  float rs = 0.f, rd = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    rs += hsum(u.xc[t]);
+    rd += hsum(zero4());
+  }
+  const bool act = (row_sum(rs) != 0.f) || (row_sum(rd) != 0.f);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f32x4 gv;
+    if (d.grad) {
+      gv = zero4() - u.xc[t];
+      if (d.upwind) {
+        gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
+        gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
+      }
+    } else {
+      gv = u.xc[t];
+    }
+    const f32x4 m = gv * sv[t];
+    const f32x4 agg = zero4() + ((u.ev && act) ? m : zero4());
+    res[t] = (zero4() + agg) + u.sk[t];
+  }
+  if (d.post_act) act_tiles<-1, NT>(res, d.post_act, d.post_slope);
+}
+
+// FUSE: 0 plain, 1 pooling fused in (PoolFuse::slots), 2 unpooling fused in (PoolFuse::parent)
+template <int NT, int ACT, int LST, int P, int FUSE = 0>
 __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT, T2 = 2 * NT;
@@ -1352,8 +1459,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
   EdgeHopRows<NT> q;
   [[maybe_unused]] PoolIn<NT> pin;
-  if constexpr (POOL)
+  [[maybe_unused]] UnpoolIn<NT> uin;
+  if constexpr (FUSE == 1)
     edge_pool_load<NT, LST>(q, pin, a, live ? tile : 0, j, g, r);
+  else if constexpr (FUSE == 2)
+    edge_unpool_load<NT, LST>(q, uin, a, live ? tile : 0, j, g, r);
   else
     edge_hop_load<NT, LST>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
   const bool split = a.reg.split < a.reg_nf;
@@ -1361,11 +1471,16 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   __syncthreads();
   c.W = smem;
   if (split) stage_glds<kWaves>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
-  if constexpr (POOL) {
-    static_assert(P == 2, "fused pooling: a source rank and a destination rank");
+  if constexpr (FUSE != 0) {
+    static_assert(P == 2, "fused pooling / unpooling: a source rank and a destination rank");
     __shared__ __attribute__((aligned(16))) float pbuf[G][kRowsPerWave][XS];
-    edge_pool_project<NT, XS>(q, pin, a, c.W, lane, g, j, r, &pbuf[grp][0][0], &slab_all[grp * P][0][0],
-                              &slab_all[grp * P + 1][0][0]);
+    f32x4 xp[NT];
+    if constexpr (FUSE == 1)
+      pool_mean<NT>(xp, pin, a, g);
+    else
+      unpool_row<NT>(xp, uin, a, c.W, lane, g);
+    side_project_exchange<NT, XS>(q, xp, FUSE == 1 ? pin.xs : uin.xs, a.pool.np, c.W, lane, g, j, r,
+                                  &pbuf[grp][0][0], &slab_all[grp * P][0][0], &slab_all[grp * P + 1][0][0]);
   }
   float* slab = &slab_all[w][0][0];
   float* b0 = &xbuf[grp][0][0][0];
@@ -1373,7 +1488,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   const Lanes& L = q.L;
   // ---- as edge_hop_core up to the MLP (every rank)
   float* my = slab + j * XS;
-  if constexpr (!POOL) {  // fused pooling: the destination rank stored them (barrier above)
+  if constexpr (FUSE == 0) {  // fused (un)pooling: the destination rank stored them (barrier above)
     store_row<T2>(my, q.Vn, T2, g);
     store_row<NT>(my + 16 * T2, q.inn, NT, g);
     wave_lds_sync();
@@ -1667,9 +1782,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 template <int NT>
 static const void* edge_coop_kernel(int prelu, int last, int pw = 0, int pool = 0) {
   if constexpr (NT == 2) {  // F = 32: each MLP layer's output tiles halve (F = 16 has one)
-    if (pool) {  // pooling fused in (EdgeHopArgs::pool)
-      if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2, true> : (const void*)k_edge_coop<NT, -1, 1, 2, true>;
-      return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2, true> : (const void*)k_edge_coop<NT, -1, 0, 2, true>;
+    if (pool == 1) {  // pooling fused in (EdgeHopArgs::pool)
+      if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2, 1> : (const void*)k_edge_coop<NT, -1, 1, 2, 1>;
+      return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2, 1> : (const void*)k_edge_coop<NT, -1, 0, 2, 1>;
+    }
+    if (pool == 2) {  // unpooling fused in
+      if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2, 2> : (const void*)k_edge_coop<NT, -1, 1, 2, 2>;
+      return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2, 2> : (const void*)k_edge_coop<NT, -1, 0, 2, 2>;
     }
     if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
     return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
@@ -2874,8 +2993,8 @@ hipError_t prepare_kernels() {
     const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
     for (int prelu = 0; prelu < 2; ++prelu)
       for (int last = 0; last < 2; ++last)
-        for (int pool = 0; pool < 2; ++pool) {
-          // fused pooling: + the source rank's U | O exchange rows (one slab per tile)
+        for (int pool = 0; pool < 3; ++pool) {
+          // fused (un)pooling: + the source rank's U | O exchange rows (one slab per tile)
           const int ps = pool ? (kWaves / 2) * kRowsPerWave * (48 * NT + 4) * 4 : 0;
           hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, 0, pool),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st - ps);
@@ -3005,14 +3124,15 @@ template <int NT>
 hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
-    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop, a.pool.slots != nullptr);
-    if (!f || (a.pool.slots && NT == 2 && a.coop != 2)) return hipErrorInvalidValue;
+    const int fuse = a.pool.slots ? 1 : a.pool.parent ? 2 : 0;
+    const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop, fuse);
+    if (!f || (fuse && NT == 2 && a.coop != 2) || (fuse == 2 && NT != 2)) return hipErrorInvalidValue;
     EdgeHopArgs b = a;
     const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
     void* args[] = {&b};
     return hipLaunchKernel(f, grid, dim3(kBlock), args, a.wdirect ? 0 : eh_lds_bytes(a.reg_nf), st);
   }
-  if (a.pool.slots) return hipErrorInvalidValue;  // pooling is fused into k_edge_coop only
+  if (a.pool.slots || a.pool.parent) return hipErrorInvalidValue;  // fused into k_edge_coop only
   const bool loop = tile_loop(a);
   EdgeHopArgs b = a;
   const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));

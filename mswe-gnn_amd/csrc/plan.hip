@@ -218,6 +218,8 @@ struct LevelMaps {              // level l: coarse scale l+1, fine scale l
   int* pool_child = nullptr;    // internal fine rows, reference order
   PoolSlot* pool_slots = nullptr; // per edge slot of the coarse scale: children of its source /
                                   // destination (pooling fused into the coarse edge hop)
+  int2* parent_slots = nullptr;   // per edge slot of the fine scale: parents of its source /
+                                  // destination (unpooling fused into the fine edge hop)
   LaneRec* un_recs = nullptr;   // fine nodes (scale l) and their coarse parents
   int un_ntiles = 0;
 };
@@ -729,6 +731,18 @@ bool pool_fusable(const msw_plan* P, int s, const Proc& pr) {
   return P->coop_w[0] > 0 && 2L * g.ntiles <= std::min(P->coop_w[0], kWaves * kMaxFusedPoolBlocks);
 }
 
+// The unpooling layer into fine scale s fused into the first launch of the processor on s
+// (k_edge_coop with PoolFuse::parent): F = 32, as pool_fusable; MSW_UNPOOL_FUSE=0 keeps the
+// unpooling launch.
+bool unpool_fusable(const msw_plan* P, int s, const Proc& pr, const Proc& up) {
+  const int on = getenv("MSW_UNPOOL_FUSE") ? atoi(getenv("MSW_UNPOOL_FUSE")) : 1;
+  if (!on || P->NT != 2 || P->part_rank >= 0 || s < 0 || s + 1 >= P->S) return false;
+  const ScaleCSR& g = P->sc[s];
+  if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s].parent_slots || g.ntiles <= 0) return false;
+  if (up.h1t > 2 * P->NT || up.K != 1) return false;
+  return P->coop_w[0] > 0 && 2L * g.ntiles <= std::min(P->coop_w[0], kWaves * kMaxFusedPoolBlocks);
+}
+
 // One forward.  Forward mode: the encoder reads graph rows of x (via perm) and the decoder
 // writes y (both patched per call); rollout mode: the internal state X is updated in place
 // by the decoder epilogue.
@@ -799,6 +813,7 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
       pa.np = np_of(P, P->procs[i + 1]);
       q.push_back(L);
     }
+    PoolFuse ufuse{};
     for (int i = 0; i < S; ++i) {      // coarse -> fine
       const int j = S - 1 + i, s = S - 1 - i;
       Epilogue e{};
@@ -809,11 +824,21 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
         e.uu_a = up.a_u; e.uu_h1t = up.h1t; e.Uu = P->Uu;
       }
       e.dec = dl;  // every scale's rows are decoded once final (gnn.py:335-348)
-      sched_proc(P, q, P->procs[j], P->xup, e, i == 0 && fuse.slots ? &fuse : nullptr);
+      sched_proc(P, q, P->procs[j], P->xup, e, i == 0 && fuse.slots ? &fuse : ufuse.parent ? &ufuse : nullptr);
+      ufuse = PoolFuse{};
       if (s > 0) {                      // intra_scale_gnn[i] on level s-1 (+ skip) + projection
         const Proc& up = P->unpools[i];
         const ScaleCSR& fs = P->sc[s - 1];
         const LevelMaps& m = P->lv[s - 1];
+        if (unpool_fusable(P, s - 1, P->procs[j + 1], up)) {  // the next processor's first launch unpools
+          ufuse.parent = m.parent_slots; ufuse.cpad = P->sc[s].n0;
+          ufuse.Uu = P->Uu; ufuse.Vu = P->Vu; ufuse.xc = P->xup; ufuse.skip = P->skip ? P->xdown : nullptr;
+          ufuse.b1_off = up.b1_off; ufuse.h1t = up.h1t; ufuse.act1 = up.act1; ufuse.slope1 = up.slope1;
+          ufuse.rest = up.rest; ufuse.normalize = up.normalize; ufuse.grad = up.with_gradient;
+          ufuse.upwind = up.upwind; ufuse.post_act = 0; ufuse.post_slope = 0.f;
+          ufuse.np = np_of(P, P->procs[j + 1]);
+          continue;
+        }
         Launch L;
         L.kind = L_EDGE_HOP;
         L.scale = s - 1;
@@ -970,7 +995,11 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       RegionBuilder R(P->blob, 0);
       a.b1_off = R.put(a.b1_off, 16 * a.h1t);
       rl.mlp(R, a.rest);
-      if (a.pool.slots) rl.np(R, a.pool.np);  // fused pooling: projected before the MLP
+      if (a.pool.parent) {  // fused unpooling: its edge MLP, then the projection
+        a.pool.b1_off = R.put(a.pool.b1_off, 16 * a.pool.h1t);
+        rl.mlp(R, a.pool.rest);
+      }
+      if (a.pool.slots || a.pool.parent) rl.np(R, a.pool.np);  // fused (un)pooling: before the MLP
       const int split = R.pos();  // operands after this one stream in behind the MLP
       if (a.last) rl.epi(R, a.epi);
       // filt_a stays a blob offset (the one-tile-per-wave variant loads it into registers and
@@ -1107,7 +1136,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // place of four, for tests)
       // fused pooling exists in the cooperative kernels only (pool_fusable): F = 32 two waves
       // per tile; F = 64 four, or two where four do not fit one round (below)
-      if (a.pool.slots && P->NT == 2) a.coop = 2;
+      if ((a.pool.slots || a.pool.parent) && P->NT == 2) a.coop = 2;
       const int c2 = getenv("MSW_COOP2_F64") ? atoi(getenv("MSW_COOP2_F64")) : 1;
       if (c2 == 2 && a.coop == 4) a.coop = 0;
       a.wdirect = 0;
@@ -1578,6 +1607,20 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       if ((rc = build_tiles(rp, tl))) return rc;
       m.un_ntiles = (int)tl.size();
       if ((rc = pupload(P, &m.un_recs, make_recs(rp, us, fs.n0, tl, nullptr)))) return rc;
+      {  // fused unpooling: one parent per fine node at most (else the launch stays)
+        bool one = true;
+        std::vector<int> par(fs.ns, -1);
+        for (int i = 0; i < fs.ns; ++i) {
+          if (rp[i + 1] - rp[i] > 1) one = false;
+          if (rp[i + 1] > rp[i]) par[i] = us[rp[i]];
+        }
+        if (one && !fs.hrecs.empty()) {
+          auto par_of = [&](int row) { return row >= fs.n0 && row < fs.n0 + fs.ns ? par[row - fs.n0] : -1; };
+          std::vector<int2> pv(fs.hrecs.size());
+          for (size_t q = 0; q < pv.size(); ++q) pv[q] = int2{par_of(fs.hrecs[q].src), par_of(fs.hrecs[q].n)};
+          if ((rc = pupload(P, &m.parent_slots, pv))) return rc;
+        }
+      }
     }
   }
   return MSW_OK;
