@@ -1626,7 +1626,8 @@ __device__ __forceinline__ void pool_project_part(float* dst_row, const f32x4 (&
 // still fits beside it; the epilogue's operands stay in the blob (F = 64 relocation).
 // P = 2: two tiles per workgroup, two waves each (a slab and exchange buffers per tile);
 // P = 4: the whole workgroup on one tile.
-template <int ACT, int LST, int P = 4, bool POOL = false>
+// FUSE: 0 plain, 1 pooling fused in, 2 unpooling fused in (as k_edge_coop)
+template <int ACT, int LST, int P = 4, int FUSE = 0>
 __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma clang fp contract(off)
   constexpr int NT = 4, F = 16 * NT, T2 = 2 * NT, G = kWaves / P, TS = NT / P;
@@ -1657,9 +1658,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   }
   EdgeHopRows<NT> q;
   [[maybe_unused]] PoolIn<NT> pin;
-  [[maybe_unused]] const int side = r >= P / 2;  // fused pooling: 0 source side, 1 destination side
-  if constexpr (POOL)
+  [[maybe_unused]] UnpoolIn<NT> uin;
+  [[maybe_unused]] const int side = r >= P / 2;  // fused (un)pooling: 0 source side, 1 destination side
+  if constexpr (FUSE == 1)
     edge_pool_load<NT, LST>(q, pin, a, tile, j, g, side);
+  else if constexpr (FUSE == 2)
+    edge_unpool_load<NT, LST>(q, uin, a, tile, j, g, side);
   else
     edge_hop_load<NT, LST>(q, a, tile, j, g);
   const Lanes& L = q.L;
@@ -1667,18 +1671,23 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   if (a.reg.len > 0 && !a.wdirect) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
   const float* Wm = a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W;
   float* my = &slab[j][0];
-  if constexpr (POOL) {
+  if constexpr (FUSE != 0) {
     // source side -> exchange rows (in xbuf, free until the MLP), destination side -> the
-    // node slab; projection operands from the blob (c.W)
+    // node slab; projection (and unpooling MLP) operands from the blob (c.W); the unpooling
+    // row is formed by every rank of its side (the projection's output tiles are split)
     constexpr int XPB = 16 * T2 + 16 * NT + 4;
     static_assert(kRowsPerWave * XPB <= 2 * kRowsPerWave * XW, "exchange rows fit the xbuf pair");
     float* pb = &xbuf[0][0][0] + j * XPB;
     f32x4 xp[NT];
-    pool_mean<NT>(xp, pin, a, g);
-    if (a.pool.np.h1t == T2)
-      pool_project_part<NT, P, T2>(side ? my : pb, xp, pin.xs, a.pool.np, c.W, lane, g, side, r % (P / 2));
+    if constexpr (FUSE == 1)
+      pool_mean<NT>(xp, pin, a, g);
     else
-      pool_project_part<NT, P, NT>(side ? my : pb, xp, pin.xs, a.pool.np, c.W, lane, g, side, r % (P / 2));
+      unpool_row<NT>(xp, uin, a, c.W, lane, g);
+    const f32x4(&xsr)[NT] = FUSE == 1 ? pin.xs : uin.xs;
+    if (a.pool.np.h1t == T2)
+      pool_project_part<NT, P, T2>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
+    else
+      pool_project_part<NT, P, NT>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
     __syncthreads();
     load_row<T2>(q.Us, pb, g);
     load_row<NT>(q.os, pb + 16 * T2, g);
@@ -1793,13 +1802,21 @@ static const void* edge_coop_kernel(int prelu, int last, int pw = 0, int pool = 
     if (last) return prelu ? (const void*)k_edge_coop<NT, 1, 1, 2> : (const void*)k_edge_coop<NT, -1, 1, 2>;
     return prelu ? (const void*)k_edge_coop<NT, 1, 0, 2> : (const void*)k_edge_coop<NT, -1, 0, 2>;
   } else if constexpr (NT == 4) {  // F = 64: four waves per tile (pw = 2: two)
-    if (pool) {  // pooling fused in (EdgeHopArgs::pool)
+    if (pool == 1) {  // pooling fused in (EdgeHopArgs::pool)
       if (pw == 2) {
-        if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2, true> : (const void*)k_edge_coop4<-1, 1, 2, true>;
-        return prelu ? (const void*)k_edge_coop4<1, 0, 2, true> : (const void*)k_edge_coop4<-1, 0, 2, true>;
+        if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2, 1> : (const void*)k_edge_coop4<-1, 1, 2, 1>;
+        return prelu ? (const void*)k_edge_coop4<1, 0, 2, 1> : (const void*)k_edge_coop4<-1, 0, 2, 1>;
       }
-      if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 4, true> : (const void*)k_edge_coop4<-1, 1, 4, true>;
-      return prelu ? (const void*)k_edge_coop4<1, 0, 4, true> : (const void*)k_edge_coop4<-1, 0, 4, true>;
+      if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 4, 1> : (const void*)k_edge_coop4<-1, 1, 4, 1>;
+      return prelu ? (const void*)k_edge_coop4<1, 0, 4, 1> : (const void*)k_edge_coop4<-1, 0, 4, 1>;
+    }
+    if (pool == 2) {  // unpooling fused in
+      if (pw == 2) {
+        if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2, 2> : (const void*)k_edge_coop4<-1, 1, 2, 2>;
+        return prelu ? (const void*)k_edge_coop4<1, 0, 2, 2> : (const void*)k_edge_coop4<-1, 0, 2, 2>;
+      }
+      if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 4, 2> : (const void*)k_edge_coop4<-1, 1, 4, 2>;
+      return prelu ? (const void*)k_edge_coop4<1, 0, 4, 2> : (const void*)k_edge_coop4<-1, 0, 4, 2>;
     }
     if (pw == 2) {
       if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2> : (const void*)k_edge_coop4<-1, 1, 2>;
@@ -2982,7 +2999,7 @@ hipError_t prepare_kernels() {
       const int st = (kWaves / pw) * (kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4);
       for (int prelu = 0; prelu < 2; ++prelu)
         for (int last = 0; last < 2; ++last)
-          for (int pool = 0; pool < 2; ++pool) {
+          for (int pool = 0; pool < 3; ++pool) {
             hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, pw, pool),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st);
             if (e != hipSuccess) return e;
@@ -3126,7 +3143,7 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   if (a.coop == 2 || a.coop == 4) {  // waves per tile; 4: F = 64, one tile per workgroup
     const int fuse = a.pool.slots ? 1 : a.pool.parent ? 2 : 0;
     const void* f = edge_coop_kernel<NT>(a.c.prelu, a.last, a.coop, fuse);
-    if (!f || (fuse && NT == 2 && a.coop != 2) || (fuse == 2 && NT != 2)) return hipErrorInvalidValue;
+    if (!f || (fuse && NT == 2 && a.coop != 2)) return hipErrorInvalidValue;
     EdgeHopArgs b = a;
     const dim3 grid = xcd_grid(b, a.coop == 4 ? a.ntiles : cdiv((long)a.ntiles * a.coop, kWaves));
     void* args[] = {&b};

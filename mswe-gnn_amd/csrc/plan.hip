@@ -732,11 +732,14 @@ bool pool_fusable(const msw_plan* P, int s, const Proc& pr) {
 }
 
 // The unpooling layer into fine scale s fused into the first launch of the processor on s
-// (k_edge_coop with PoolFuse::parent): F = 32, as pool_fusable; MSW_UNPOOL_FUSE=0 keeps the
+// (k_edge_coop / k_edge_coop4 with PoolFuse::parent), as pool_fusable, F = 32 (F = 64 with
+// MSW_UNPOOL_FUSE=2); MSW_UNPOOL_FUSE=0 keeps the
 // unpooling launch.
 bool unpool_fusable(const msw_plan* P, int s, const Proc& pr, const Proc& up) {
   const int on = getenv("MSW_UNPOOL_FUSE") ? atoi(getenv("MSW_UNPOOL_FUSE")) : 1;
-  if (!on || P->NT != 2 || P->part_rank >= 0 || s < 0 || s + 1 >= P->S) return false;
+  // F = 64 only on request (=2): its 384-MFMA unpooling MLP per side outweighs the launch it
+  // saves (zenodo4_f64 -2.5 %, profiles/r03/ab_unpool_fuse_f64.txt)
+  if (!on || !(P->NT == 2 || (P->NT == 4 && on == 2)) || P->part_rank >= 0 || s < 0 || s + 1 >= P->S) return false;
   const ScaleCSR& g = P->sc[s];
   if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s].parent_slots || g.ntiles <= 0) return false;
   if (up.h1t > 2 * P->NT || up.K != 1) return false;
@@ -1154,7 +1157,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
           a.wdirect = 1;
         }
       }
-      if (a.pool.slots && !a.coop) a.coop = 2;  // F = 64 fused pooling: two waves per tile, any grid
+      if ((a.pool.slots || a.pool.parent) && !a.coop) a.coop = 2;  // F = 64 fused: two waves per tile, any grid
       break;
     }
     case L_HOP:

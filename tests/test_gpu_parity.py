@@ -820,21 +820,26 @@ def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, F, act, coop2):
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
 
 
-@pytest.mark.parametrize("kw", [{}, {"mlp_activation": "relu"}, {"skip_connections": False}])
-def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, kw):
+@pytest.mark.parametrize("F,kw,coop2", [(32, {}, None), (32, {"mlp_activation": "relu"}, None),
+                                        (32, {"skip_connections": False}, None), (64, {}, None),
+                                        (64, {"mlp_activation": "relu"}, "2")])
+def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, F, kw, coop2):
     """The unpooling layer (intra-scale SWEGNN, own rows zero, + skip, + projection of the next
     processor) fused into the fine scale's first edge-MLP + hop launch (k_edge_coop<.., 2>,
-    MSW_UNPOOL_FUSE=1, the default on small scales at F = 32) == the separate unpooling launch
-    (MSW_UNPOOL_FUSE=0), bit for bit: forward, rollout, a batch of two meshes; fewer launches;
-    and the oracle."""
+    k_edge_coop4<.., 2> at F = 64 -- four or, with MSW_COOP2_F64=2, two waves per tile;
+    MSW_UNPOOL_FUSE=1, the default on small scales at F = 32; =2 at F = 64) == the separate
+    unpooling launch (MSW_UNPOOL_FUSE=0), bit for bit: forward, rollout, a batch of two meshes;
+    fewer launches; and the oracle."""
+    if coop2:
+        monkeypatch.setenv("MSW_COOP2_F64", coop2)
     from mswegnn.batch import collate
     from mswegnn.rollout import rollout_test
     ga = _reparent(wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=23))
     gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=24, T=6), seed=24)
     outs, kps = {}, {}
-    for sv in ("0", "1"):
-        monkeypatch.setenv("MSW_UNPOOL_FUSE", sv)
-        m = _hip(build_msgnn(4, 32, 4, **kw), cuda)
+    for sv in ("0", "1"):  # F = 64 fuses only on request (MSW_UNPOOL_FUSE=2)
+        monkeypatch.setenv("MSW_UNPOOL_FUSE", sv if sv == "0" or F == 32 else "2")
+        m = _hip(build_msgnn(4, F, 4, **kw), cuda)
         gd = ga.to(cuda)
         with torch.no_grad():
             y = m(gd).cpu()
@@ -843,6 +848,6 @@ def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, kw):
     assert kps["1"] <= kps["0"] - 2, kps
     for a, b in zip(outs["0"], outs["1"]):
         assert torch.equal(a, b)
-    m = build_msgnn(4, 32, 4, **kw)
-    cfg = orc.msgnn_config(num_scales=4, hid_features=32, K=4, **kw)
+    m = build_msgnn(4, F, 4, **kw)
+    cfg = orc.msgnn_config(num_scales=4, hid_features=F, K=4, **kw)
     assert per_step_rel(outs["1"][1], orc.rollout(state_dict_of(m), cfg, ga)) <= REL_TOL
