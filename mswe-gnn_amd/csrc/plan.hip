@@ -1158,6 +1158,14 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         }
       }
       if ((a.pool.slots || a.pool.parent) && !a.coop) a.coop = 2;  // F = 64 fused: two waves per tile, any grid
+      // A/B (MSW_FUSE_P4=1): an F = 64 fused launch on four waves per tile with the MLP region
+      // read from the blob (two workgroups per CU) where staging it would cost a second round
+      if ((a.pool.slots || a.pool.parent) && P->NT == 4 && a.coop == 2 && getenv("MSW_FUSE_P4") &&
+          atoi(getenv("MSW_FUSE_P4")) != 0 && a.reg.len > 0 &&
+          a.ntiles <= resident_of(P->NT, 7, a.c.prelu, a.last, 0, 0)) {
+        a.coop = 4;
+        a.wdirect = 1;
+      }
       break;
     }
     case L_HOP:
