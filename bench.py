@@ -145,14 +145,25 @@ def time_kernel(plan, kernel, scale, iters=200):
     return e0.elapsed_time(e1) / 1e3 / iters, units
 
 
-def read_traffic(path, kernel_prefix):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), or None."""
+def summary_provenance(d, lib_sha):
+    """Which library a committed profile summary was measured on, against the one loaded now."""
+    src = d.get("library_sha256")
+    return {"source_library_sha256": src, "stale": (src != lib_sha) if src else True,
+            "source": d.get("source")}
+
+
+def read_traffic(path, kernel_prefix, lib_sha=None):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), or None.
+    With lib_sha: {"bytes_per_launch", "source_library_sha256", "stale"} instead."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
     except OSError:
         return None
+    v = d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
+    if lib_sha is None or v is None:
+        return v
+    return dict(summary_provenance(d, lib_sha), bytes_per_launch=v, kernel=d.get(kernel_prefix, {}).get("kernel"))
 
 
 def lpt_split(sizes, world):
@@ -379,6 +390,104 @@ def ddp_training_check(rank, world, barrier, timeout=150):
     return res
 
 
+# N > 1 records after the weak line's timed region, run in this order inside ONE wall-clock
+# budget (--extras-budget): a section starts only when its estimated cost fits what is left,
+# so the line is printed before a driver time limit whatever the node does.  Estimates (s):
+# a strong-scaling set of G config-3 simulations ~ 10 + 0.4 G (mesh generation on rank 0
+# dominates: ~26 s for G = 128); the RCCL children get min(their limit, what is left) and
+# start only with at least `start_s` left.
+CHILD_SECTIONS = {  # name -> (limit s, minimum left to start s)
+    "zenodo4_2_parts": (180, 60), "ddp": (150, 60), "hbm1m_parts": (240, 120)}
+
+
+def strong_set_cost(G):
+    return 10.0 + 0.4 * G
+
+
+def run_extras(dist, rank, world, dev, args, cpu_barrier, backend, group=None, engine="hip",
+               workload="config3", gpus=None):
+    """The N > 1 records (strong scaling, RCCL single-mesh decomposition, DDP training) under
+    one budget.  Every rank calls this; rank 0 decides whether a section starts and broadcasts
+    the decision (host group), so all ranks take the same branches.  Returns the records
+    (complete on rank 0): skipped sections are {"skipped": ...}, every section has wall_s."""
+    t0 = time.perf_counter()
+    budget = float(args.extras_budget)
+    gpus = torch.cuda.device_count() if gpus is None else gpus
+
+    def left():
+        return budget - (time.perf_counter() - t0)
+
+    def agree(ok):
+        obj = [bool(ok)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return obj[0]
+    sets = [int(x) for x in str(args.strong_sets).split(",") if x.strip()]
+    small = [G for G in sets if G <= 16]
+    large = [G for G in sets if G > 16]
+    rccl_ok = backend == "nccl" and gpus >= 2 and not args.no_partition_check
+    W = min(world, gpus)
+    order = ([("strong", G) for G in small] + [("child", "zenodo4_2_parts"), ("child", "ddp")]
+             + [("strong", G) for G in large] + [("child", "hbm1m_parts")])
+    strong = None
+    part, ddp = {}, None
+    log = []
+    for kind, what in order:
+        s0 = time.perf_counter()
+        if kind == "strong":
+            need = strong_set_cost(what)
+            go = agree(left() >= need)
+            if go:
+                try:
+                    rec = strong_scaling_section(dist, rank, world, dev, engine, [what], args.T, args.strong_steps,
+                                                 1, cpu_barrier, workload=workload)
+                except Exception as e:  # noqa: BLE001
+                    rec = {"sets": [{"G": what, "error": repr(e)}]}
+                ent = rec["sets"][0] if rec.get("sets") else {"G": what}
+                if strong is None:
+                    strong = {k: v for k, v in rec.items() if k != "sets"}
+                    strong["sets"] = []
+            else:
+                ent = {"G": what, "skipped": "budget", "left_s": round(left(), 1), "needs_s": need}
+                if strong is None:
+                    strong = {"workload": workload, "sets": []}
+            ent["wall_s"] = round(time.perf_counter() - s0, 2)
+            strong["sets"].append(ent)
+            log.append((f"strong_G{what}", ent["wall_s"], "skipped" in ent))
+            continue
+        limit, start = CHILD_SECTIONS[what]
+        if what == "hbm1m_parts" and (args.no_partition_large or W < 4):
+            res = {"skipped": "single-mesh decomposition of the ~1.3M-node mesh runs at N >= 4"
+                              + (" (--no-partition-large)" if args.no_partition_large else "")}
+        elif not rccl_ok:
+            res = {"skipped": "needs the nccl (RCCL) backend and >= 2 GPUs"
+                              + (" (--no-partition-check)" if args.no_partition_check else "")}
+        elif not agree(left() >= start):
+            res = {"skipped": "budget", "left_s": round(left(), 1), "needs_s": start}
+        else:
+            tl = int(max(30, min(limit, left())))
+            if what == "ddp":
+                res = ddp_training_check(rank, world, cpu_barrier, timeout=tl)
+            elif what == "zenodo4_2_parts":
+                res = partitioned_rollout_check(rank, world, cpu_barrier, timeout=tl)
+            else:
+                res = partitioned_rollout_check(rank, world, cpu_barrier, timeout=tl, parts=W, mesh="hbm1m", steps=2)
+            res = dict(res or {}, time_limit_s=tl)
+        res["wall_s"] = round(time.perf_counter() - s0, 2)
+        log.append((what, res["wall_s"], "skipped" in res))
+        if what == "ddp":
+            ddp = res
+        else:
+            part[f"hbm1m_{W}_parts" if what == "hbm1m_parts" else what] = res
+    return {"strong_scaling": strong, "partitioned_rollout_rccl": part, "ddp_training_rccl": ddp,
+            "extras": {"budget_s": budget, "wall_s": round(time.perf_counter() - t0, 2),
+                       "order": [{"section": n, "wall_s": w, "skipped": sk} for n, w, sk in log]}}
+
+
+def msw_env():
+    """The engine switches set in this process (DESIGN §4 'Switches'): empty on a default run."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("MSW_")}
+
+
 def _built_from_sources():
     try:
         import build_engine
@@ -414,6 +523,10 @@ def main():
                     help="N > 1: skip the ~1.3M-node mesh in the RCCL single-mesh decomposition record")
     ap.add_argument("--no-partition-check", action="store_true",
                     help="N > 1: skip the RCCL single-mesh decomposition check")
+    ap.add_argument("--extras-budget", type=float, default=180.0,
+                    help="N > 1: wall-clock budget (s) of the records after the timed region, run in "
+                         "the order strong G<=16, zenodo4 2 parts, DDP, strong G>16, hbm1m parts; "
+                         "a section that does not fit is recorded as skipped")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -527,31 +640,6 @@ def main():
                            "note": "the reference loop with a no-op model (stub returning zeros): "
                                    "what the caller itself costs per step"}
 
-    strong = part_check = ddp_check = None
-    if world > 1:
-        # the north star's strong scaling (fixed config-3 sets, rank 0 alone vs all ranks with
-        # the RCCL all-gather) and the RCCL single-mesh decomposition: after the weak line's
-        # timed region, recorded, never fatal
-        def cpu_barrier():
-            dist.barrier(group=cpu_group)
-        sets = [int(s) for s in args.strong_sets.split(",") if s.strip()]
-        if sets:
-            try:
-                strong = strong_scaling_section(dist, rank, world, dev, "hip", sets, T, args.strong_steps,
-                                                1, cpu_barrier)
-            except Exception as e:  # noqa: BLE001
-                strong = {"error": repr(e)}
-        if not args.no_partition_check and backend == "nccl" and torch.cuda.device_count() >= 2:
-            # zenodo4 over two GPUs (transport check), then config 5's ~1.3M-node mesh over
-            # every rank's GPU: the single-mesh strong scaling of SURVEY §8 f2
-            # (the large mesh at N >= 4 only, to bound the driver's N = 2 / 4 / 8 sequence)
-            part_check = {"zenodo4_2_parts": partitioned_rollout_check(rank, world, cpu_barrier, timeout=180)}
-            W = min(world, torch.cuda.device_count())
-            if not args.no_partition_large and W >= 4:
-                part_check[f"hbm1m_{W}_parts"] = partitioned_rollout_check(
-                    rank, world, cpu_barrier, timeout=240, parts=W, mesh="hbm1m", steps=2)
-            ddp_check = ddp_training_check(rank, world, cpu_barrier)
-
     result = None
     if rank == 0:
         st = plan.stats()
@@ -569,15 +657,20 @@ def main():
         # the PMC summary holds the default workload's finest hop ("k_hop") and the config-5
         # mesh's ("k_hop_large"); other workloads have no committed counter pass
         pmc_key = {"zenodo4": "k_hop", "hbm1m": "k_hop_large"}.get(args.workload) if B == 1 else None
-        traffic = read_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), pmc_key) if pmc_key else None
+        lib_sha = _lib.lib_info()["sha256"]
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+        traffic_rec = read_traffic(pmc_path, pmc_key, lib_sha) if pmc_key else None
+        traffic = traffic_rec["bytes_per_launch"] if traffic_rec else None
         roof = {"kernel": "k_hop<32> (SWEGNN hop: CSR pull + filter), finest scale",
                 "bound": "hbm", "achieved": hop_bytes / t_hop / 1e9, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": hop_bytes / t_hop / 1e9 / HBM_PEAK_GBS,
-                "traffic": traffic, "algorithmic_bytes_per_launch": hop_bytes,
+                "traffic": traffic, "traffic_source": traffic_rec, "algorithmic_bytes_per_launch": hop_bytes,
                 "avg_launch_us": t_hop * 1e6, "rows": rows, "edges": edges,
                 "timer": "HIP events on the launching stream around 200 back-to-back launches: "
-                         "launch-to-launch period (kernel + boundary); rocprof = the committed "
-                         "rocprofv3 kernel durations of the same runs (tools/roofline_check.py)",
+                         "launch-to-launch period (kernel + boundary); rocprof = rocprofv3 kernel "
+                         "durations from the committed trace summary of this command "
+                         "(tools/roofline_check.py), on the library named by its source_library_sha256 "
+                         "(stale = measured on another build than the one loaded now)",
                 "other_kernels": {
                     "k_edge_hop<32> (edge MLP + hop 1)": {
                         "avg_launch_us": t_eh * 1e6, "edges": e_eh,
@@ -632,13 +725,14 @@ def main():
                       "unit": "TFLOP/s", "frac": fle / tle / 1e12 / FP32_MFMA_PEAK_TFS}
                 hb = {"algorithmic_bytes_per_launch": ble, "achieved": ble / tle / 1e9, "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": ble / tle / 1e9 / HBM_PEAK_GBS,
-                      "traffic": read_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"),
-                                              "k_edge_hop_large")}
+                      "traffic": read_traffic(pmc_path, "k_edge_hop_large"),
+                      "traffic_source": read_traffic(pmc_path, "k_edge_hop_large", lib_sha)}
                 roof["large_mesh"] = {
                     "workload": "hbm1m", "fine_nodes": dl["fine_nodes"], "rows": rl, "edges": el,
                     "algorithmic_bytes_per_launch": bl, "avg_launch_us": tl * 1e6,
                     "achieved": bl / tl / 1e9, "frac": bl / tl / 1e9 / HBM_PEAK_GBS,
-                    "traffic": read_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_hop_large"),
+                    "traffic": read_traffic(pmc_path, "k_hop_large"),
+                    "traffic_source": read_traffic(pmc_path, "k_hop_large", lib_sha),
                     "edge_mlp": {"kernel": "k_edge_hop<32> (edge MLP + hop 1), finest scale",
                                  "bound": "hbm" if hb["frac"] >= mf["frac"] else "mfma",
                                  "edges": ele, "rows": rle, "avg_launch_us": tle * 1e6, "mfma": mf, "hbm": hb}}
@@ -651,8 +745,9 @@ def main():
         try:
             if args.workload == "zenodo4" and B == 1:
                 with open(os.path.join(ROOT, "profiles", "roofline_rocprof.json")) as f:
-                    rp = json.load(f)["by_role"]
-                rr = {}
+                    rpd = json.load(f)
+                rp = rpd["by_role"]
+                rr = summary_provenance(rpd, lib_sha)
                 if "hop" in rp:
                     d = rp["hop"]["avg_duration_us"] * 1e-6
                     rr["hop"] = {"kernel": rp["hop"]["kernel"], "avg_duration_us": d * 1e6,
@@ -723,7 +818,12 @@ def main():
         result = {
             "metric": "mesh-nodes x rollout-steps / sec (fine-scale nodes); fp32 max-abs err vs CPU ref",
             "value": value, "unit": "fine-node-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "ms_per_rollout": ms_per_step / B, "us_per_timestep": ms_per_step * 1e3 / T,
+            "step_note": "one bench step = one T-step rollout of this rank's simulation(s): ms_per_step = "
+                         "ms per rollout call (ms_per_rollout: per simulation of the batch), "
+                         "us_per_timestep = one autoregressive time step of the whole batch",
+            "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (own multi-scale triangular mesh generator; dry start + hydrograph BC)",
             "config": dict(desc, caller=args.caller, global_batch=args.global_batch or None,
@@ -733,6 +833,7 @@ def main():
             "timed_region": "whole rollouts (T steps each) incl. the per-rollout edge encoder + edge "
                             "terms of every processor (msw_rollout prologue); inputs resident in HBM",
             "library": dict(_lib.lib_info(), built_from_current_sources=_built_from_sources()),
+            "msw_env": msw_env(),
             "all_node_steps_per_s": value * desc.get("batch_nodes", desc["all_nodes"]) / fine_rank,
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "engine": {"kernels_per_step": st["kernels_per_step"], "graph_captured": st["graph_captured"],
@@ -743,12 +844,15 @@ def main():
         }
         if caller_overhead is not None:
             result["caller_overhead"] = caller_overhead
-        if world > 1:
-            result["strong_scaling"] = strong
-            result["partitioned_rollout_rccl"] = part_check
-            if ddp_check is not None:
-                result["ddp_training_rccl"] = ddp_check
     if world > 1:
+        # the north star's strong scaling (fixed config-3 sets, rank 0 alone vs all ranks with
+        # the RCCL all-gather), the RCCL single-mesh decomposition and DDP training: after the
+        # weak line's timed region and its rank-0 records, inside --extras-budget, never fatal
+        def cpu_barrier():
+            dist.barrier(group=cpu_group)
+        extras = run_extras(dist, rank, world, dev, args, cpu_barrier, backend, group=cpu_group)
+        if rank == 0:
+            result.update(extras)
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:

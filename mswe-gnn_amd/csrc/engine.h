@@ -362,6 +362,26 @@ struct RowMlpArgs {
   float* out; int out_stride, out_tiles;
 };
 
+// dynamic LDS of a launch: its weight region rounded up to whole 1-KB LDS-DMA chunks
+// (kChunk floats); the edge hop stages its MLP region at every width
+constexpr int kChunk = 256;
+constexpr size_t eh_lds_bytes(int floats) {
+  return (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float);
+}
+// Dynamic-LDS cap of the cooperative edge hop (k_edge_coop / k_edge_coop4) with `pw` waves
+// per tile, with fused (un)pooling or not: 160 KB minus its static slabs and exchange buffers.
+// prepare_kernels sets exactly this; plan creation checks every such launch against it.
+template <int NT>
+constexpr int edge_coop_lds_cap(int pw, int fuse) {
+  if constexpr (NT == 4) {
+    return 160 * 1024 - (kWaves / pw) * (kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4);
+  } else {
+    const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
+    // fused (un)pooling: + the source rank's U | O exchange rows (one slab per tile)
+    const int ps = fuse ? (kWaves / 2) * kRowsPerWave * (48 * NT + 4) * 4 : 0;
+    return 160 * 1024 - st - ps;
+  }
+}
 // Records `msg` as msw_last_error() (thread-local) and returns `code` (plan.hip).
 int set_error(int code, const char* msg);
 

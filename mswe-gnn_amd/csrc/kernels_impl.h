@@ -489,7 +489,6 @@ constexpr int kTraceWG = 8192;
 // of the region straight into LDS, no VGPR round trip.  Copies the 256-float chunks that
 // cover [first, last) floats of the region; a partial final chunk reads up to 255 floats
 // past the region (the blob and the LDS allocation are padded for it).
-constexpr int kChunk = 256;
 template <int WV = kWaves>
 __device__ __forceinline__ void stage_glds(float* smem, const float* __restrict__ W, WReg r, int first, int last) {
   const int lane = threadIdx.x & 63;
@@ -2919,11 +2918,6 @@ __global__ __launch_bounds__(kBlock) void k_rowmlp(RowMlpArgs a) {
 // ---------------------------------------------------------------------------- launchers
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
-// dynamic LDS of a launch: its weight region rounded up to whole 1-KB LDS-DMA chunks
-// the edge hop stages its MLP region at every width
-constexpr size_t eh_lds_bytes(int floats) {
-  return (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float);
-}
 template <int NT>
 constexpr size_t lds_bytes(int floats) {
   return kStaged<NT> ? (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float) : 0;
@@ -2996,25 +2990,23 @@ hipError_t prepare_kernels() {
   }
   if constexpr (NT == 4) {  // F = 64 cooperative edge hops: a slab + exchange buffers per tile
     for (int pw = 2; pw <= 4; pw += 2) {
-      const int st = (kWaves / pw) * (kRowsPerWave * (48 * NT + 4) * 4 + 2 * kRowsPerWave * (32 * NT + 4) * 4);
       for (int prelu = 0; prelu < 2; ++prelu)
         for (int last = 0; last < 2; ++last)
           for (int pool = 0; pool < 3; ++pool) {
             hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, pw, pool),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st);
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               edge_coop_lds_cap<NT>(pw, pool));
             if (e != hipSuccess) return e;
           }
     }
   }
   if constexpr (NT == 2) {  // cooperative edge hops: 160 KB minus slabs and exchange buffers
-    const int st = kWaves * kRowsPerWave * (48 * NT + 4) * 4 + (kWaves / 2) * 2 * kRowsPerWave * (32 * NT + 4) * 4;
     for (int prelu = 0; prelu < 2; ++prelu)
       for (int last = 0; last < 2; ++last)
         for (int pool = 0; pool < 3; ++pool) {
-          // fused (un)pooling: + the source rank's U | O exchange rows (one slab per tile)
-          const int ps = pool ? (kWaves / 2) * kRowsPerWave * (48 * NT + 4) * 4 : 0;
           hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, 0, pool),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - st - ps);
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             edge_coop_lds_cap<NT>(2, pool));
           if (e != hipSuccess) return e;
         }
   }

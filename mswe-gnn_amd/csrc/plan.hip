@@ -401,6 +401,9 @@ struct msw_plan {
   int xcd_max = 1;
   int coop_waves = 1024;
   int coop_w[3] = {1024, 1024, 1024};
+  // set when a fused (un)pooling launch's weight region would not fit its kernel's LDS cap
+  // (edge_coop_lds_cap): the schedule is rebuilt with the pooling / unpooling launches
+  int no_fuse = 0;
   std::vector<void*> owned;
   void drop_graphs() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
@@ -721,7 +724,7 @@ constexpr int kMaxFusedPoolBlocks = 256;  // one 4-wave workgroup (two tiles) pe
 // halo exchange sits between the two launches).  MSW_POOL_FUSE=0 keeps the pooling launch.
 bool pool_fusable(const msw_plan* P, int s, const Proc& pr) {
   const int on = getenv("MSW_POOL_FUSE") ? atoi(getenv("MSW_POOL_FUSE")) : 1;
-  if (!on || (P->NT != 2 && P->NT != 4) || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
+  if (!on || P->no_fuse || (P->NT != 2 && P->NT != 4) || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
   const ScaleCSR& g = P->sc[s];
   // K > 1: the launch is not the layer's last hop (k_edge_coop runs no unpool / decoder epilogue)
   if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s - 1].pool_slots || g.ntiles <= 0)
@@ -739,7 +742,8 @@ bool unpool_fusable(const msw_plan* P, int s, const Proc& pr, const Proc& up) {
   const int on = getenv("MSW_UNPOOL_FUSE") ? atoi(getenv("MSW_UNPOOL_FUSE")) : 1;
   // F = 64 only on request (=2): its 384-MFMA unpooling MLP per side outweighs the launch it
   // saves (zenodo4_f64 -2.5 %, profiles/r03/ab_unpool_fuse_f64.txt)
-  if (!on || !(P->NT == 2 || (P->NT == 4 && on == 2)) || P->part_rank >= 0 || s < 0 || s + 1 >= P->S) return false;
+  if (!on || P->no_fuse || !(P->NT == 2 || (P->NT == 4 && on == 2)) || P->part_rank >= 0 || s < 0 || s + 1 >= P->S)
+    return false;
   const ScaleCSR& g = P->sc[s];
   if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s].parent_slots || g.ntiles <= 0) return false;
   if (up.h1t > 2 * P->NT || up.K != 1) return false;
@@ -1238,6 +1242,19 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     }
   }
+}
+
+// The first cooperative edge hop whose staged weight region exceeds the dynamic LDS
+// prepare_kernels allowed its kernel (edge_coop_lds_cap), or nullptr.
+const Launch* lds_overflow(const msw_plan* P) {
+  for (const auto* q : {&P->sched_fwd, &P->sched_roll})
+    for (const Launch& L : *q) {
+      if (L.kind != L_EDGE_HOP || !(L.eh.coop == 2 || L.eh.coop == 4) || L.eh.wdirect) continue;
+      const int fuse = L.eh.pool.slots ? 1 : L.eh.pool.parent ? 2 : 0;
+      const int cap = P->NT == 4 ? edge_coop_lds_cap<4>(L.eh.coop, fuse) : edge_coop_lds_cap<2>(2, fuse);
+      if (eh_lds_bytes(L.eh.reg_nf) > (size_t)cap) return &L;
+    }
+  return nullptr;
 }
 
 template <int NT>
@@ -1884,24 +1901,35 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
         return rc;
 
   // ---- launch schedules (forward / rollout), per-launch weight regions, weight upload
-  sched_step(P.get(), P->sched_fwd, false);
-  sched_step(P.get(), P->sched_roll, true);
-  {
-    const bool mlp_only = P->NT > 2;  // F = 64: only the edge-MLP operands fit in LDS
-    if ((rc = relocate(P.get(), P->sched_fwd, mlp_only)) || (rc = relocate(P.get(), P->sched_roll, mlp_only)))
-      return rc;
-  }
-  P->blob.alloc(256);  // slack: LDS-DMA chunks may read up to 255 floats past a region
-  if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
-  for (auto* q : {&P->sched_fwd, &P->sched_roll})
-    for (Launch& L : *q) L.common().W = P->dW;
   switch (P->NT) {
     case 1: HIP_TRY(prepare_kernels<1>()); break;
     case 2: HIP_TRY(prepare_kernels<2>()); break;
     default: HIP_TRY(prepare_kernels<4>()); break;
   }
+  const size_t blob0 = P->blob.h.size();
+  for (;;) {
+    sched_step(P.get(), P->sched_fwd, false);
+    sched_step(P.get(), P->sched_roll, true);
+    const bool mlp_only = P->NT > 2;  // F = 64: only the edge-MLP operands fit in LDS
+    if ((rc = relocate(P.get(), P->sched_fwd, mlp_only)) || (rc = relocate(P.get(), P->sched_roll, mlp_only)))
+      return rc;
+    for (auto* q : {&P->sched_fwd, &P->sched_roll})
+      for (Launch& L : *q) set_grid_cap(P.get(), L);
+    // every cooperative edge hop's staged region must fit the LDS its kernel was given; a
+    // fused (un)pooling launch that does not (e.g. F = 32 with mlp_layers = 4: two edge MLPs
+    // + the projection) falls back to the separate pooling / unpooling launches
+    const Launch* bad = lds_overflow(P.get());
+    if (!bad) break;
+    if (P->no_fuse || !(bad->eh.pool.slots || bad->eh.pool.parent))
+      return fail(MSW_ERR_UNSUPPORTED, "weights of a cooperative edge hop exceed its LDS budget (" +
+                                           std::to_string(eh_lds_bytes(bad->eh.reg_nf)) + " B)");
+    P->no_fuse = 1;
+    P->blob.h.resize(blob0);  // drop the regions of the fused schedule
+  }
+  P->blob.alloc(256);  // slack: LDS-DMA chunks may read up to 255 floats past a region
+  if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
   for (auto* q : {&P->sched_fwd, &P->sched_roll})
-    for (Launch& L : *q) set_grid_cap(P.get(), L);
+    for (Launch& L : *q) L.common().W = P->dW;
 
   // ---- static per-edge features: edge encoder + edge part of each processor's layer 1
   if (P->E > 0) {

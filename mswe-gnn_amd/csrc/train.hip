@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "../../include/mswegnn.h"
 #include "engine.h"
@@ -30,6 +31,7 @@ namespace {
 
 using msw::set_error;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBM = 64, kBN = 64, kBK = 16, kGemmThreads = 256;
 constexpr int kMaxSplits = 256;
@@ -76,8 +78,12 @@ __device__ __forceinline__ float act_grad(int act, float x, float a) {
 // the MFMA fragments are read along m / n across lanes); each wave owns a 32 x 32 quarter as
 // 2 x 2 tiles of v_mfma_f32_16x16x4_f32 (A: lane l gives A(i = l & 15, k = l >> 4); B: lane l
 // gives B(k = l >> 4, j = l & 15); D: lane l holds D(4 (l >> 4) + r, l & 15)).  Split-K
-// (part != null): workgroup z sums K slice z into part[z][M][N]; k_sum_splits adds the slices
-// in order.
+// (part != null, the weight gradients dY^T X): F64 -- the fp32 operands multiplied on
+// v_mfma_f64_16x16x4_f64 (exact products, fp64 sums; D: lane l holds D((l >> 4) + 4 r, l & 15)),
+// workgroup z writes K slice z as doubles into part[z][M][N]; k_sum_splits adds the slices in
+// order in fp64.  A weight / bias gradient sums every edge or node of a layer, often with heavy
+// cancellation (a PReLU slope's gradient sums every element): fp64 accumulation leaves only the
+// final rounding, closer to exact arithmetic than torch's own fp32 reductions.
 struct GemmArgs {
   int M, N, K;
   const float* A; long lam, lak;
@@ -91,7 +97,9 @@ struct GemmArgs {
   int bones;                      // B(k, N - 1) = 1: an implicit ones column (bias gradient)
 };
 
+template <bool F64>
 __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
+  using acc_t = typename std::conditional<F64, f64x4, f32x4>::type;
   __shared__ float As[kBK][kBM + 4];
   __shared__ float Bs[kBK][kBN + 4];
   constexpr int UA = (kBM * kBK) / kGemmThreads, UB = (kBN * kBK) / kGemmThreads;
@@ -100,11 +108,11 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
   const int kb = a.part ? blockIdx.z * a.kchunk : 0;
   const int ke = a.part ? min(a.K, kb + a.kchunk) : a.K;
   const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
-  f32x4 acc[2][2];
+  acc_t acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
   const bool a_mfast = a.lam == 1 && a.lak != 1;  // A stored m-contiguous (transposed operand)
   const bool b_kfast = a.lbk == 1 && a.lbn != 1;  // B stored k-contiguous
   // per thread: its UA + UB tile elements (fixed positions), the next slice's values in
@@ -154,7 +162,12 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (F64)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)av[i], (double)bv[j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
     }
     __syncthreads();
   }
@@ -165,8 +178,13 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm + 16 * i + 4 * (lane >> 4) + r, n = n0 + wn + 16 * j + (lane & 15);
+        const int m = m0 + wm + 16 * i + (F64 ? (lane >> 4) + 4 * r : 4 * (lane >> 4) + r);
+        const int n = n0 + wn + 16 * j + (lane & 15);
         if (m >= a.M || n >= a.N) continue;
+        if constexpr (F64) {  // split-K weight gradients only
+          reinterpret_cast<double*>(a.part)[((long)blockIdx.z * a.M + m) * a.N + n] = acc[i][j][r];
+          continue;
+        } else {
         float v = acc[i][j][r];
         if (a.part) {
           a.part[((long)blockIdx.z * a.M + m) * a.N + n] = v;
@@ -176,40 +194,41 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs a) {
         if (a.bias) v = v + a.bias[n];
         if (a.pre) a.pre[(long)m * a.ldp + n] = v;
         a.C[(long)m * a.ldc + n] = act_fwd(a.act, v, sl);
+        }
       }
 }
 
-// out[i] = sum_{s < splits} part[s][i], i < count.  A 256-thread workgroup owns 64 outputs;
-// row group p (of 4) adds splits p, p + 4, ... in order, then the 4 partials are added in
-// order through LDS (fixed order: deterministic)
-__global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ part, int splits, long count,
+// out[i] = sum_{s < splits} part[s][i], i < count (fp64 partials, summed in fp64).  A
+// 256-thread workgroup owns 64 outputs; row group p (of 4) adds splits p, p + 4, ... in order,
+// then the 4 partials are added in order through LDS (fixed order: deterministic)
+__global__ __launch_bounds__(256) void k_sum_splits(const double* __restrict__ part, int splits, long count,
                                                     float* __restrict__ out) {
-  __shared__ float red[4][64];
+  __shared__ double red[4][64];
   const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
   for (long i0 = blockIdx.x * 64L; i0 < count; i0 += gridDim.x * 64L) {
     const long i = i0 + c;
-    float v = 0.f;
+    double v = 0.0;
     if (i < count) {
 #pragma unroll 8
       for (int s = p; s < splits; s += 4) v += part[(long)s * count + i];
     }
     red[p][c] = v;
     __syncthreads();
-    if (p == 0 && i < count) out[i] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    if (p == 0 && i < count) out[i] = (float)(((red[0][c] + red[1][c]) + red[2][c]) + red[3][c]);
     __syncthreads();
   }
 }
 
 // k_sum_splits over [M][N1] partials whose last column is the bias gradient: columns < N1 - 1
 // go to dW [M][N1 - 1], the last to db [M]
-__global__ __launch_bounds__(256) void k_sum_splits_wb(const float* __restrict__ part, int splits, int M, int N1,
+__global__ __launch_bounds__(256) void k_sum_splits_wb(const double* __restrict__ part, int splits, int M, int N1,
                                                        float* __restrict__ dW, float* __restrict__ db) {
-  __shared__ float red[4][64];
+  __shared__ double red[4][64];
   const int c = threadIdx.x & 63, p = threadIdx.x >> 6;
   const long count = (long)M * N1;
   for (long i0 = blockIdx.x * 64L; i0 < count; i0 += gridDim.x * 64L) {
     const long i = i0 + c;
-    float v = 0.f;
+    double v = 0.0;
     if (i < count) {
 #pragma unroll 8
       for (int s = p; s < splits; s += 4) v += part[(long)s * count + i];
@@ -217,7 +236,7 @@ __global__ __launch_bounds__(256) void k_sum_splits_wb(const float* __restrict__
     red[p][c] = v;
     __syncthreads();
     if (p == 0 && i < count) {
-      const float t = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+      const float t = (float)(((red[0][c] + red[1][c]) + red[2][c]) + red[3][c]);
       const long m = i / N1;
       const int n = (int)(i - m * N1);
       if (n < N1 - 1) dW[m * (N1 - 1) + n] = t;
@@ -375,17 +394,17 @@ __global__ void k_normalize_bwd(const float* __restrict__ s, const float* __rest
 }
 
 // dpre = dy * act'(pre); PReLU slope: per-block partial of sum(pre <= 0 ? pre * dy : 0)
-// (torch's prelu backward), written to spart[blockIdx.x]
+// (torch's prelu backward), fp64 products and sums, written to spart[blockIdx.x]
 __global__ __launch_bounds__(256) void k_act_bwd(const float* __restrict__ pre, const float* __restrict__ dy, long count,
                                                  int act, const float* __restrict__ slope, float* __restrict__ dpre,
-                                                 float* __restrict__ spart) {
-  __shared__ float red[256];
+                                                 double* __restrict__ spart) {
+  __shared__ double red[256];
   const float a = slope ? *slope : 0.f;
-  float sacc = 0.f;
+  double sacc = 0.0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
     const float x = pre[i], g = dy[i];
     dpre[i] = g * act_grad(act, x, a);
-    if (act == MSW_ACT_PRELU && !(x > 0.f)) sacc += x * g;
+    if (act == MSW_ACT_PRELU && !(x > 0.f)) sacc += (double)x * (double)g;
   }
   red[threadIdx.x] = sacc;
   __syncthreads();
@@ -396,24 +415,24 @@ __global__ __launch_bounds__(256) void k_act_bwd(const float* __restrict__ pre, 
   if (threadIdx.x == 0 && spart) spart[blockIdx.x] = red[0];
 }
 
-// column sums of X [R][W] over row slice blockIdx.x -> part[blockIdx.x][W]: thread t sums
-// column t % W over rows t / W, t / W + P, ... (P = 256 / W row lanes), then the P partials
-// are added in order through LDS (deterministic)
+// column sums of X [R][W] over row slice blockIdx.x -> part[blockIdx.x][W] (fp64): thread t
+// sums column t % W over rows t / W, t / W + P, ... (P = 256 / W row lanes), then the P
+// partials are added in order through LDS (deterministic)
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ X, long R, int W, long rchunk,
-                                                float* __restrict__ part) {
-  __shared__ float red[256];
+                                                double* __restrict__ part) {
+  __shared__ double red[256];
   const long r0 = blockIdx.x * rchunk, r1 = min(R, r0 + rchunk);
   for (int c0 = 0; c0 < W; c0 += 256) {
     const int wc = min(256, W - c0);
     const int P = 256 / wc;
     const int c = threadIdx.x % wc, rl = threadIdx.x / wc;
-    float v = 0.f;
+    double v = 0.0;
     if (rl < P)
       for (long r = r0 + rl; r < r1; r += P) v += X[r * W + c0 + c];
     red[threadIdx.x] = v;
     __syncthreads();
     if ((int)threadIdx.x < wc) {
-      float sacc = 0.f;
+      double sacc = 0.0;
       for (int p = 0; p < P; ++p) sacc += red[p * wc + threadIdx.x];
       part[(long)blockIdx.x * W + c0 + threadIdx.x] = sacc;
     }
@@ -499,6 +518,10 @@ inline int blocks_for(long n, int threads = 256) {
   return (int)std::max<long>(1, std::min<long>(b, 16384));
 }
 
+// split-K partial slices a weight gradient over R rows uses (weight_grad) -- also bounds the
+// column-sum slices of mlp_backward (ceil(R / max(256, R / kMaxSplits)) <= this)
+inline long splits_for(long R) { return std::min<long>(kMaxSplits, std::max<long>(1, R / (8 * kBK))); }
+
 struct Layout {  // float offsets into the saved / scratch buffers
   long X0, pre[4], post[4], s, nrm, outk, agg, nz, saved;
   long G0, G1, dagg, t, ds, dA, dB, part, spart, scratch;
@@ -537,7 +560,7 @@ bool layout_of(const msw_swegnn_train_desc* d, Layout& y) {
   y.ds = o; o += al(E * F);
   y.dA = o; o += al(E * y.wmax);
   y.dB = o; o += al(E * y.wmax);
-  y.part = o; o += al((long)kMaxSplits * y.wmax * (y.wmax + 1));
+  y.part = o; o += al(2L * splits_for(std::max(E, N)) * y.wmax * (y.wmax + 1));  // fp64 partials
   y.spart = o; o += al(kMaxSplits * 4L);
   y.scratch = o;
   return true;
@@ -579,7 +602,7 @@ bool mlp_layout_of(const msw_mlp_train_desc* d, MlpLayout& y) {
   o = 0;
   y.A = o; o += al(R * y.wmax);
   y.B = o; o += al(R * y.wmax);
-  y.part = o; o += al((long)kMaxSplits * y.wmax * (y.wmax + 1));
+  y.part = o; o += al(2L * splits_for(R) * y.wmax * (y.wmax + 1));  // fp64 partials
   y.spart = o; o += al(kMaxSplits * 4L);
   y.scratch = o;
   return true;
@@ -598,13 +621,16 @@ hipError_t gemm(const GemmArgs& a0, hipStream_t st, int splits = 1) {
     grid.z = (a.K + a.kchunk - 1) / a.kchunk;
     if (grid.z == 0) grid.z = 1;
   }
-  hipLaunchKernelGGL(k_gemm, grid, dim3(kGemmThreads), 0, st, a);
+  if (a.part)
+    hipLaunchKernelGGL(k_gemm<true>, grid, dim3(kGemmThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_gemm<false>, grid, dim3(kGemmThreads), 0, st, a);
   return hipGetLastError();
 }
 
 // dW [M][N] = sum_rows A(row, m) B(row, n): split-K over the rows, partials summed in order
 // db (nullable) [M] = sum_rows A(row, m): the same GEMM against an implicit ones column of B
-// (part: [splits][M][N + 1] floats then)
+// (part: [splits][M][N (+ 1)] doubles)
 hipError_t weight_grad(const float* A, int lda, const float* B, int ldb, long R, int M, int N, float* part,
                        float* dW, hipStream_t st, float* db = nullptr) {
   GemmArgs g{};
@@ -613,16 +639,17 @@ hipError_t weight_grad(const float* A, int lda, const float* B, int ldb, long R,
   g.B = B; g.lbk = ldb; g.lbn = 1;
   g.part = part;
   g.bones = db ? 1 : 0;
-  const int splits = (int)std::min<long>(kMaxSplits, std::max<long>(1, R / (8 * kBK)));
+  const int splits = (int)splits_for(R);
   hipError_t e = gemm(g, st, splits);
   if (e != hipSuccess) return e;
   const int kchunk = ((g.K + splits - 1) / splits + kBK - 1) / kBK * kBK;
   const int used = std::max(1, (g.K + kchunk - 1) / kchunk);
+  const double* p64 = reinterpret_cast<const double*>(part);
   if (db)
-    hipLaunchKernelGGL(k_sum_splits_wb, dim3(blocks_for((long)M * g.N, 64)), dim3(256), 0, st, part, used, M, g.N, dW,
+    hipLaunchKernelGGL(k_sum_splits_wb, dim3(blocks_for((long)M * g.N, 64)), dim3(256), 0, st, p64, used, M, g.N, dW,
                        db);
   else
-    hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N, 64)), dim3(256), 0, st, part, used, (long)M * N,
+    hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for((long)M * N, 64)), dim3(256), 0, st, p64, used, (long)M * N,
                        dW);
   return hipGetLastError();
 }
@@ -660,19 +687,21 @@ hipError_t mlp_backward(const MlpRun& m, const float* X, const float* const* pre
   const int nrs = (int)((R + rchunk - 1) / rchunk);
   const float* dcur = dY;
   float* dpre = bufB;
+  double* sp64 = reinterpret_cast<double*>(spart);
+  double* p64 = reinterpret_cast<double*>(part);
   for (int l = m.L - 1; l >= 0; --l) {
     const int wi = m.w[l], wo = m.w[l + 1];
     const int ab = blocks_for(R * wo) < kMaxSplits ? blocks_for(R * wo) : kMaxSplits;
-    hipLaunchKernelGGL(k_act_bwd, dim3(ab), dim3(256), 0, st, pre[l], dcur, R * wo, m.act[l], m.slope[l], dpre, spart);
+    hipLaunchKernelGGL(k_act_bwd, dim3(ab), dim3(256), 0, st, pre[l], dcur, R * wo, m.act[l], m.slope[l], dpre, sp64);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (dslope[l]) hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, st, spart, ab, 1L, dslope[l]);
+    if (dslope[l]) hipLaunchKernelGGL(k_sum_splits, dim3(1), dim3(256), 0, st, sp64, ab, 1L, dslope[l]);
     // the bias gradient rides on the weight-gradient GEMM as an extra ones column of X where
     // that column fits the last 64-wide output tile; else its own column sums
     const bool fuse_db = db[l] && dW[l] && wi % kBN != 0;
     if (db[l] && !fuse_db) {
-      hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, R, wo, rchunk, part);
-      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo, 64)), dim3(256), 0, st, part, nrs, (long)wo, db[l]);
+      hipLaunchKernelGGL(k_colsum, dim3(nrs), dim3(256), 0, st, dpre, R, wo, rchunk, p64);
+      hipLaunchKernelGGL(k_sum_splits, dim3(blocks_for(wo, 64)), dim3(256), 0, st, p64, nrs, (long)wo, db[l]);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const float* Xl = l == 0 ? X : post[l - 1];

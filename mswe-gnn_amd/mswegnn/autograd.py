@@ -23,20 +23,24 @@ the output mask stay elementwise torch ops.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from collections import OrderedDict
 
 import torch
 import torch.nn as nn
+from torch.autograd.function import once_differentiable
 
 from . import _lib as L
 from .engine import _act_code, _raw_stream
 
-__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported", "pool_apply", "pool_supported"]
+__all__ = ["swegnn_apply", "supported", "graph_csr", "mlp_apply", "mlp_supported", "pool_apply", "pool_supported",
+           "clear_caches"]
 
 _CSR_CACHE = OrderedDict()
 _CSR_KEEP = 32
-MLP_CALLS = [0]  # mlp_apply / pool_apply calls (tests check that the HIP path ran)
+MLP_CALLS = [0]  # mlp_apply / pool_apply / swegnn_apply calls (tests check that the HIP path ran)
 POOL_CALLS = [0]
+SWEGNN_CALLS = [0]
 
 
 class GraphCSR:
@@ -61,20 +65,40 @@ class GraphCSR:
         self.out_ptr, self.out_edge = csr(ei[0])
 
 
+def _drop_csr(key):
+    """Forget one cached GraphCSR and every descriptor template bound to it."""
+    ent = _CSR_CACHE.pop(key, None)
+    if ent is not None:
+        for k in [k for k, m in _META_CACHE.items() if getattr(m, "csr", None) is ent[1]]:
+            del _META_CACHE[k]
+
+
 def graph_csr(edge_index, num_nodes):
-    """Cached GraphCSR: keyed by the index tensor's address, layout and in-place version; the
-    cache holds the tensor itself, so its storage (and address) cannot be reused meanwhile."""
+    """Cached GraphCSR, keyed by the index tensor's address, layout and in-place version.  The
+    entry holds only a weak reference to the storage owner (the tensor, or the base of a
+    slice such as MSGNN's per-scale ``edge_index[:, a:b]``) and is dropped, with the
+    descriptors bound to it, when that owner is collected: a training loop over many batches
+    keeps no previous batch's graph (or its GPU CSR) alive."""
     key = (edge_index.data_ptr(), tuple(edge_index.shape), tuple(edge_index.stride()), edge_index._version,
            int(num_nodes), str(edge_index.device))
+    owner = edge_index._base if edge_index._base is not None else edge_index
     hit = _CSR_CACHE.get(key)
-    if hit is not None:
+    if hit is not None and hit[0]() is owner:
         _CSR_CACHE.move_to_end(key)
         return hit[1]
+    _drop_csr(key)
     g = GraphCSR(edge_index, num_nodes)
-    _CSR_CACHE[key] = (edge_index, g)
+    _CSR_CACHE[key] = (weakref.ref(owner), g)
+    weakref.finalize(owner, _drop_csr, key)
     while len(_CSR_CACHE) > _CSR_KEEP:
-        _CSR_CACHE.popitem(last=False)
+        _drop_csr(next(iter(_CSR_CACHE)))
     return g
+
+
+def clear_caches():
+    """Drop every cached CSR and descriptor template (their GPU arrays are freed)."""
+    _CSR_CACHE.clear()
+    _META_CACHE.clear()
 
 
 def _mlp_layers(seq):
@@ -103,10 +127,18 @@ def _mlp_layers(seq):
 
 
 def supported(layer, x_s, x_d, edge_attr):
-    """The HIP training path implements this layer call (else the torch path runs)."""
+    """The HIP training path implements this layer call (else the torch path runs): fp32 GPU
+    tensors, static and dynamic node features of one width F over the same rows (the kernels'
+    edge-MLP input is [x_s(row), x_s(col), x_d(row), x_d(col), e] = 4F + ef wide), no double
+    backward (the kernels' backward is not itself differentiable)."""
     if not (x_d.is_cuda and x_s.is_cuda) or x_d.dtype != torch.float32 or x_s.dtype != torch.float32:
         return False
+    if x_s.dim() != 2 or x_d.dim() != 2 or x_s.shape != x_d.shape:
+        return False
     if layer.K < 1 or layer.K > L.MAX_HOPS or _mlp_layers(layer.edge_mlp) is None:
+        return False
+    ef = int(layer.edge_features) if layer.edge_features > 0 else 0
+    if _mlp_layers(layer.edge_mlp)[0][0].in_features != 4 * x_d.shape[1] + ef:
         return False
     if layer.edge_features > 0 and (edge_attr is None or edge_attr.dtype != torch.float32):
         return False
@@ -221,6 +253,7 @@ class _SwegnnFunction(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gout):
         meta = ctx.meta
         x_s, x_d, ea, saved, *params = ctx.saved_tensors
@@ -270,6 +303,7 @@ def swegnn_apply(layer, x_s, x_d, edge_index, edge_attr=None):
                         lambda: _Meta(layer, _mlp_layers(layer.edge_mlp), csr, F, ef))
     if ef > 0 and edge_attr.dim() == 1:
         edge_attr = edge_attr.unsqueeze(1)
+    SWEGNN_CALLS[0] += 1
     return _SwegnnFunction.apply(meta, x_s, x_d, edge_attr if ef > 0 else None, *meta.params)
 
 
@@ -336,6 +370,7 @@ class _MlpFunction(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gout):
         meta = ctx.meta
         x, saved, *params = ctx.saved_tensors
@@ -389,6 +424,7 @@ class _PoolFunction(torch.autograd.Function):
         return out
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gout):
         csr = ctx.csr
         gout = gout.contiguous().to(torch.float32)

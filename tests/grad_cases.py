@@ -1,0 +1,169 @@
+"""Gradient cases of the reference-made fixtures (oracle/gen_golden_grad.py), runnable on any
+device and engine: the CPU tests run the drop-in's torch path, the GPU tests the HIP training
+kernels (mswegnn/autograd.py).  Each returns {name: tensor} in the fixture's key names.
+
+Reference: SWEGNN.forward models/gnn.py:387-445, MSGNN.forward :267-350,
+LightningTrainer.training_step training/train.py:125-145, loss_function training/loss.py:76-118.
+"""
+import numpy as np
+import torch
+
+from conftest import build_gnn, build_msgnn, golden, graph_digest, manifest, rel_err, weights
+
+import loss_ref  # oracle/: the reference's loss and training step, restated
+
+
+def grad_graph(name, T):
+    """A fixture graph regenerated from its mesh arguments (manifest 'grad_graphs')."""
+    from mswegnn.mesh import make_multiscale_mesh, make_single_scale_mesh, wet_state
+    kind, kw, wet = manifest()["grad_graphs"][name]
+    g = make_multiscale_mesh(**kw, T=T) if kind == "msgnn" else make_single_scale_mesh(**kw, T=T)
+    return wet_state(g, seed=wet)
+
+
+def processor_case(dev, train_engine="auto"):
+    """gnn_processor[0], [2] and intra_scale_gnn[2] of K4_F32: out, input and parameter
+    gradients of sum(out * wout)."""
+    fx = golden("fx_grad_processor_K4_F32")
+    g = grad_graph("tiny4", 4)
+    assert np.array_equal(graph_digest(g), fx["digest"])
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(dev)
+    x_s, x_d, ea, wout = (torch.from_numpy(fx[k]).to(dev) for k in ("x_s", "x_d", "edge_attr", "wout"))
+    ep, iep = g.edge_ptr, g.intra_edge_ptr
+    ei, iei = g.edge_index.to(dev), g.intra_mesh_edge_index.to(dev)
+    cases = {"proc0": (m.gnn_processor[0], ei[:, ep[0]:ep[1]], ea[ep[0]:ep[1]]),
+             "proc2": (m.gnn_processor[2], ei[:, ep[2]:ep[3]], ea[ep[2]:ep[3]]),
+             "intra2": (m.intra_scale_gnn[2], iei[:, iep[0]:iep[1]], None)}
+    out = {}
+    for name, (layer, e_idx, e) in cases.items():
+        layer.train_engine = train_engine
+        layer.zero_grad(set_to_none=True)
+        xs = x_s.clone().requires_grad_(True)
+        xd = x_d.clone().requires_grad_(True)
+        ee = e.clone().requires_grad_(True) if e is not None else None
+        y = layer(xs, xd, e_idx, ee)
+        (y * wout).sum().backward()
+        out[f"{name}__out"] = y.detach()
+        out[f"{name}__d_x_s"] = xs.grad
+        out[f"{name}__d_x_d"] = xd.grad
+        if ee is not None:
+            out[f"{name}__d_edge_attr"] = ee.grad
+        for n, p in layer.named_parameters():
+            out[f"{name}__g__{n}"] = p.grad
+        layer.train_engine = "auto"
+    return out, fx
+
+
+def msgnn_mse_case(dev, engine="auto"):
+    """MSGNN (K4_F32) with an MSE loss against the fixture's target: every parameter gradient."""
+    fx = golden("fx_grad_msgnn_K4_F32")
+    g = grad_graph("tiny4", 4)
+    assert np.array_equal(graph_digest(g), fx["digest"])
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(dev).train()
+    m.engine = engine
+    tgt = torch.from_numpy(fx["tgt"]).to(dev)
+    y = m(g.to(dev))
+    loss = ((y - tgt) ** 2).mean()
+    loss.backward()
+    out = {"y": y.detach(), "loss": loss.detach()}
+    out.update({"g__" + n: p.grad for n, p in m.named_parameters() if p.grad is not None})
+    return out, fx
+
+
+def training_batch(prefix_y, names, T, fx, dev, dtype=torch.float32):
+    """The fixture's PyG-style batch: members regenerated, targets y from the fixture, collated
+    (mswegnn.batch, PyG semantics) and adapted as training_step does (train.py:130)."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import adapt_batch_training
+    gs = []
+    for n in names:
+        g = grad_graph(n, T)
+        g.y = torch.from_numpy(fx[f"{prefix_y}y_{n}"])
+        gs.append(g)
+    b = collate(gs)
+    for k in ("x", "edge_attr", "BC", "y"):
+        setattr(b, k, getattr(b, k).to(dtype))
+    return adapt_batch_training(b.to(dev))
+
+
+def training_step_case(dev, sname, R, engine="auto", dtype=torch.float32, model=None):
+    """The reference's training_step (config.yaml trainer_options) on the fixture's batch
+    `sname` ('b1': one graph, 'b2': two) with R rollout steps -> (loss, gradients)."""
+    fx = golden("fx_grad_train_K4_F32")
+    names = manifest()["fx_grad_train_K4_F32_sets"][sname]
+    m = model if model is not None else build_msgnn(4, 32, 4, state=weights("K4_F32"))
+    m = m.to(dev).to(dtype).train()
+    m.engine = engine
+    m.zero_grad(set_to_none=True)
+    temp = training_batch(f"{sname}__", names, 5, fx, dev, dtype)
+    loss = loss_ref.training_step(m, temp, R)
+    loss.backward()
+    out = {"loss": loss.detach()}
+    out.update({"g__" + n: p.grad for n, p in m.named_parameters() if p.grad is not None})
+    return out, fx
+
+
+def gnn_training_step_case(dev, R, engine="auto"):
+    """training_step of the 1-scale GNN (config 1 model) on a batch of two graphs."""
+    fx = golden("fx_grad_train_gnn")
+    m = build_gnn(state=weights("gnn_F32_seed42")).to(dev).train()
+    m.engine = engine
+    m.zero_grad(set_to_none=True)
+    temp = training_batch("", ["g1_0", "g1_1"], 3, fx, dev)
+    loss = loss_ref.training_step(m, temp, R)
+    loss.backward()
+    out = {"loss": loss.detach()}
+    out.update({"g__" + n: p.grad for n, p in m.named_parameters() if p.grad is not None})
+    return out, fx
+
+
+def compare(ours, fx, prefix, keys=None):
+    """{key: rel err} of ours[key] against fx[prefix + key] (every gradient the fixture holds
+    under `prefix`, which must all be present in ours)."""
+    want = [k[len(prefix):] for k in fx if k.startswith(prefix)] if keys is None else keys
+    errs = {}
+    for k in want:
+        if not (k in ("out", "y", "loss") or k.startswith(("g__", "d_"))):
+            continue  # inputs, targets, digests
+        mine = ours.get(k, ours.get(prefix + k))
+        assert mine is not None, f"missing {prefix}{k}"
+        errs[k] = rel_err(mine, torch.from_numpy(np.asarray(fx[prefix + k])))
+    return errs
+
+
+def global_rel(ours, fx, prefix):
+    """Global relative L2 difference over every parameter gradient ('g__*')."""
+    num = den = 0.0
+    for k in fx:
+        if k.startswith(prefix + "g__"):
+            ref = torch.from_numpy(fx[k]).double()
+            a = ours[k[len(prefix):]].detach().double().cpu()
+            num += float(((a - ref) ** 2).sum())
+            den += float((ref ** 2).sum())
+    return (num / den) ** 0.5
+
+
+def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0):
+    """The gradient bar: every tensor within `tol` (relative: max|ours - ref| / max|ref|) of
+    the reference's fp32 result, or -- for a tensor the fp32 reference itself does not
+    resolve to `tol` (a PReLU slope's gradient sums every element of its layer; a mask flip
+    of _mask_small_WD forks a rollout) -- no further from the reference's float64 result than
+    `slack` x the fp32 reference is.  Returns (worst error vs fp32, {tensor: (ours vs fp64,
+    fp32 ref vs fp64)} for the tensors that took the fp64 rule); asserts."""
+    errs = compare(ours, fx, prefix)
+    worst = max(errs.values())
+    rule64, bad = {}, {}
+    for k, e in errs.items():
+        if e <= tol:
+            continue
+        if fp64_prefix is None or (fp64_prefix + k) not in fx:
+            bad[k] = e
+            continue
+        ref64 = torch.from_numpy(fx[fp64_prefix + k])
+        e_o = rel_err(ours.get(k, ours.get(prefix + k)), ref64)
+        e_r = rel_err(torch.from_numpy(fx[prefix + k]), ref64)
+        rule64[k] = (e_o, e_r)
+        if not e_o <= max(tol, slack * e_r):
+            bad[k] = (e, e_o, e_r)
+    assert not bad, (prefix, bad)
+    return worst, rule64

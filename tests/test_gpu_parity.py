@@ -258,11 +258,14 @@ def test_hid64_random_init_vs_oracle(cuda):
 
 
 def test_variants_vs_oracle(cuda):
-    """Less common constructor options: mlp_layers=2, K per scale, no filter matrix,
+    """Less common constructor options: mlp_layers=2 / 4, K per scale, no filter matrix,
     learned_residuals='all' / False, gnn_activation='prelu', K=1 GNN with 3 layers."""
     g = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=3, T=3), seed=7)
     cases = [
         dict(mlp_layers=2, K=[2, 3, 1]),
+        # F = 32, 4-layer MLPs: the fused unpooling launch's region (two edge MLPs + the
+        # projection) exceeds the cooperative kernel's LDS cap -> separate (un)pooling launches
+        dict(mlp_layers=4, K=3),
         dict(with_filter_matrix=False, learned_residuals="all"),
         dict(gnn_activation="prelu", learned_residuals=False, skip_connections=False),
     ]

@@ -264,3 +264,113 @@ def test_batched_training_step_gradients(cuda):
     assert ag.MLP_CALLS[0] > calls
     print(f"batched MSGNN training step vs float64: 1 step worst tensor {worst:.2e}; "
           f"2 steps global {g_o:.2e} (torch fp32 {g_t:.2e})")
+
+
+# ---------------------------------------------------------------- against the reference's own gradients
+# (tests/golden/fx_grad_*: oracle/gen_golden_grad.py ran the reference's SWEGNN / MSGNN /
+# LightningTrainer.training_step; tests/grad_cases.py regenerates the inputs)
+
+def test_hip_processor_gradients_vs_reference_fixture(cuda):
+    """gnn_processor[0] / [2] and intra_scale_gnn[2] on the HIP training kernels against the
+    reference's own output and gradients (1e-4 per tensor)."""
+    import grad_cases as gc
+    from mswegnn import autograd as ag
+    n0 = ag.SWEGNN_CALLS[0]
+    ours, fx = gc.processor_case(cuda)
+    assert ag.SWEGNN_CALLS[0] == n0 + 3  # the three layers ran on the HIP training kernels
+    for case in ("proc0", "proc2", "intra2"):
+        worst, _ = gc.check(ours, fx, case + "__", TOL)
+        print(f"HIP {case}: worst rel err vs reference {worst:.2e}")
+
+
+def test_hip_msgnn_gradients_vs_reference_fixture(cuda):
+    import grad_cases as gc
+    from mswegnn import autograd as ag
+    calls = ag.MLP_CALLS[0], ag.POOL_CALLS[0]
+    ours, fx = gc.msgnn_mse_case(cuda)
+    assert ag.MLP_CALLS[0] > calls[0] and ag.POOL_CALLS[0] > calls[1]
+    worst, rule64 = gc.check(ours, fx, "", TOL, "fp64__")
+    print(f"HIP MSGNN MSE: worst {worst:.2e}; fp64 rule for {rule64}")
+
+
+@pytest.mark.parametrize("sname,R", [("b1", 1), ("b1", 4), ("b2", 1), ("b2", 4)])
+def test_hip_training_step_vs_reference_fixture(cuda, sname, R):
+    """The reference's training_step (config.yaml trainer_options; one- and two-graph batches,
+    1 and 4 rollout steps) with every layer on the HIP training kernels: loss and every
+    parameter gradient against the reference's (1e-4 per tensor, else the fp64 rule)."""
+    import grad_cases as gc
+    from mswegnn import autograd as ag
+    calls = ag.MLP_CALLS[0]
+    ours, fx = gc.training_step_case(cuda, sname, R)
+    assert ag.MLP_CALLS[0] > calls
+    pre = f"{sname}_R{R}__"
+    worst, rule64 = gc.check(ours, fx, pre, TOL, f"{sname}_R{R}_fp64__")
+    print(f"HIP training_step {sname} R={R}: loss {float(ours['loss']):.7e} (reference "
+          f"{float(fx[pre + 'loss']):.7e}), worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; "
+          f"fp64 rule for {rule64}")
+
+
+@pytest.mark.parametrize("R", [1, 2])
+def test_hip_gnn_training_step_vs_reference_fixture(cuda, R):
+    import grad_cases as gc
+    ours, fx = gc.gnn_training_step_case(cuda, R)
+    worst, _ = gc.check(ours, fx, f"R{R}__", TOL)
+    print(f"HIP GNN training_step R={R}: worst {worst:.2e}")
+
+
+@pytest.mark.parametrize("sname,R", [("b2", 1), ("b2", 4)])
+def test_hip_training_step_under_autocast_fp16(cuda, sname, R):
+    """main.py trains with precision='16-mixed' (main.py:106-110: torch.autocast fp16 + a
+    gradient scaler).  Under autocast the HIP training kernels still run -- and compute in
+    fp32 -- while the torch ops between them follow autocast (the residual matmul in fp16, as
+    in the reference).  Both the HIP path and torch's own AMP path are bounded against the
+    reference's float64 gradients: HIP within the fp32 bar (1e-4 global / the fp64 rule per
+    tensor), torch-AMP within fp16 accuracy (reported, loose bound)."""
+    import grad_cases as gc
+    from mswegnn import autograd as ag
+    fx = gc.golden("fx_grad_train_K4_F32")
+    p64 = f"{sname}_R{R}_fp64__"
+    res = {}
+    for engine in ("auto", "torch"):
+        calls = ag.MLP_CALLS[0], ag.POOL_CALLS[0]
+        with torch.autocast("cuda", dtype=torch.float16):
+            ours, _ = gc.training_step_case(cuda, sname, R, engine=engine)
+        if engine == "auto":
+            assert ag.MLP_CALLS[0] > calls[0] and ag.POOL_CALLS[0] > calls[1], "HIP kernels did not run"
+        else:
+            assert ag.MLP_CALLS[0] == calls[0]
+        res[engine] = gc.global_rel(ours, fx, p64), ours
+    g_hip, g_amp = res["auto"][0], res["torch"][0]
+    g_ref = gc.global_rel({k[len(f'{sname}_R{R}__'):]: torch.from_numpy(v) for k, v in fx.items()
+                           if k.startswith(f"{sname}_R{R}__g__")}, fx, p64)
+    print(f"autocast fp16 {sname} R={R}: global rel vs fp64 -- HIP {g_hip:.2e}, torch AMP {g_amp:.2e}, "
+          f"reference fp32 {g_ref:.2e}")
+    assert g_hip <= max(TOL, 3 * g_ref) or g_hip <= 0.1 * g_amp, (g_hip, g_amp, g_ref)
+    assert g_amp <= 5e-2, g_amp
+
+
+def test_autograd_caches_follow_graph_lifetime_and_guards(cuda):
+    """the CSR / descriptor caches drop a graph's entries when its edge_index is
+    collected; mismatched x_s / x_d widths take the torch path; the kernels' backward is not
+    differentiable twice (once_differentiable raises instead of dropping terms)."""
+    import gc as pygc
+    from mswegnn import autograd as ag
+    ag.clear_caches()
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=4), seed=1).to(cuda)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda).train()
+    ((m(g) ** 2).mean()).backward()
+    assert len(ag._CSR_CACHE) > 0 and len(ag._META_CACHE) > 0
+    del g
+    pygc.collect()
+    assert len(ag._CSR_CACHE) == 0
+    assert not any(hasattr(v, "csr") for v in ag._META_CACHE.values())
+    layer = m.gnn_processor[0]
+    x = torch.randn(50, 32, device=cuda)
+    assert not ag.supported(layer, torch.randn(50, 16, device=cuda), x, None)
+    assert ag.supported(layer, x, x, torch.randn(10, 32, device=cuda))
+    ei = torch.randint(0, 50, (2, 120), device=cuda)
+    xs = x.clone().requires_grad_(True)
+    out = layer(xs, x, ei, torch.randn(120, 32, device=cuda))
+    (gx,) = torch.autograd.grad(out.sum(), xs, create_graph=True)
+    with pytest.raises(RuntimeError):
+        gx.sum().backward()

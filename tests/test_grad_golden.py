@@ -1,0 +1,82 @@
+"""Training-path gradients of the drop-in (CPU, torch autograd) against gradients the REFERENCE
+computed itself (oracle/gen_golden_grad.py: its SWEGNN / MSGNN modules, its
+LightningTrainer.training_step and loss_function with config.yaml's trainer_options).
+
+The drop-in's torch path is not bit-identical to the reference's: it computes s_ij once per
+SWEGNN layer and masks the inactive edges per hop (models/gnn.py of this package), where the
+reference recomputes the edge MLP on each hop's active edges (models/gnn.py:406-426) -- the
+same values, but the weight gradients are accumulated in another order.  The bar is 1e-5
+relative per tensor, or, for a tensor the reference's own fp32 result does not resolve to 1e-5
+(PReLU slope gradients sum every element of their layer), the fp64 rule of
+grad_cases.check against the reference run in float64.  The GPU counterpart (HIP training
+kernels, 1e-4) is tests/test_gpu_train.py.
+"""
+import pytest
+import torch
+
+import grad_cases as gc
+import loss_ref
+
+CPU = torch.device("cpu")
+TOL = 1e-5
+
+
+def test_processor_gradients_vs_reference():
+    """gnn_processor[0] / [2] and intra_scale_gnn[2] (K4_F32, partly dry tiny mesh): output,
+    d x_s, d x_d, d edge_attr and every parameter gradient."""
+    ours, fx = gc.processor_case(CPU)
+    for case in ("proc0", "proc2", "intra2"):
+        worst, _ = gc.check(ours, fx, case + "__", TOL)
+        print(f"{case}: worst rel err {worst:.2e}")
+
+
+def test_msgnn_mse_gradients_vs_reference():
+    ours, fx = gc.msgnn_mse_case(CPU)
+    worst, rule64 = gc.check(ours, fx, "", TOL, "fp64__")
+    print(f"MSGNN MSE: worst {worst:.2e}; fp64 rule for {rule64}")
+
+
+@pytest.mark.parametrize("sname,R", [("b1", 1), ("b1", 4), ("b2", 1), ("b2", 4)])
+def test_training_step_gradients_vs_reference(sname, R):
+    """The reference's training_step (curriculum rollout of R steps, per-step RMSE on the finest
+    scale's wet rows, velocity_scaler 7) on a one-graph and a two-graph batch: the loss and
+    every parameter gradient."""
+    ours, fx = gc.training_step_case(CPU, sname, R)
+    pre = f"{sname}_R{R}__"
+    assert abs(float(ours["loss"]) - float(fx[pre + "loss"])) <= 1e-6 * abs(float(fx[pre + "loss"]))
+    worst, rule64 = gc.check(ours, fx, pre, TOL, f"{sname}_R{R}_fp64__")
+    print(f"training_step {sname} R={R}: worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; "
+          f"fp64 rule for {rule64}")
+
+
+@pytest.mark.parametrize("R", [1, 2])
+def test_gnn_training_step_gradients_vs_reference(R):
+    ours, fx = gc.gnn_training_step_case(CPU, R)
+    worst, _ = gc.check(ours, fx, f"R{R}__", TOL)
+    print(f"GNN training_step R={R}: worst {worst:.2e}")
+
+
+def test_loss_restatement_branches():
+    """oracle/loss_ref.py's loss_function against hand-computed values of each branch of
+    training/loss.py:76-118 (multiscale single graph / batch, only_where_water, MAE, velocity
+    scaler) -- its training-step use is pinned by the fixtures above."""
+    from mswegnn.mesh import Graph
+    preds = torch.tensor([[1.0, 2.0], [0.0, 0.0], [3.0, 1.0], [5.0, 5.0]])
+    real = torch.tensor([[0.0, 0.0], [0.0, 0.0], [1.0, 1.0], [0.0, 0.0]])
+    single = Graph(node_ptr=torch.tensor([0, 3, 4]))
+    # finest rows 0..2, wet rows (diff != 0) 0 and 2: diffs [1, 2], [2, 0]
+    rm = torch.sqrt(torch.tensor([(1 + 4) / 2, (4 + 0) / 2]))
+    want = (rm[0] + 7 * rm[1]) / 8
+    got = loss_ref.loss_function(preds, real, single, "RMSE", only_where_water=True, velocity_scaler=7)
+    assert torch.allclose(got, want)
+    batch = Graph(node_ptr=torch.tensor([[0, 1, 2], [2, 3, 4]]))  # finest rows 0 and 2
+    mae = torch.tensor([(1 + 2) / 2, (2 + 0) / 2])
+    got = loss_ref.loss_function(preds, real, batch, "MAE", only_where_water=False, velocity_scaler=1)
+    assert torch.allclose(got, mae.mean())
+    flat = Graph()
+    d = (preds - real)[[0, 2, 3]]
+    want = torch.sqrt((d ** 2).mean(0))
+    got = loss_ref.loss_function(preds, real, flat, "RMSE", only_where_water=True, velocity_scaler=1)
+    assert torch.allclose(got, want.mean())
+    with pytest.raises(NotImplementedError):
+        loss_ref.loss_function(preds, real, flat, conservation=1)

@@ -7,6 +7,7 @@ import ctypes as C
 import os
 import re
 import socket
+import time
 import sys
 
 import numpy as np
@@ -90,7 +91,9 @@ def test_training_abi_validation_and_workspace_without_gpu(libso):
     assert lib.msw_mlp_train_workspace(C.byref(d), C.byref(s), C.byref(t)) == 0
     al = lambda n: (n + 63) // 64 * 64  # noqa: E731
     assert s.value == al(100 * 32) + al(100 * 32) + al(100 * 2) + al(100 * 32) + al(100 * 32)
-    assert t.value == 2 * al(100 * 32) + al(256 * 32 * 33) + al(256 * 4)
+    # scratch: two [rows][max width] buffers, fp64 split-K partials (splits = max(1, rows / 128)
+    # slices of [max width][max width + 1] doubles), fp64 slope partials
+    assert t.value == 2 * al(100 * 32) + al(2 * 1 * 32 * 33) + al(256 * 4)
     assert lib.msw_mlp_train_forward(C.byref(d), None, None, None, None) != 0
     assert b"null" in lib.msw_last_error()
     d.width[3] = 0
@@ -731,3 +734,56 @@ def test_flip_localisation_rules():
     r64v = r64.clone()
     r64v[7, :, 3] = torch.tensor([0.0, 0.011], dtype=torch.float64)
     assert flip_localisation(r64v, ref, r64v) == (3, [7])
+
+
+def _extras_main(rank, world, port, q, budget):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    torch.set_num_threads(2)
+    import argparse
+    import json as _json
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    args = argparse.Namespace(extras_budget=budget, strong_sets="3,40", strong_steps=1, T=2,
+                              no_partition_check=False, no_partition_large=False)
+    t0 = time.perf_counter()
+    rec = bench.run_extras(dist, rank, world, torch.device("cpu"), args, dist.barrier, "gloo", engine="torch",
+                           workload="tiny_mixed", gpus=0)
+    if rank == 0:
+        q.put((_json.dumps(rec), time.perf_counter() - t0))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("budget", [1.0, 600.0])
+def test_extras_budget_two_ranks_gloo(budget):
+    """bench.py's N > 1 records after the timed region run inside ONE budget (verdict r3 item 3):
+    with 1 s every section is recorded as skipped and the call returns at once; with room, the
+    small strong-scaling set runs (both ranks agree on every branch), the large one (G = 40,
+    est. 26 s) is skipped for budget only when it does not fit, and the RCCL sections say why
+    they are absent (gloo, no GPUs).  Every section carries wall_s; the record is JSON."""
+    import json as _json
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_extras_main, args=(r, 2, port, q, budget)) for r in range(2)]
+    for p in procs:
+        p.start()
+    line, wall = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rec = _json.loads(line)
+    order = [o["section"] for o in rec["extras"]["order"]]
+    assert order == ["strong_G3", "zenodo4_2_parts", "ddp", "strong_G40", "hbm1m_parts"]
+    sets = {e["G"]: e for e in rec["strong_scaling"]["sets"]}
+    assert all("wall_s" in e for e in sets.values())
+    assert "skipped" in rec["ddp_training_rccl"] and "wall_s" in rec["ddp_training_rccl"]
+    assert "skipped" in rec["partitioned_rollout_rccl"]["zenodo4_2_parts"]
+    if budget < 2:
+        assert all(e.get("skipped") == "budget" for e in sets.values())
+        assert wall < 30
+    else:
+        assert "t1_ms" in sets[3] and "speedup" in sets[3] and sets[3]["gathered_vs_single_gpu_max_rel"] <= 1e-5
+        assert "skipped" not in sets[40] or sets[40]["skipped"] == "budget"

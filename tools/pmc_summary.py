@@ -17,6 +17,20 @@ import sys
 from collections import defaultdict
 
 
+def library_sha256():
+    """sha256 of the engine library the profiled command loaded (bench.py compares it with the
+    library it loads: roofline.rocprof / traffic_source .stale)."""
+    import hashlib
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mswe-gnn_amd", "lib",
+                        "libmswegnn.so")
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def load(d, counter):
     files = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
     acc = defaultdict(list)
@@ -43,7 +57,7 @@ def main():
             "write_bytes_per_launch": wb,
             "hbm_bytes_per_launch": (rd or 0) + (wb or 0) if (rd is not None or wb is not None) else None}
     hops = [(k, v) for k, v in table.items() if k.startswith("k_hop")]
-    res = {"note": __doc__.strip().splitlines()[2], "kernels": table}
+    res = {"note": __doc__.strip().splitlines()[2], "library_sha256": library_sha256(), "kernels": table}
     if hops:
         k, v = max(hops, key=lambda kv: kv[1]["dispatches"])
         res["k_hop"] = dict(v, kernel=k)

@@ -17,6 +17,20 @@ import sys
 ROLES = ["hop", "edge_hop", "pool", "hop_large", "edge_hop_large"]
 
 
+def library_sha256():
+    """sha256 of the engine library the profiled command loaded (bench.py compares it with the
+    library it loads: roofline.rocprof / traffic_source .stale)."""
+    import hashlib
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mswe-gnn_amd", "lib",
+                        "libmswegnn.so")
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def runs_of(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     runs, i = [], 0
@@ -48,7 +62,7 @@ def main(argv):
         out = argv[argv.index("--json") + 1]
         ours = [r for r in runs if r["kernel"].startswith("k_")]  # engine kernels only
         with open(out, "w") as f:
-            json.dump({"source": path, "runs": runs,
+            json.dump({"source": path, "library_sha256": library_sha256(), "runs": runs,
                        "by_role": {ROLES[i]: r for i, r in enumerate(ours[:len(ROLES)])}}, f, indent=1)
 
 

@@ -5,7 +5,7 @@ AdamW step, with every SWEGNN layer on the HIP training kernels (mswegnn/autogra
 the all-torch autograd path of the same drop-in model on the same GPU.  Also reports the loss
 and gradient agreement of the two paths at the first step.
 
-    python tools/train_bench.py [--workload zenodo4] [--rollout-steps 4] [--steps 5]
+    python tools/train_bench.py [--workload zenodo4] [--rollout-steps 4] [--steps 5] [--amp] [--fp64-ref]
 """
 import argparse
 import json
@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--only", choices=["hip", "torch"], default=None)
     ap.add_argument("--fp64-ref", action="store_true",
                     help="also the first-step gradients of the torch path in float64 (the yardstick)")
+    ap.add_argument("--amp", action="store_true",
+                    help="also both paths under main.py's precision='16-mixed' (autocast fp16 + GradScaler)")
     ap.add_argument("--parts", default="swegnn,mlp,pool",
                     help="diagnostics: which layer kinds run on the HIP training kernels")
     a = ap.parse_args()
@@ -62,40 +64,49 @@ def main():
         y = (m0.rollout(g, R) * 1.1 + 0.01).detach()
     state0 = {k: v.detach().clone() for k, v in m0.state_dict().items()}
 
-    def run(engine):
+    def run(engine, amp=False):
+        """Training steps of one path; amp: main.py's precision='16-mixed' (autocast fp16 around
+        the forward + loss, GradScaler, unscale before clipping -- Lightning's order)."""
         from models.gnn import MSGNN  # noqa: F401
         m = m0
         m.load_state_dict(state0)
         m.train()
         m.engine = engine
         opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=0.0)
+        scaler = torch.amp.GradScaler("cuda", enabled=amp)
         dyn = m.previous_t * m.NUM_WATER_VARS
 
         def step():
             opt.zero_grad(set_to_none=True)
             temp = g.clone()
             losses = []
-            for i in range(R):
-                temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, i], temp.node_BC,
-                                                            type_BC=temp.type_BC)
-                preds = m(temp)
-                temp.x = use_prediction(temp.x, preds, m.previous_t)
-                losses.append(rmse_loss(preds, y[:, :, i], n0))
-            loss = torch.stack(losses).mean()
-            loss.backward()
+            with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
+                for i in range(R):
+                    temp.x[:, -dyn:] = apply_boundary_condition(temp.x[:, -dyn:], temp.BC[:, :, i], temp.node_BC,
+                                                                type_BC=temp.type_BC)
+                    preds = m(temp)
+                    temp.x = use_prediction(temp.x, preds, m.previous_t)
+                    losses.append(rmse_loss(preds, y[:, :, i], n0))
+                loss = torch.stack(losses).mean()
+            scaler.scale(loss).backward()
+            scaler.unscale_(opt)
             torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
             return loss
+
+        def opt_step():
+            scaler.step(opt)
+            scaler.update()
         first = step()
         grads = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
-        opt.step()
+        opt_step()
         for _ in range(a.warmup):
             step()
-            opt.step()
+            opt_step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
-            opt.step()
+            opt_step()
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / max(a.steps, 1), float(first.detach()), grads
     if a.only:
@@ -140,6 +151,19 @@ def main():
         fp64 = {"hip_vs_fp64_global_rel": global_rel(g_hip, g64s), "torch_vs_fp64_global_rel": global_rel(g_torch, g64s),
                 "hip_vs_fp64_worst_tensor_rel": max(per_tensor(g_hip, g64s).values()),
                 "torch_vs_fp64_worst_tensor_rel": max(per_tensor(g_torch, g64s).values())}
+    # main.py's training configuration: precision='16-mixed' (autocast fp16 + GradScaler).  The
+    # HIP training kernels run under autocast in fp32; torch's own AMP path is the reference's
+    amp = None
+    if a.amp:
+        t_hip_amp, _, g_hip_amp = run("auto", amp=True)
+        t_torch_amp, _, g_torch_amp = run("torch", amp=True)
+        amp = {"hip_ms_per_training_step": t_hip_amp * 1e3, "torch_amp_ms_per_training_step": t_torch_amp * 1e3,
+               "speedup_vs_torch_amp": t_torch_amp / t_hip_amp,
+               "hip_amp_vs_hip_fp32_global_rel": global_rel(g_hip_amp, g_hip),
+               "torch_amp_vs_torch_fp32_global_rel": global_rel(g_torch_amp, g_torch)}
+        if fp64 is not None:
+            amp["hip_amp_vs_fp64_global_rel"] = global_rel(g_hip_amp, g64s)
+            amp["torch_amp_vs_fp64_global_rel"] = global_rel(g_torch_amp, g64s)
     pt = per_tensor(g_hip, g_torch)
     worst_k = max(pt, key=pt.get)
     print(json.dumps({"workload": a.workload, "fine_nodes": n0, "all_nodes": desc["all_nodes"],
@@ -156,6 +180,7 @@ def main():
                           "torch_vs_torch_worst_tensor_rel": max(per_tensor(g_torch2, g_torch).values()),
                           "hip_vs_hip_max_abs": max((g_hip2[k] - g_hip[k]).abs().max().item() for k in g_hip),
                           "fp64": fp64},
+                      "amp_16_mixed": amp,
                       "note": "SWEGNN layers (7 processors + 3 unpooling), encoders, decoder and mean pooling on "
                               "HIP training kernels; scale selections, loss, clipping, AdamW: torch on the same "
                               "GPU. Gradients after clip_grad_norm_(1.0) of the first training step."}),
