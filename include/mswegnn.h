@@ -223,8 +223,7 @@ int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
  *   kernel: 0 = middle hop (first processor on `scale`), 1 = fused edge MLP + hop 1
  *           (same processor), 2 = mean pooling + projection into `scale` (scale >= 1),
  *           3 = node encoders (+ projection of processor 0), 4 = unpooling layer into
- *           `scale` (scale < S-1) with its projection epilogue, 5 = hop pair (two middle
- *           hops in one launch; processors with K >= 4).
+ *           `scale` (scale < S-1) with its projection epilogue.
  * units_out (optional) receives {rows, edges} processed by ONE launch. */
 int msw_bench_kernel(msw_plan* plan, int32_t kernel, int32_t scale, int32_t iters,
                      int64_t* units_out, void* stream);

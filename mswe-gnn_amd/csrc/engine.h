@@ -256,52 +256,6 @@ struct HopArgs {
   const int2* redge; // [E] {internal source row, tile-padded s slot}, reference edge order
 };
 
-// Hop chain: M = 2 or 3 consecutive hops (k .. k+M-1) in one launch, the last of them
-// optionally the layer's last hop (its epilogue runs on the workgroup's own rows).
-// Workgroup b owns the nodes A of its kWaves edge tiles.  Sets D_{M-1} = A + in-neighbours
-// of A, D_{l-1} = D_l + in-neighbours of D_l (each set a prefix of the next: one index per
-// node in the workgroup).  Level l = 1 .. M-1 computes out_{k+l} on D_l (level 1 gathers
-// out_k from HBM, level l > 1 reads level l-1 from LDS), recomputing the halo redundantly
-// in every workgroup that needs it -- same arithmetic, same order as k_hop.  The final
-// level computes out_{k+M} on A from LDS.  Saves M-1 launches (dispatch + drain + cold
-// gathers) at the price of the halo recomputation; used where a launch is latency-bound.
-struct PairRec {  // level lane record (32 B)
-  int src;        // level 1: internal source row (out_k, HBM); level > 1: source's set index;
-                  // -1 = no edge in this slot
-  int p;          // tile-padded s slot of the edge
-  int dl;         // destination lane
-  int n;          // level 1: internal destination row; level > 1: its set index; -1 = no node
-  int bl;         // destination's set index (row of the level's LDS buffer)
-  int q;          // q0 | q1 << 8
-  int pad0, pad1;
-};
-constexpr int kChainMax = 3;
-template <int NT> constexpr int chain_waves() { return 8; }  // 2 per SIMD: 256 VGPRs each
-struct HopMArgs {
-  Common c;
-  WReg reg;                         // last: epilogue operands (LDS region at dynamic offset 0)
-  int wfloats;                      // LDS floats of that region (1-KB chunks); buffers follow
-  int max_blocks;
-  int n0;
-  const LaneRec* recs; int ntiles;  // final level = the layer's edge tiles
-  const int2* lf;                   // [ntiles][16] {source, destination} set indices
-  int nblocks;                      // ceil(ntiles / kWaves)
-  int m;                            // hops in the launch (2 or 3)
-  int lv_base[kChainMax - 1];       // level l tiles start at lv_base[l-1]: [nblocks][lv_tiles[l-1]]
-  int lv_tiles[kChainMax - 1];      // tiles per workgroup of level l (padded with empty tiles)
-  const PairRec* lv;                // [level tiles][16], every level
-  const int* a0;                    // [nblocks] local index of the workgroup's first A node
-  int bmax;                         // rows of the largest set D_1 (one LDS buffer)
-  const float* s;
-  const float* xs;
-  const float* in;                  // out_k
-  float* out;                       // out_{k+M} (last: may be null, the epilogue consumes it)
-  int filt[kChainMax];              // blob offsets of the filters of hops k .. k+M-1 (-1: none)
-  int grad, upwind;
-  int last;
-  Epilogue epi;
-};
-
 // Mean pooling into the coarse rows + projection of the next processor.
 
 struct PoolArgs {
@@ -393,15 +347,14 @@ hipError_t launch_copy_rows(const float* src, const int* srows, float* dst, cons
 
 // NT = F / 16 feature tiles (F = 16, 32, 64 -> NT = 1, 2, 4)
 template <int NT> hipError_t prepare_kernels();
-// kind 0 encode, 1 edge_hop, 2 hop, 3 pool, 4 hop chain (last: 0/1, loop = M), 5 pool edge
-// tiles, 6 row epilogue
+// kind 0 encode, 1 edge_hop, 2 hop, 3 pool, 5 pool edge tiles, 6 row epilogue (and the
+// cooperative / split / row-layout variants, kernels_impl.h kernel_of)
 template <int NT> int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop);
 template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
-template <int NT> hipError_t launch_hopm(const HopMArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_epi(const EpiArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);
 

@@ -930,19 +930,6 @@ void k_edge_hop(EdgeHopArgs a) {
       __syncthreads();
       Wm = smem;
     }
-#if defined(MSW_EH_PRIO) || defined(MSW_EH_STAGGER)
-    // A/B (build variants): break the lockstep of the SIMD's co-resident waves, which run the
-    // same gather -> MFMA chain program -- static priority for the younger half, or a delayed
-    // start of the younger half
-    if (w >= WV / 2) {
-#ifdef MSW_EH_PRIO
-      __builtin_amdgcn_s_setprio(MSW_EH_PRIO);
-#endif
-#ifdef MSW_EH_STAGGER
-      for (int i = 0; i < MSW_EH_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
-    }
-#endif
     for (; tile < a.ntiles; tile += stride) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       EdgeHopRows<NT> q;
@@ -1625,10 +1612,12 @@ __device__ __forceinline__ void pool_project_part(float* dst_row, const f32x4 (&
 // still fits beside it; the epilogue's operands stay in the blob (F = 64 relocation).
 // P = 2: two tiles per workgroup, two waves each (a slab and exchange buffers per tile);
 // P = 4: the whole workgroup on one tile.
-// FUSE: 0 plain, 1 pooling fused in, 2 unpooling fused in (as k_edge_coop)
+// FUSE: 0 plain, 1 pooling fused in (F = 64 keeps the unpooling launch: its 384-MFMA MLP per
+// side costs more than the launch it saves, zenodo4_f64 -2.5 %, profiles/r03/ab_unpool_fuse_f64.txt)
 template <int ACT, int LST, int P = 4, int FUSE = 0>
 __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma clang fp contract(off)
+  static_assert(FUSE == 0 || FUSE == 1, "k_edge_coop4: plain or fused pooling");
   constexpr int NT = 4, F = 16 * NT, T2 = 2 * NT, G = kWaves / P, TS = NT / P;
   constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
   constexpr int XW = 16 * T2 + 4;
@@ -1657,12 +1646,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   }
   EdgeHopRows<NT> q;
   [[maybe_unused]] PoolIn<NT> pin;
-  [[maybe_unused]] UnpoolIn<NT> uin;
-  [[maybe_unused]] const int side = r >= P / 2;  // fused (un)pooling: 0 source side, 1 destination side
+  [[maybe_unused]] const int side = r >= P / 2;  // fused pooling: 0 source side, 1 destination side
   if constexpr (FUSE == 1)
     edge_pool_load<NT, LST>(q, pin, a, tile, j, g, side);
-  else if constexpr (FUSE == 2)
-    edge_unpool_load<NT, LST>(q, uin, a, tile, j, g, side);
   else
     edge_hop_load<NT, LST>(q, a, tile, j, g);
   const Lanes& L = q.L;
@@ -1672,17 +1658,14 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   float* my = &slab[j][0];
   if constexpr (FUSE != 0) {
     // source side -> exchange rows (in xbuf, free until the MLP), destination side -> the
-    // node slab; projection (and unpooling MLP) operands from the blob (c.W); the unpooling
-    // row is formed by every rank of its side (the projection's output tiles are split)
+    // node slab; projection operands from the blob (c.W), its output tiles split over the
+    // ranks of a side
     constexpr int XPB = 16 * T2 + 16 * NT + 4;
     static_assert(kRowsPerWave * XPB <= 2 * kRowsPerWave * XW, "exchange rows fit the xbuf pair");
     float* pb = &xbuf[0][0][0] + j * XPB;
     f32x4 xp[NT];
-    if constexpr (FUSE == 1)
-      pool_mean<NT>(xp, pin, a, g);
-    else
-      unpool_row<NT>(xp, uin, a, c.W, lane, g);
-    const f32x4(&xsr)[NT] = FUSE == 1 ? pin.xs : uin.xs;
+    pool_mean<NT>(xp, pin, a, g);
+    const f32x4(&xsr)[NT] = pin.xs;
     if (a.pool.np.h1t == T2)
       pool_project_part<NT, P, T2>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
     else
@@ -1809,14 +1792,7 @@ static const void* edge_coop_kernel(int prelu, int last, int pw = 0, int pool = 
       if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 4, 1> : (const void*)k_edge_coop4<-1, 1, 4, 1>;
       return prelu ? (const void*)k_edge_coop4<1, 0, 4, 1> : (const void*)k_edge_coop4<-1, 0, 4, 1>;
     }
-    if (pool == 2) {  // unpooling fused in
-      if (pw == 2) {
-        if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2, 2> : (const void*)k_edge_coop4<-1, 1, 2, 2>;
-        return prelu ? (const void*)k_edge_coop4<1, 0, 2, 2> : (const void*)k_edge_coop4<-1, 0, 2, 2>;
-      }
-      if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 4, 2> : (const void*)k_edge_coop4<-1, 1, 4, 2>;
-      return prelu ? (const void*)k_edge_coop4<1, 0, 4, 2> : (const void*)k_edge_coop4<-1, 0, 4, 2>;
-    }
+    if (pool == 2) return nullptr;  // F = 64 keeps the unpooling launch
     if (pw == 2) {
       if (last) return prelu ? (const void*)k_edge_coop4<1, 1, 2> : (const void*)k_edge_coop4<-1, 1, 2>;
       return prelu ? (const void*)k_edge_coop4<1, 0, 2> : (const void*)k_edge_coop4<-1, 0, 2>;
@@ -2129,43 +2105,14 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
   const int w = wave_id();
   const int stride = gridDim.x * kRowHopWaves;
   const int ntile = (a.nrows + kRowsPerWave - 1) / kRowsPerWave;
-#ifdef MSW_ROW_FILT_LDS
-  // the filter operand in LDS (ds_read per use) instead of 4 NT^2 VGPRs
-  __shared__ __attribute__((aligned(16))) float wl[NT * NT * 256];
-  for (int i = threadIdx.x; i < NT * NT * 64; i += 64 * kRowHopWaves)
-    st4(wl + 4 * i, ld4(a.c.W + (a.filt_a >= 0 ? a.filt_a : 0) + 4 * i));
-  __syncthreads();
-#else
-  f32x4 wf[NT][NT];
+  f32x4 wf[NT][NT];  // the filter in registers (in LDS: equal, profiles/r03/ab_rows_variants.jsonl)
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
-#endif
-#ifdef MSW_ROW_PIPE
-  // the next tile's CSR offsets are loaded while this tile computes: per tile the dependent
-  // chain is edge records -> rows instead of offsets -> edge records -> rows
-  int pq0, pq1;
-  {
-    const int k = (blockIdx.x * kRowHopWaves + w) * kRowsPerWave + (threadIdx.x & 15);
-    const int kc = k < a.nrows ? k : 0;
-    pq0 = a.rptr[kc];
-    pq1 = k < a.nrows ? a.rptr[kc + 1] : pq0;
-  }
-#endif
   for (int tile = blockIdx.x * kRowHopWaves + w; tile < ntile; tile += stride) {
     const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
     const int k = tile * kRowsPerWave + j;
     const bool valid = k < a.nrows;
     const int kc = valid ? k : 0;
-#ifdef MSW_ROW_PIPE
-    const int q0 = pq0, q1 = pq1;
-    {
-      const int kn = (tile + stride) * kRowsPerWave + j;
-      const int knc = kn < a.nrows ? kn : 0;
-      pq0 = a.rptr[knc];
-      pq1 = kn < a.nrows ? a.rptr[knc + 1] : pq0;
-    }
-#else
     const int q0 = a.rptr[kc], q1 = valid ? a.rptr[kc + 1] : q0;
-#endif
     const size_t n = (size_t)a.n0 + kc;
     f32x4 od[NT];
     load_row<NT>(od, a.in + n * F, g);
@@ -2219,11 +2166,7 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
     f32x4 res[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) res[t] = od[t];
-#ifdef MSW_ROW_FILT_LDS
-    apply_filter<NT>(res, agg, a.filt_a >= 0 ? 0 : -1, wl, ln);
-#else
     apply_filter_regs<NT>(res, agg, a.filt_a, wf);
-#endif
     if (valid) store_row<NT>(a.out + n * F, res, NT, g);
   }
 }
@@ -2472,197 +2415,6 @@ template <int NT>
 static const void* hop_coop_kernel(int prelu) {
   if constexpr (NT >= 2) return prelu ? (const void*)k_hop_coop<NT, 1, NT> : (const void*)k_hop_coop<NT, -1, NT>;
   return nullptr;
-}
-
-// ---------------------------------------------------------------------------- hop chain
-// Hops k .. k+M-1 in one launch (engine.h HopMArgs).  Grid-stride over workgroup blocks;
-// every wave of a workgroup walks the same blocks and levels, so the barriers are uniform.
-// chain_waves<NT>() waves per workgroup: a level's halo tiles run one per wave (their
-// gathers in parallel); waves 0 .. kWaves-1 also own the final level's tiles, whose
-// records, s rows and epilogue inputs are loaded at block start, behind level 1.
-template <int NT, int M>
-struct ChainFilt {  // the M filters in registers (F <= 32); F = 64 reads them from the blob
-  f32x4 w[NT <= 2 ? M : 1][NT][NT];
-};
-template <int NT, int M>
-__device__ __forceinline__ void chain_filter(f32x4 (&res)[NT], const f32x4 (&agg)[NT], const ChainFilt<NT, M>& cf,
-                                             int l, const HopMArgs& a, int lane) {
-  if constexpr (NT <= 2) {
-    apply_filter_regs<NT>(res, agg, a.filt[l], cf.w[l]);
-  } else {
-    apply_filter<NT>(res, agg, a.filt[l], a.c.W, lane);
-  }
-}
-// A level tile of this wave: its lane record {src, p, dl, n}, {bl, q} and s rows.
-constexpr int kPre1 = 2;  // level-1 tiles per wave fetched up front (~11 per block of 4 tiles / 8 waves)
-template <int NT>
-struct LvPre {
-  int4 r0, r1;
-  f32x4 sv[NT];
-};
-// The load is unconditional (t must be a valid tile; callers clamp it) and `ok` selects
-// afterwards: a predicated load made the compiler drain the memory counter behind each one.
-template <int NT>
-__device__ __forceinline__ void lv_rec(LvPre<NT>& q, const HopMArgs& a, int t, bool ok, int j) {
-  const int4* rp = reinterpret_cast<const int4*>(a.lv + (size_t)t * kRowsPerWave + j);
-  const int4 r0 = rp[0], r1 = rp[1];
-  q.r0 = ok ? r0 : int4{-1, 0, 0, -1};
-  q.r1 = ok ? r1 : int4{0, 0, 0, 0};
-}
-// a tile with a node in lane 0 (wave-uniform test; padding tiles and absent slots have none)
-template <int NT>
-__device__ __forceinline__ bool lv_live(const LvPre<NT>& q) {
-  return __builtin_amdgcn_readfirstlane(q.r0.w) >= 0;
-}
-template <int NT>
-__device__ __forceinline__ void lv_s(LvPre<NT>& q, const HopMArgs& a, int g) {
-  load_row<NT>(q.sv, a.s + (size_t)(q.r0.x >= 0 ? q.r0.y : 0) * 16 * NT, g);
-}
-// One level tile: message, segmented sum, filter of hop l; result row to `to` (LDS set).
-template <int NT, int M>
-__device__ __forceinline__ void lv_hop(const LvPre<NT>& q, const f32x4 (&os)[NT], const f32x4 (&inn)[NT], float* to,
-                                       float* slab, float* my, const ChainFilt<NT, M>& cf, int l,
-                                       const HopMArgs& a, int lane, int g) {
-#pragma clang fp contract(off)
-  constexpr int XS = 16 * NT + 4;
-  const bool ev = q.r0.x >= 0, nv = q.r0.w >= 0;
-  f32x4 od[NT];
-  store_row<NT>(my, inn, NT, g);
-  wave_lds_sync();
-  load_row<NT>(od, slab + (ev ? q.r0.z : 0) * XS, g);
-  put_message<NT>(my, os, od, q.sv, ev, a.grad, a.upwind, g);
-  f32x4 agg[NT], res[NT];
-  const int q0 = q.r1.y & 255, q1 = nv ? (q.r1.y >> 8) : q0;
-  gather_messages<NT, XS>(agg, slab, q0, q1, g);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) res[t] = inn[t];
-  chain_filter<NT, M>(res, agg, cf, l, a, lane);
-  if (nv) store_row<NT>(to + (size_t)q.r1.x * XS, res, NT, g);
-}
-template <int NT, int ACT, int M, bool LAST>
-__global__ __launch_bounds__(64 * chain_waves<NT>()) void k_hopm(HopMArgs a) {
-#pragma clang fp contract(off)
-  constexpr int WV = chain_waves<NT>();
-  constexpr int F = 16 * NT;
-  constexpr int XS = F + 4;  // padded rows: conflict-free b128 LDS accesses
-  __shared__ __attribute__((aligned(16))) float slab_all[WV][kRowsPerWave][XS];
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // [weights][buf0][buf1]
-  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  Common c = a.c;
-  MSW_MARK(c, 0);
-  ChainFilt<NT, M> cf;
-  if constexpr (LAST && kStaged<NT>) stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);  // waited at level 1's barrier
-  float* const buf[2] = {smem + a.wfloats, smem + a.wfloats + (size_t)a.bmax * XS};
-  float* slab = &slab_all[w][0][0];
-  float* my = slab + j * XS;
-  bool staged = !(LAST && kStaged<NT>);
-  for (int blk = blockIdx.x; blk < a.nblocks; blk += gridDim.x) {
-    // final level of this wave (its own tile): everything that does not depend on the levels
-    const int tile = blk * kWaves + w;
-    const bool live = w < kWaves && tile < a.ntiles;
-    const int ts = live ? tile : 0;
-    const Lanes LF = lanes_of(load_rec(a.recs, ts, j), ts, j, a.n0);
-    const int2 sd = a.lf[(size_t)ts * kRowsPerWave + j];
-    const int a0 = a.a0[blk];
-    f32x4 svF[NT];
-    load_row<NT>(svF, a.s + LF.p * F, g);
-    EpiPre<NT> pre;
-    if constexpr (LAST) epi_prefetch<NT>(pre, a.epi, c, a.xs, LF.n, g);
-    // ---- levels 1 .. M-1: out_{k+l} on D_l into buf[(l-1) & 1].  The first kPre1 level-1
-    // tiles and the first level-2 tile of this wave are fetched up front (records, then s
-    // rows and level 1's HBM gathers, all in flight together); further tiles (rare) load
-    // on the spot.
-    // level l's tiles of this block: lv_base + blk * lv_tiles + slot (fixed stride: no
-    // offset load in front of the records); empty padding tiles have no node in lane 0
-    const int n1 = a.lv_tiles[0], b1 = a.lv_base[0] + blk * n1;
-    LvPre<NT> p1[kPre1], p2;
-    f32x4 os1[kPre1][NT], in1[kPre1][NT];
-#pragma unroll
-    for (int u = 0; u < kPre1; ++u) {
-      const int sl = w + u * WV;
-      lv_rec<NT>(p1[u], a, b1 + (sl < n1 ? sl : n1 - 1), sl < n1, j);
-    }
-    const int n2 = M > 2 ? a.lv_tiles[1] : 0, b2 = M > 2 ? a.lv_base[1] + blk * n2 : 0;
-    if constexpr (M > 2) lv_rec<NT>(p2, a, b2 + (w < n2 ? w : n2 - 1), w < n2, j);
-    MSW_MARK(c, 2);
-    // the filters (blob -> registers) go out behind the records: issued first, their
-    // register writes held the records back (the compiler waited on them)
-    if constexpr (NT <= 2) {
-#pragma unroll
-      for (int l = 0; l < M; ++l) load_filter<NT>(cf.w[l], a.c.W, a.filt[l], lane);
-    }
-    MSW_MARK(c, 3);
-#pragma unroll
-    for (int u = 0; u < kPre1; ++u) {
-      lv_s<NT>(p1[u], a, g);
-      load_row<NT>(os1[u], a.in + (size_t)(p1[u].r0.x >= 0 ? p1[u].r0.x : a.n0) * F, g);
-      load_row<NT>(in1[u], a.in + (size_t)(p1[u].r0.w >= 0 ? p1[u].r0.w : a.n0) * F, g);
-    }
-    if constexpr (M > 2) lv_s<NT>(p2, a, g);
-    MSW_MARK(c, 1);
-#pragma unroll
-    for (int u = 0; u < kPre1; ++u)
-      if (lv_live(p1[u])) lv_hop<NT, M>(p1[u], os1[u], in1[u], buf[0], slab, my, cf, 0, a, lane, g);
-    for (int t = w + kPre1 * WV; t < n1; t += WV) {
-      LvPre<NT> q;
-      f32x4 os[NT], inn[NT];
-      lv_rec<NT>(q, a, b1 + t, true, j);
-      if (!lv_live(q)) continue;
-      lv_s<NT>(q, a, g);
-      load_row<NT>(os, a.in + (size_t)(q.r0.x >= 0 ? q.r0.x : a.n0) * F, g);
-      load_row<NT>(inn, a.in + (size_t)(q.r0.w >= 0 ? q.r0.w : a.n0) * F, g);
-      lv_hop<NT, M>(q, os, inn, buf[0], slab, my, cf, 0, a, lane, g);
-    }
-    MSW_MARK(c, 4);
-    __syncthreads();
-    MSW_MARK(c, 5);
-    if constexpr (M > 2) {  // level 2: from buf[0] (LDS) into buf[1]
-      auto lds_hop = [&](const LvPre<NT>& q) {
-        f32x4 os[NT], inn[NT];
-        load_row<NT>(os, buf[0] + (size_t)(q.r0.x >= 0 ? q.r0.x : 0) * XS, g);
-        load_row<NT>(inn, buf[0] + (size_t)(q.r0.w >= 0 ? q.r0.w : 0) * XS, g);
-        lv_hop<NT, M>(q, os, inn, buf[1], slab, my, cf, 1, a, lane, g);
-      };
-      if (lv_live(p2)) lds_hop(p2);
-      for (int t = w + WV; t < n2; t += WV) {
-        LvPre<NT> q;
-        lv_rec<NT>(q, a, b2 + t, true, j);
-        if (!lv_live(q)) continue;
-        lv_s<NT>(q, a, g);
-        lds_hop(q);
-      }
-      MSW_MARK(c, 6);
-      __syncthreads();
-      MSW_MARK(c, 7);
-    }
-    if (!staged) {  // the epilogue operands' LDS-DMA was waited for at the barrier above
-      c.W = smem;
-      staged = true;
-    }
-    // ---- final level: out_{k+M} on A from buf[(M-2) & 1]
-    if (live) {
-      const float* fb = buf[(M - 2) & 1];
-      const int nl = LF.nv ? (int)(LF.n - a.n0) - a0 : 0;
-      f32x4 os[NT], od[NT], inn[NT];
-      load_row<NT>(os, fb + (size_t)(LF.ev ? sd.x : 0) * XS, g);
-      load_row<NT>(od, fb + (size_t)(LF.ev ? sd.y : 0) * XS, g);
-      load_row<NT>(inn, fb + (size_t)nl * XS, g);
-      put_message<NT>(my, os, od, svF, LF.ev, a.grad, a.upwind, g);
-      f32x4 agg[NT], res[NT];
-      gather_messages<NT, XS>(agg, slab, LF.q0, LF.q1, g);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) res[tt] = inn[tt];
-      chain_filter<NT, M>(res, agg, cf, M - 1, a, lane);
-      MSW_MARK(c, 8);
-      if constexpr (LAST) {
-        node_epilogue<NT, ACT>(res, a.epi, c, pre, a.out, (int)LF.n, LF.nv, lane, g);
-      } else {
-        if (LF.nv) store_row<NT>(a.out + LF.n * F, res, NT, g);
-      }
-    }
-    __syncthreads();  // the buffers are reused by the next block
-  }
-  MSW_MARK(c, 9);
 }
 
 // ---------------------------------------------------------------------------- pooling
@@ -2923,16 +2675,6 @@ constexpr size_t lds_bytes(int floats) {
   return kStaged<NT> ? (size_t)((floats + kChunk - 1) / kChunk * kChunk) * sizeof(float) : 0;
 }
 
-template <int NT>
-static const void* hopm_kernel(int m, int last, int prelu) {
-  if (!last) return m == 3 ? (const void*)k_hopm<NT, 1, 3, false> : (const void*)k_hopm<NT, 1, 2, false>;
-  if (prelu) return m == 3 ? (const void*)k_hopm<NT, 1, 3, true> : (const void*)k_hopm<NT, 1, 2, true>;
-  return m == 3 ? (const void*)k_hopm<NT, -1, 3, true> : (const void*)k_hopm<NT, -1, 2, true>;
-}
-template <int NT>
-size_t hopm_lds(const HopMArgs& a) {
-  return ((size_t)a.wfloats + (size_t)(a.m == 3 ? 2 : 1) * a.bmax * (16 * NT + 4)) * sizeof(float);
-}
 // Allow the dynamic weight regions past the 64 KB default (gfx950: 160 KB per CU).
 template <int NT>
 hipError_t prepare_kernels() {
@@ -2992,7 +2734,7 @@ hipError_t prepare_kernels() {
     for (int pw = 2; pw <= 4; pw += 2) {
       for (int prelu = 0; prelu < 2; ++prelu)
         for (int last = 0; last < 2; ++last)
-          for (int pool = 0; pool < 3; ++pool) {
+          for (int pool = 0; pool < 2; ++pool) {
             hipError_t e = hipFuncSetAttribute(edge_coop_kernel<NT>(prelu, last, pw, pool),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                edge_coop_lds_cap<NT>(pw, pool));
@@ -3010,15 +2752,6 @@ hipError_t prepare_kernels() {
           if (e != hipSuccess) return e;
         }
   }
-  // hop chains: 160 KB minus their own (narrower) static slabs
-  constexpr int WC = chain_waves<NT>();
-  for (int m = 2; m <= kChainMax; ++m)
-    for (int last = 0; last < 2; ++last)
-      for (int prelu = 0; prelu < 2; ++prelu) {
-        hipError_t e = hipFuncSetAttribute(hopm_kernel<NT>(m, last, prelu), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024 - WC * kRowsPerWave * (16 * NT + 4) * (int)sizeof(float));
-        if (e != hipSuccess) return e;
-      }
   return hipSuccess;
 }
 
@@ -3234,15 +2967,6 @@ hipError_t launch_pool(const PoolArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 template <int NT>
-hipError_t launch_hopm(const HopMArgs& a, hipStream_t st) {
-  if (a.nblocks <= 0) return hipSuccess;
-  if (a.m < 2 || a.m > kChainMax) return hipErrorInvalidValue;
-  const int grid = a.max_blocks > 0 && a.nblocks > a.max_blocks ? a.max_blocks : a.nblocks;
-  void* args[] = {const_cast<HopMArgs*>(&a)};
-  return hipLaunchKernel(hopm_kernel<NT>(a.m, a.last, a.c.prelu), dim3(grid), dim3(64 * chain_waves<NT>()), args,
-                         hopm_lds<NT>(a), st);
-}
-template <int NT>
 hipError_t launch_epi(const EpiArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
   const bool loop = tile_loop(a);
@@ -3292,19 +3016,17 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
     case 14: return (const void*)k_hop_rows<NT>;
     case 15: return prelu ? (const void*)k_edge_mlp_pipe<NT, 1> : (const void*)k_edge_mlp_pipe<NT, -1>;
-    default: return nullptr;  // kind 4: resident_blocks asks hopm_kernel
+    default: return nullptr;
   }
 }
 template <int NT>
 int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
-  const void* f = kind == 4 ? hopm_kernel<NT>(loop, last, prelu)
-                 : loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
+  const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
-  const size_t dyn = kind == 4 ? dyn_bytes : (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
+  const size_t dyn = (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
-  const int block = kind == 4 ? 64 * chain_waves<NT>()
-                    : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
+  const int block = kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
                     : kind == 15 ? 64 * kMlpPipeWaves
                     : kind == 13 ? 64 * 2 * NT
@@ -3326,7 +3048,6 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_edge_mlp<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
-  template hipError_t launch_hopm<NT>(const HopMArgs&, hipStream_t);              \
   template hipError_t launch_epi<NT>(const EpiArgs&, hipStream_t);                \
   template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);
 

@@ -199,15 +199,6 @@ struct ScaleCSR {
 
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
   std::vector<LaneRec> hrecs;   // host copy of recs (fused pooling slots, PoolSlot)
-  // hop chains of m = 2, 3 hops (engine.h HopMArgs), indexed by m; ok = false -> not built
-  struct Chain {
-    bool ok = false;
-    int nblocks = 0, bmax = 0;
-    int lv_base[kChainMax - 1] = {}, lv_tiles[kChainMax - 1] = {};
-    PairRec* lv = nullptr;
-    int* a0 = nullptr;
-    int2* lf = nullptr;
-  } chain[kChainMax + 1];
 };
 
 struct LevelMaps {              // level l: coarse scale l+1, fine scale l
@@ -277,7 +268,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_HOPM, L_EXCHANGE, L_EPI, L_EDGE_MLP };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -297,7 +288,6 @@ struct Launch {
     EdgeHopArgs eh;
     HopArgs hop;
     PoolArgs pool;
-    HopMArgs hopm;
     ExchangeArgs xch;
     EpiArgs ep;
   };
@@ -308,13 +298,52 @@ struct Launch {
       case L_EDGE_HOP:
       case L_EDGE_MLP: return eh.c;
       case L_HOP: return hop.c;
-      case L_HOPM: return hopm.c;
       case L_EXCHANGE: return xch.c;
       case L_EPI: return ep.c;
       default: return pool.c;
     }
   }
 };
+
+// Engine switches: read ONCE per plan (knobs_from_env) from MSW_* environment variables.
+// Defaults are the measured-best settings; every switch flips a schedule between variants
+// that are bit-identical (each has a -m gpu test that flips it), so a stray variable can
+// change speed, never results.  bench.py records the MSW_* variables of its process.
+struct Knobs {
+  int split_edge_mlp = -1;  // MSW_SPLIT_EDGE_MLP  F = 64 split edge MLP: -1 size rule, 0 / 1 force
+  int pool_fuse = 1;        // MSW_POOL_FUSE       mean pooling fused into the coarse first launch
+  int unpool_fuse = 1;      // MSW_UNPOOL_FUSE     F = 32 unpooling fused into the fine first launch
+  int defer_decode = -1;    // MSW_DEFER_DECODE    decoder in the next step's encoder: -1 size rule
+  int hop_rows = -1;        // MSW_HOP_ROWS        row-layout middle hops: -1 size rule, 0 off, 2 all
+  int coop2_direct = 1;     // MSW_COOP2_DIRECT    F = 64 two-wave edge hop, blob-read MLP: 0 / 1 / 2
+  int coop2_f64 = 1;        // MSW_COOP2_F64       F = 64 two-wave edge hops: 0 off, 2 also for four
+  int enc_coop = -1;        // MSW_ENC_COOP        cooperative encoder: -1 size rule, 0 / 1 force
+  int enc_coop_p = 0;       // MSW_ENC_COOP_P      F = 64 cooperative encoder on 2 waves per tile
+  int mlp_pipe = -1;        // MSW_MLP_PIPE        pipelined split edge MLP: -1 = F = 64
+  int eh_loop = 0;          // MSW_EH_LOOP         grid-stride fused edge hops at any size
+  int hop_split = -1;       // MSW_HOP_SPLIT       feature-split middle hops: -1 = F = 64 rule
+  int pool_wide = 1;        // MSW_POOL_WIDE       2F / 16 waves per pooling tile
+  int tile_pack = 1;        // MSW_TILE_PACK       degree-aware destination order
+  int xcd_max = 1;          // MSW_XCD_MAX         XCD packing of small grids (0 = all eight XCDs)
+  int coop_waves = -1;      // MSW_COOP_WAVES      cooperative kernels while P x tiles <= this (-1 default)
+  int epi_split_tiles = -1; // MSW_EPI_SPLIT_TILES row-epilogue threshold in edge tiles (-1 default)
+  int trace_encode = 0;     // MSW_TRACE_ENCODE    diagnostic builds (-DMSW_TRACE): encoder marks only
+};
+inline Knobs knobs_from_env() {
+  Knobs k;
+  const struct { const char* name; int* v; } tab[] = {
+      {"MSW_SPLIT_EDGE_MLP", &k.split_edge_mlp}, {"MSW_POOL_FUSE", &k.pool_fuse},
+      {"MSW_UNPOOL_FUSE", &k.unpool_fuse}, {"MSW_DEFER_DECODE", &k.defer_decode}, {"MSW_HOP_ROWS", &k.hop_rows},
+      {"MSW_COOP2_DIRECT", &k.coop2_direct}, {"MSW_COOP2_F64", &k.coop2_f64}, {"MSW_ENC_COOP", &k.enc_coop},
+      {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_EH_LOOP", &k.eh_loop},
+      {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
+      {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
+      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
+  for (const auto& t : tab)
+    if (const char* e = getenv(t.name)) *t.v = atoi(e);
+  if (getenv("MSW_TRACE_ENCODE")) k.trace_encode = 1;
+  return k;
+}
 
 struct msw_plan {
   int device = 0;
@@ -356,13 +385,6 @@ struct msw_plan {
   int kernels_per_step = 0;
   std::vector<Launch> sched_fwd, sched_roll;  // one forward step: forward / rollout mode
   int use_graph = 1;
-  // Hop chains (several hops per launch, halo recomputed in LDS) are off by default:
-  // measured on MI355X (graph replay) one launch per hop is 0.7-1.6 % faster on zenodo4,
-  // the batch of 8 and dk15 (profiles/r01_v7/ab_chains.txt).  MSW_HOP_CHAINS=m (2 or 3)
-  // turns chains of up to m hops on.
-  int hop_pairs = 0;
-  int chain_max = kChainMax;
-  int chain_max_tiles = 1 << 30;  // chains only on scales with at most this many edge tiles (MSW_HOP_CHAIN_TILES)
   // A layer's last hop on a scale with at least this many edge tiles runs as a middle hop
   // + a row epilogue launch (engine.h EpiArgs); MSW_EPI_SPLIT_TILES overrides (0: never).
   // Measured on MI355X (profiles/r01_v7/ab_epi_split.txt).
@@ -391,16 +413,14 @@ struct msw_plan {
   float *fwd_x = nullptr, *fwd_y = nullptr;
   // Steps per graph launch: consecutive launches of one graph leave a ~8.5 us gap on the
   // device (measured, rocprofv3 step breakdown), inside a graph the steps run back to back.
-  // MSW_GRAPH_STEPS overrides (1: one graph launch per step).
   int graph_steps = 16;
-  // Fused edge MLP + hop with two waves per tile (k_edge_coop) when 2 x tiles <= coop_waves
-  // (MSW_COOP_WAVES; 0: never).  Per launch kind: coop_w[0] edge hop, [1] last hop,
-  // [2] pooling (MSW_COOP_WAVES_EH / _HOP / _POOL override the shared value).
+  // Cooperative kernels (several waves per tile: edge hop, last hop, pooling) while
+  // waves-per-tile x tiles <= coop_waves (MSW_COOP_WAVES; 0: never).
   // small one-round grids on at most this many XCDs (engine.h Common::xcd, MSW_XCD_MAX;
   // 0 = all eight)
   int xcd_max = 1;
   int coop_waves = 1024;
-  int coop_w[3] = {1024, 1024, 1024};
+  Knobs kn;                 // engine switches of this plan (knobs_from_env)
   // set when a fused (un)pooling launch's weight region would not fit its kernel's LDS cap
   // (edge_coop_lds_cap): the schedule is rebuilt with the pooling / unpooling launches
   int no_fuse = 0;
@@ -566,44 +586,11 @@ void sched_exchange(msw_plan* P, std::vector<Launch>& q, int scale, std::initial
   q.push_back(L);
 }
 
-// Floats of a launch's epilogue operand region, as Relocator::epi lays it out (before its
-// de-duplication: an upper bound), in whole 1-KB LDS-DMA chunks.
-int epi_floats(const msw_plan* P, const Epilogue& e) {
-  if (P->NT > 2) return 0;  // F = 64: read from the blob in place
-  const int NT = P->NT;
-  int n = 0;
-  auto add = [&](int off, int len) { if (off >= 0) n += (len + 3) & ~3; };
-  add(e.np.a_u, e.np.h1t * 2 * NT * 256);
-  add(e.np.a_v, e.np.h1t * 2 * NT * 256);
-  add(e.np.a_o, NT * NT * 256);
-  add(e.uu_a, e.uu_h1t * 2 * NT * 256);
-  if (e.dec.on) {
-    for (int i = 0; i < e.dec.dec.n; ++i) {
-      add(e.dec.dec.l[i].a_off, e.dec.dec.l[i].tout * e.dec.dec.l[i].tin * 256);
-      add(e.dec.dec.l[i].b_off, 16 * e.dec.dec.l[i].tout);
-    }
-    add(e.dec.resw_off, 2 * P->p);
-  }
-  return (n + 255) / 256 * 256;
-}
-// LDS of an m-hop chain launch on scale g: static slab + epilogue operands + level buffers.
-size_t chain_lds(const msw_plan* P, const ScaleCSR::Chain& ch, int m, int last_floats) {
-  const int WV = P->NT <= 2 ? chain_waves<2>() : chain_waves<4>();
-  const size_t row = (size_t)(16 * P->NT + 4) * sizeof(float);
-  return (size_t)WV * kRowsPerWave * row + (size_t)last_floats * sizeof(float) +
-         (size_t)(m == 3 ? 2 : 1) * ch.bmax * row;
-}
-bool chain_fits(const msw_plan* P, const ScaleCSR& g, int m, bool last, const Epilogue& epi) {
-  if (m < 2 || m > kChainMax || !g.chain[m].ok) return false;
-  return chain_lds(P, g.chain[m], m, last ? epi_floats(P, epi) : 0) <= 160 * 1024;
-}
-
 constexpr int kSplitMlpTiles = 1024;  // F = 64: split edge MLP from this many edge tiles up
 // the layer's edge MLP runs alone (k_edge_mlp) and hop 1 as a k_hop launch
 bool edge_mlp_split(const msw_plan* P, const Proc& pr) {
-  bool split = P->NT == 4 && pr.K > 1 && P->part_rank < 0 && P->sc[pr.scale].ntiles >= kSplitMlpTiles;
-  if (const char* sv = getenv("MSW_SPLIT_EDGE_MLP")) split = pr.K > 1 && P->part_rank < 0 && atoi(sv) != 0;
-  return split;
+  if (P->NT != 4 || pr.K < 2 || P->part_rank >= 0) return false;  // F = 64 only (F = 32: -3.4 %)
+  return P->kn.split_edge_mlp >= 0 ? P->kn.split_edge_mlp != 0 : P->sc[pr.scale].ntiles >= kSplitMlpTiles;
 }
 void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out, const Epilogue& epi,
                 const PoolFuse* pool = nullptr) {
@@ -654,32 +641,14 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   const float* cur = P->T[0];
   for (int k = 2; k <= pr.K;) {
     sched_exchange(P, q, pr.scale, {{cur == P->T[0] ? B_T0 : B_T1, P->F}});
-    // hops k .. k+m-1 as one chain where the scale has one: the longest that fits, never
-    // leaving a single hop behind it (4 hops -> 2 + 2)
-    const int rem = pr.K - k + 1;
-    int m = 1;
-    for (int mm = std::min({rem, P->chain_max, kChainMax}); mm >= 2; --mm) {
-      if (rem - mm == 1) continue;
-      if (chain_fits(P, g, mm, k + mm - 1 == pr.K, epi)) { m = mm; break; }
-    }
-    const bool last = k + m - 1 == pr.K;
+    // one launch per hop (hop chains -- several hops per launch with the halo recomputed --
+    // measured 0.7-1.6 % slower under graph replay, profiles/r01_v7/ab_chains.txt; removed)
+    const int m = 1;
+    const bool last = k == pr.K;
     float* nxt = last ? out : (cur == P->T[0] ? P->T[1] : P->T[0]);
     Launch L;
     L.scale = pr.scale;
-    if (m >= 2) {
-      const ScaleCSR::Chain& ch = g.chain[m];
-      L.kind = L_HOPM;
-      HopMArgs& h = L.hopm;
-      h.c = c;
-      h.n0 = g.n0; h.recs = g.recs; h.ntiles = g.ntiles; h.lf = ch.lf; h.nblocks = ch.nblocks; h.m = m;
-      for (int l = 0; l < kChainMax - 1; ++l) { h.lv_base[l] = ch.lv_base[l]; h.lv_tiles[l] = ch.lv_tiles[l]; }
-      h.lv = ch.lv; h.a0 = ch.a0; h.bmax = ch.bmax;
-      h.s = P->s; h.xs = P->xs; h.in = cur; h.out = nxt;
-      for (int i = 0; i < kChainMax; ++i) h.filt[i] = (i < m && !pr.filt.empty()) ? pr.filt[k - 1 + i] : -1;
-      h.grad = pr.with_gradient; h.upwind = pr.upwind;
-      h.last = last;
-      h.epi = epi;
-    } else {
+    {
       // the last hop of a large scale: a middle hop into the free ping-pong buffer, then
       // the epilogue on dense node tiles (not on parts: their schedules must stay equal)
       // (only an epilogue with MFMA work gains: a bare store of the layer's output costs a
@@ -723,31 +692,26 @@ constexpr int kMaxFusedPoolBlocks = 256;  // one 4-wave workgroup (two tiles) pe
 // cooperative edge hop in one round (set_grid_cap's k_edge_coop rule), not on parts (their
 // halo exchange sits between the two launches).  MSW_POOL_FUSE=0 keeps the pooling launch.
 bool pool_fusable(const msw_plan* P, int s, const Proc& pr) {
-  const int on = getenv("MSW_POOL_FUSE") ? atoi(getenv("MSW_POOL_FUSE")) : 1;
-  if (!on || P->no_fuse || (P->NT != 2 && P->NT != 4) || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
+  if (!P->kn.pool_fuse || P->no_fuse || (P->NT != 2 && P->NT != 4) || P->part_rank >= 0 || s <= 0 || s >= P->S) return false;
   const ScaleCSR& g = P->sc[s];
   // K > 1: the launch is not the layer's last hop (k_edge_coop runs no unpool / decoder epilogue)
   if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s - 1].pool_slots || g.ntiles <= 0)
     return false;
   // the scales the cooperative kernels take in one round (F = 32: two waves per tile; F = 64:
   // four, or two with two tiles per workgroup)
-  return P->coop_w[0] > 0 && 2L * g.ntiles <= std::min(P->coop_w[0], kWaves * kMaxFusedPoolBlocks);
+  return P->coop_waves > 0 && 2L * g.ntiles <= std::min(P->coop_waves, kWaves * kMaxFusedPoolBlocks);
 }
 
 // The unpooling layer into fine scale s fused into the first launch of the processor on s
-// (k_edge_coop / k_edge_coop4 with PoolFuse::parent), as pool_fusable, F = 32 (F = 64 with
-// MSW_UNPOOL_FUSE=2); MSW_UNPOOL_FUSE=0 keeps the
-// unpooling launch.
+// (k_edge_coop with PoolFuse::parent), as pool_fusable, F = 32 only (at F = 64 its 384-MFMA
+// unpooling MLP per side outweighs the launch it saves: zenodo4_f64 -2.5 %,
+// profiles/r03/ab_unpool_fuse_f64.txt); MSW_UNPOOL_FUSE=0 keeps the unpooling launch.
 bool unpool_fusable(const msw_plan* P, int s, const Proc& pr, const Proc& up) {
-  const int on = getenv("MSW_UNPOOL_FUSE") ? atoi(getenv("MSW_UNPOOL_FUSE")) : 1;
-  // F = 64 only on request (=2): its 384-MFMA unpooling MLP per side outweighs the launch it
-  // saves (zenodo4_f64 -2.5 %, profiles/r03/ab_unpool_fuse_f64.txt)
-  if (!on || P->no_fuse || !(P->NT == 2 || (P->NT == 4 && on == 2)) || P->part_rank >= 0 || s < 0 || s + 1 >= P->S)
-    return false;
+  if (!P->kn.unpool_fuse || P->no_fuse || P->NT != 2 || P->part_rank >= 0 || s < 0 || s + 1 >= P->S) return false;
   const ScaleCSR& g = P->sc[s];
   if (pr.scale != s || pr.K < 2 || edge_mlp_split(P, pr) || !P->lv[s].parent_slots || g.ntiles <= 0) return false;
   if (up.h1t > 2 * P->NT || up.K != 1) return false;
-  return P->coop_w[0] > 0 && 2L * g.ntiles <= std::min(P->coop_w[0], kWaves * kMaxFusedPoolBlocks);
+  return P->coop_waves > 0 && 2L * g.ntiles <= std::min(P->coop_waves, kWaves * kMaxFusedPoolBlocks);
 }
 
 // One forward.  Forward mode: the encoder reads graph rows of x (via perm) and the decoder
@@ -787,7 +751,7 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
   // MSW_DEFER_DECODE=0/1 overrides.
   constexpr int kDeferMaxTiles = 65536;
   bool defer = rollout && P->sc[0].ntiles < kDeferMaxTiles;
-  if (const char* dv = getenv("MSW_DEFER_DECODE")) defer = rollout && atoi(dv) != 0;
+  if (P->kn.defer_decode >= 0) defer = rollout && P->kn.defer_decode != 0;
   ea.dec = dd;
   ea.dec.on = defer ? 1 : 0;
   ea.dec_in = P->model_type == 0 ? P->xup : P->xgnn;
@@ -1023,14 +987,6 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       rl.epi(R, a.epi);
       a.reg = R.done();
       reg = &a.reg;
-    } else if (L.kind == L_HOPM) {
-      HopMArgs& a = L.hopm;  // filters stay blob offsets (loaded into registers)
-      if (!a.last) continue;
-      RegionBuilder R(P->blob, 0);
-      rl.epi(R, a.epi);
-      a.reg = R.done();
-      a.wfloats = (a.reg.len + 255) / 256 * 256;
-      reg = &a.reg;
     } else if (L.kind == L_HOP) {
       HopArgs& a = L.hop;
       if (!a.last) continue;  // middle hops load their filter from the blob (k_hop<.., false>)
@@ -1073,29 +1029,12 @@ constexpr int kHopLoopTiles = 65536;
 // (k_hop_rows; MSW_HOP_ROWS=0 keeps the edge tiles)
 constexpr int kRowHopMinTiles = kHopLoopTiles;
 // MSW_HOP_ROWS=2: every middle hop in the row layout, at any size (parity tests)
-bool row_hops_forced() {
-  const char* e = getenv("MSW_HOP_ROWS");
-  return e && atoi(e) == 2;
-}
+bool row_hops_forced(const msw_plan* P) { return P->kn.hop_rows == 2; }
 constexpr long kEncCoopWaves = 4096;
-// MSW_COOP2_DIRECT: 0 never read the two-wave cooperative edge hop's MLP region from the
-// blob, 1 (default) when staging it would cost a second round, 2 always (parity tests)
-int wdirect_mode() {
-  const char* e = getenv("MSW_COOP2_DIRECT");
-  return e ? atoi(e) : 1;
-}
-bool no_loop(const char* kind) {
-  const char* e = getenv("MSW_NO_LOOP");
-  return e && (strstr(e, kind) || strstr(e, "all"));
-}
 void set_grid_cap(msw_plan* P, Launch& L) {
-  {  // XCD packing per launch kind (MSW_XCD_KINDS bit mask: 1 hop, 2 last hop, 4 edge MLP,
-     // 8 pooling, 16 row epilogue)
-    static const int kinds = getenv("MSW_XCD_KINDS") ? atoi(getenv("MSW_XCD_KINDS")) : 31;
-    const int bit = L.kind == L_HOP ? (L.hop.last ? 2 : 1) : L.kind == L_EDGE_HOP ? 4 : L.kind == L_POOL ? 8
-                  : L.kind == L_EPI ? 16 : 0;
-    if (!(kinds & bit)) L.common().xcd_max = 0;
-  }
+  // XCD packing (Common::xcd_max) applies to the hop, edge-hop, pooling and row-epilogue
+  // launches (the only one-round grids small enough to fit one XCD)
+  if (L.kind != L_HOP && L.kind != L_EDGE_HOP && L.kind != L_POOL && L.kind != L_EPI) L.common().xcd_max = 0;
   switch (L.kind) {
     case L_ENCODE: {
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
@@ -1103,19 +1042,17 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // zenodo4_f64 +5.0 %; at F = 32 the halved chains are too short for the seven LDS
       // exchanges: -2.5 %; MSW_ENC_COOP=0/1 overrides)
       bool coop = P->NT == 4 && (long)(L.enc.Npad / kRowsPerWave) * P->NT <= kEncCoopWaves;
-      if (const char* ec = getenv("MSW_ENC_COOP")) coop = P->NT >= 2 && atoi(ec) != 0;
+      if (P->kn.enc_coop >= 0) coop = P->NT >= 2 && P->kn.enc_coop != 0;
       L.enc.coop = coop ? P->NT : 0;
-      // MSW_ENC_COOP_P=2: F = 64 on two waves per row tile instead of four (A/B)
-      if (const char* cp = getenv("MSW_ENC_COOP_P"))
-        if (coop && P->NT == 4 && atoi(cp) == 2) L.enc.coop = 2;
+      // MSW_ENC_COOP_P=2: F = 64 on two waves per row tile instead of four (bit-identity test)
+      if (coop && P->NT == 4 && P->kn.enc_coop_p == 2) L.enc.coop = 2;
       break;
     }
     case L_EDGE_MLP: {
       // one wave per SIMD walking ~2 chunks, the next chunk's gathers in flight under the
       // current chunk's MLP (k_edge_mlp_pipe; zenodo4_f64: 27.8 -> 27.0 us per launch,
       // +0.4 %; MSW_MLP_PIPE=0: k_edge_mlp, two waves per SIMD, one chunk each)
-      const char* pp = getenv("MSW_MLP_PIPE");
-      L.eh.pipe = pp ? atoi(pp) != 0 : P->NT == 4;  // F = 32 (forced split): -11 % on config 5
+      L.eh.pipe = P->kn.mlp_pipe >= 0 ? P->kn.mlp_pipe != 0 : P->NT == 4;
       L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
     }
@@ -1123,10 +1060,8 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       EdgeHopArgs& a = L.eh;
       caps(P, a, 1, a.c.prelu, a.last, a.reg.len);
       a.fit_blocks = resident_of(P->NT, 1, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0);
-      if (no_loop("eh")) a.max_blocks = 0;
       // MSW_EH_LOOP=1: the grid-stride variant at any size (parity tests of the large-mesh path)
-      if (const char* el = getenv("MSW_EH_LOOP"))
-        if (atoi(el) != 0 && a.max_blocks > 0 && a.ntiles > kWaves) a.fit_blocks = 1;
+      if (P->kn.eh_loop && a.max_blocks > 0 && a.ntiles > kWaves) a.fit_blocks = 1;
       // two waves per tile (k_edge_coop) while the tiles leave most SIMDs idle: one tile
       // per wave at most, no grid-stride loop, an epilogue of projections only
       const bool loop = a.fit_blocks > 0 && a.max_blocks > 0 && (a.ntiles + kWaves - 1) / kWaves > a.fit_blocks;
@@ -1136,7 +1071,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // (F = 32: two waves per tile; F = 64: four, one tile per workgroup)
       const int pw = P->NT == 2 ? 2 : P->NT == 4 ? 4 : 0;
       const int coop_fit = pw ? resident_of(P->NT, 7, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0) : 0;
-      a.coop = (pw && !loop && epi_ok && P->coop_w[0] > 0 && (long)pw * a.ntiles <= P->coop_w[0] &&
+      a.coop = (pw && !loop && epi_ok && P->coop_waves > 0 && (long)pw * a.ntiles <= P->coop_waves &&
                 (pw * a.ntiles + kWaves - 1) / kWaves <= coop_fit) ? pw : 0;
       // F = 64 where four waves per tile do not fit one round: two, two tiles per workgroup
       // (zenodo4_f64 scale 1: 508 tiles in one round, +2.0 %; MSW_COOP2_F64=0 off, =2 also in
@@ -1144,12 +1079,12 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // fused pooling exists in the cooperative kernels only (pool_fusable): F = 32 two waves
       // per tile; F = 64 four, or two where four do not fit one round (below)
       if ((a.pool.slots || a.pool.parent) && P->NT == 2) a.coop = 2;
-      const int c2 = getenv("MSW_COOP2_F64") ? atoi(getenv("MSW_COOP2_F64")) : 1;
+      const int c2 = P->kn.coop2_f64;
       if (c2 == 2 && a.coop == 4) a.coop = 0;
       a.wdirect = 0;
-      if (P->NT == 4 && !a.coop && !loop && epi_ok && P->coop_w[0] > 0 && 2L * a.ntiles <= P->coop_w[0] && c2) {
+      if (P->NT == 4 && !a.coop && !loop && epi_ok && P->coop_waves > 0 && 2L * a.ntiles <= P->coop_waves && c2) {
         const int need = (2 * a.ntiles + kWaves - 1) / kWaves;
-        const int wd = wdirect_mode();
+        const int wd = P->kn.coop2_direct;
         if (need <= resident_of(P->NT, 12, a.c.prelu, a.last, (size_t)a.reg_nf * 4, 0)) {
           a.coop = 2;
           a.wdirect = wd == 2 && a.reg.len > 0;
@@ -1162,14 +1097,6 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         }
       }
       if ((a.pool.slots || a.pool.parent) && !a.coop) a.coop = 2;  // F = 64 fused: two waves per tile, any grid
-      // A/B (MSW_FUSE_P4=1): an F = 64 fused launch on four waves per tile with the MLP region
-      // read from the blob (two workgroups per CU) where staging it would cost a second round
-      if ((a.pool.slots || a.pool.parent) && P->NT == 4 && a.coop == 2 && getenv("MSW_FUSE_P4") &&
-          atoi(getenv("MSW_FUSE_P4")) != 0 && a.reg.len > 0 &&
-          a.ntiles <= resident_of(P->NT, 7, a.c.prelu, a.last, 0, 0)) {
-        a.coop = 4;
-        a.wdirect = 1;
-      }
       break;
     }
     case L_HOP:
@@ -1178,20 +1105,19 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // not fit): the grid-stride variant measured 1.1-1.6 % slower on the batch of 8 and
       // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
       // (profiles/r01_v7/ab_edge_waves.txt)
-      if (no_loop("hop") || (!getenv("MSW_HOP_LOOP") && L.hop.ntiles < kHopLoopTiles)) L.hop.max_blocks = 0;
+      if (L.hop.ntiles < kHopLoopTiles) L.hop.max_blocks = 0;
       {  // F = 64: feature-split middle hops below the grid-stride size (k_hop_split;
          // zenodo4_f64 +4.6 %, F = 32 neutral; MSW_HOP_SPLIT=0/1 overrides the rule)
         bool sp = P->NT == 4 && L.hop.max_blocks == 0;
-        if (const char* hs = getenv("MSW_HOP_SPLIT")) sp = atoi(hs) != 0;
+        if (P->kn.hop_split >= 0) sp = P->kn.hop_split != 0;
         L.hop.split = (sp && P->NT >= 2 && !L.hop.last) ? 1 : 0;
       }
       {  // row layout for the grid-stride middle hops of large scales (k_hop_rows)
         HopArgs& h = L.hop;
         const bool loop = h.fit_blocks > 0 && h.max_blocks > 0 && (h.ntiles + kWaves - 1) / kWaves > h.fit_blocks;
-        const char* hr = getenv("MSW_HOP_ROWS");
-        const bool want = hr ? atoi(hr) != 0 : true;
+        const bool want = P->kn.hop_rows != 0;
         h.rows = 0;
-        if (want && !h.last && (loop || row_hops_forced()) && h.rptr && h.redge) {
+        if (want && !h.last && (loop || row_hops_forced(P)) && h.rptr && h.redge) {
           h.rows = 1;
           h.split = 0;
           h.max_blocks = resident_of(P->NT, 14, 0, 0, 0, 1);
@@ -1202,39 +1128,31 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         const bool loop = h.fit_blocks > 0 && h.max_blocks > 0 && (h.ntiles + kWaves - 1) / kWaves > h.fit_blocks;
         const int pw = P->NT >= 2 ? P->NT : 0;
         h.coop = 0;
-        if (h.last && pw && !loop && P->coop_w[1] > 0 && (long)pw * h.ntiles <= P->coop_w[1] &&
+        if (h.last && pw && !loop && P->coop_waves > 0 && (long)pw * h.ntiles <= P->coop_waves &&
             (pw * h.ntiles + kWaves - 1) / kWaves <= resident_of(P->NT, 9, h.c.prelu, 1, (size_t)h.reg.len * 4, 0))
           h.coop = pw;
       }
       break;
-    case L_HOPM: {
-      HopMArgs& a = L.hopm;
-      const size_t dyn = ((size_t)a.wfloats + (size_t)(a.m == 3 ? 2 : 1) * a.bmax * (16 * P->NT + 4)) * 4;
-      a.max_blocks = resident_of(P->NT, 4, a.c.prelu, a.last, dyn, a.m);
-      break;
-    }
     case L_EXCHANGE: break;
     case L_EPI:
       caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len);
-      if (no_loop("epi")) L.ep.max_blocks = 0;
       break;
     default: {
       // edge tiles while they all fit on the chip at once (latency-bound launch), else rows
       PoolArgs& a = L.pool;
       const int fe = resident_of(P->NT, 5, 0, 0, (size_t)a.reg.len * 4, 0);
-      a.rows = !(fe > 0 && (a.etiles + kWaves - 1) / kWaves <= fe) || getenv("MSW_POOL_ROWS") != nullptr;
+      a.rows = !(fe > 0 && (a.etiles + kWaves - 1) / kWaves <= fe);
       a.ntiles = a.rows ? a.rtiles : a.etiles;
       caps(P, a, 3, 0, 0, a.reg.len);
       // two waves per edge tile (projection split) while that grid too is resident at once
       // (F = 32: two waves per tile, F = 64: four)
       const int pw = P->NT >= 2 ? P->NT : 0;
-      a.coop = (!a.rows && pw && P->coop_w[2] > 0 && (long)pw * a.etiles <= P->coop_w[2] &&
+      a.coop = (!a.rows && pw && P->coop_waves > 0 && (long)pw * a.etiles <= P->coop_waves &&
                 (pw * a.etiles + kWaves - 1) / kWaves <= fe) ? pw : 0;
       // 2F-wide first edge-MLP layer: 2 * F / 16 waves per tile (one U and one V output tile
       // each) while resident (zenodo4_f64 +1.8 %, zenodo4 +0.6 %, profiles/r02_s4/ab_pool_p8.txt,
       // ab_pool_wide_f32.txt); MSW_POOL_WIDE=0: F / 16 waves; bit-identical either way
-      const char* pw2 = getenv("MSW_POOL_WIDE");
-      const bool wide = pw2 ? atoi(pw2) != 0 : true;
+      const bool wide = P->kn.pool_wide != 0;
       if (wide && pw && a.coop == pw && a.np.h1t == 2 * pw) {
         const int f8 = resident_of(P->NT, 13, 0, 0, (size_t)a.reg.len * 4, 0);
         if (f8 > 0 && a.etiles <= f8) a.coop = 2 * pw;
@@ -1264,7 +1182,6 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
     case L_EDGE_MLP: return launch_edge_mlp<NT>(L.eh, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
-    case L_HOPM: return launch_hopm<NT>(L.hopm, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
     case L_EPI: return launch_epi<NT>(L.ep, st);
     default: return hipErrorInvalidValue;  // exchanges are run by run_schedule / the group driver
@@ -1336,7 +1253,7 @@ int final_decode(msw_plan* P, hipStream_t st) {
     return MSW_OK;
   Launch L = P->sched_roll[0];
   L.enc.decode_only = 1;
-  if (getenv("MSW_TRACE_ENCODE")) L.enc.c.trace = nullptr;  // keep the last step's encoder marks
+  if (P->kn.trace_encode) L.enc.c.trace = nullptr;  // keep the last step's encoder marks
   switch (P->NT) {
     case 1: HIP_TRY(launch_one<1>(L, st)); break;
     case 2: HIP_TRY(launch_one<2>(L, st)); break;
@@ -1349,124 +1266,13 @@ int final_decode(msw_plan* P, hipStream_t st) {
 void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
   for (Launch& L : q) {
     if (L.kind == L_ENCODE) L.enc.x = x;
-    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi : L.kind == L_HOPM ? &L.hopm.epi
+    Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi
                  : L.kind == L_EPI ? &L.ep.epi : nullptr;
     if (e && e->dec.on) {
       e->dec.X = x;
       e->dec.y = y;
     }
   }
-}
-
-constexpr int kPairMaxTiles = 1024;
-
-// Level structures of the m-hop chain kernel for one scale (engine.h HopMArgs).
-// rowptr / so: the scale's CSR by destination (local rows / internal source rows);
-// pcsr: tile-padded slot -> CSR position.  Leaves chain[m].ok = false when a workgroup's
-// buffers would not fit the LDS budget (the schedule then uses shorter chains / single hops).
-int build_chain(msw_plan* P, ScaleCSR& c, const std::vector<int>& rowptr, const std::vector<int>& so,
-                const std::vector<TileRange>& tl, const std::vector<int>& pcsr, int m) {
-  const int ns = c.ns, n0 = c.n0, nt = (int)tl.size();
-  // only where a launch is latency-bound: on larger scales the halo recomputation costs
-  // more than the saved launch (measured with pairs: zenodo4 +1 %, batch of 8 / dk15
-  // -2..-4 % when every scale pairs; the finest zenodo4 scale has ~2k tiles)
-  if (nt == 0 || nt > kPairMaxTiles) return MSW_OK;
-  std::vector<int> slot_of_csr(rowptr[ns], -1);
-  for (size_t q = 0; q < pcsr.size(); ++q)
-    if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
-  const int nb = (nt + kWaves - 1) / kWaves;
-  std::vector<int> stamp(ns, -1), idx(ns, -1), D, a0(nb);
-  std::vector<std::vector<int>> lvt_off(m - 1, std::vector<int>(nb + 1, 0));
-  std::vector<std::vector<PairRec>> lvt(m - 1);  // per level, tiles of every block
-  std::vector<int> lsize(m);                     // |D_l|, l = 1 .. m-1 (index 0 unused)
-  std::vector<int2> lf((size_t)nt * kRowsPerWave, int2{0, 0});
-  int bmax = 0;
-  for (int b = 0; b < nb; ++b) {
-    const int t0 = b * kWaves, t1 = std::min(t0 + kWaves, nt);
-    const int abeg = tl[t0].node0, aend = tl[t1 - 1].node0 + tl[t1 - 1].nnode;
-    // D_m = A, D_{l-1} = D_l + in-neighbours of D_l: index = position in D_1 (prefixes)
-    D.clear();
-    for (int v = abeg; v < aend; ++v) { stamp[v] = b; idx[v] = (int)D.size(); D.push_back(v); }
-    size_t ring0 = 0;
-    for (int l = m - 1; l >= 1; --l) {
-      const size_t ring1 = D.size();
-      for (size_t i0 = ring0; i0 < ring1; ++i0) {
-        const int v = D[i0];
-        for (int i = rowptr[v]; i < rowptr[v + 1]; ++i) {
-          const int u = so[i] - n0;
-          if (stamp[u] != b) { stamp[u] = b; idx[u] = (int)D.size(); D.push_back(u); }
-        }
-      }
-      // all in-neighbours of D_{l+1} are now in: D_l = D[0 .. size)
-      lsize[l] = (int)D.size();
-      ring0 = ring1;
-      // (the in-neighbours of nodes added before ring0 were added in an earlier pass)
-    }
-    bmax = std::max(bmax, (int)D.size());
-    a0[b] = abeg;
-    // level l tiles over D_l: whole in-neighbourhoods, <= 16 edges and <= 16 nodes each
-    for (int l = 1; l < m; ++l) {
-      std::vector<PairRec>& T = lvt[l - 1];
-      lvt_off[l - 1][b] = (int)(T.size() / kRowsPerWave);
-      size_t tbase = T.size();
-      int nn = 0, ne = 0;
-      auto open_tile = [&]() {
-        tbase = T.size();
-        T.resize(tbase + kRowsPerWave, PairRec{-1, 0, 0, -1, 0, 0, 0, 0});
-        nn = ne = 0;
-      };
-      open_tile();
-      for (int di = 0; di < lsize[l]; ++di) {
-        const int v = D[di];
-        const int d = rowptr[v + 1] - rowptr[v];
-        if (d > kRowsPerWave) return fail(MSW_ERR_UNSUPPORTED, "node with more than 16 in-edges");
-        if (nn == kRowsPerWave || ne + d > kRowsPerWave) open_tile();
-        PairRec* R = &T[tbase];
-        R[nn].n = l == 1 ? n0 + v : idx[v];
-        R[nn].bl = idx[v];
-        R[nn].q = ne | ((ne + d) << 8);
-        for (int i = rowptr[v]; i < rowptr[v + 1]; ++i, ++ne) {
-          R[ne].src = l == 1 ? so[i] : idx[so[i] - n0];
-          R[ne].p = slot_of_csr[i];
-          R[ne].dl = nn;
-        }
-        ++nn;
-      }
-    }
-    // final level: set indices of each edge slot of the workgroup's own tiles
-    for (int t = t0; t < t1; ++t)
-      for (int jn = 0; jn < tl[t].nnode; ++jn) {
-        const int v = tl[t].node0 + jn;
-        for (int i = rowptr[v]; i < rowptr[v + 1]; ++i)
-          lf[(size_t)t * kRowsPerWave + (i - tl[t].edge0)] = int2{idx[so[i] - n0], idx[v]};
-      }
-  }
-  for (int l = 1; l < m; ++l) lvt_off[l - 1][nb] = (int)(lvt[l - 1].size() / kRowsPerWave);
-  // fixed stride per level: block b's tiles of level l at lv_base + b * lv_tiles (padded
-  // with empty tiles), so a kernel finds them without loading an offset first
-  ScaleCSR::Chain& ch = c.chain[m];
-  std::vector<PairRec> lv;
-  for (int l = 1; l < m; ++l) {
-    const std::vector<int>& off = lvt_off[l - 1];
-    int tmax = 1;
-    for (int b = 0; b < nb; ++b) tmax = std::max(tmax, off[b + 1] - off[b]);
-    ch.lv_base[l - 1] = (int)(lv.size() / kRowsPerWave);
-    ch.lv_tiles[l - 1] = tmax;
-    for (int b = 0; b < nb; ++b) {
-      const auto& T = lvt[l - 1];
-      lv.insert(lv.end(), T.begin() + (size_t)off[b] * kRowsPerWave, T.begin() + (size_t)off[b + 1] * kRowsPerWave);
-      lv.resize(lv.size() + (size_t)(tmax - (off[b + 1] - off[b])) * kRowsPerWave, PairRec{-1, 0, 0, -1, 0, 0, 0, 0});
-    }
-  }
-  ch.nblocks = nb;
-  ch.bmax = bmax;
-  if (chain_lds(P, ch, m, 0) > 160 * 1024) return MSW_OK;  // buffers too large: no chain of m here
-  int rc;
-  if ((rc = pupload(P, &ch.lv, lv)) || (rc = pupload(P, &ch.a0, a0)) ||
-      (rc = pupload(P, &ch.lf, lf)))
-    return rc;
-  ch.ok = true;
-  return MSW_OK;
 }
 
 int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
@@ -1484,7 +1290,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   // (each graph's destinations of a scale in pack_order; MSW_TILE_PACK=0: graph order)
   P->perm.clear();
   P->sc.assign(S, ScaleCSR{});
-  const bool pack = !getenv("MSW_TILE_PACK") || atoi(getenv("MSW_TILE_PACK")) != 0;
+  const bool pack = P->kn.tile_pack != 0;
   std::vector<int> indeg(pack ? N : 0, 0);
   if (pack)
     for (int64_t e = 0; e < g->num_edges; ++e) {
@@ -1559,9 +1365,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
       ck.resize((size_t)c.nchunks * kRowsPerWave, EdgeChunk{-1, -1, -1, 0});
       if (c.nchunks > 0 && (rc = pupload(P, &c.chunks, ck))) return rc;
     }
-    for (int m = 2; P->hop_pairs && c.ntiles <= P->chain_max_tiles && m <= P->chain_max; ++m)
-      if ((rc = build_chain(P, c, rowptr, so, tl, pcsr, m))) return rc;
-    if (c.ntiles >= kRowHopMinTiles || row_hops_forced()) {  // row-layout middle hops: CSR + s slots
+    if (c.ntiles >= kRowHopMinTiles || row_hops_forced(P)) {  // row-layout middle hops: CSR + s slots
       std::vector<int> slot_of_csr(c.E, -1);
       for (size_t q = 0; q < pcsr.size(); ++q)
         if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
@@ -1660,8 +1464,8 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
 int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, hipStream_t st) {
   if (scale < 0 || scale >= P->S) return fail(MSW_ERR_INVALID, "scale out of range");
   if (P->sched_roll.empty()) return fail(MSW_ERR_INVALID, "run a rollout before bench_kernel");
-  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP, L_HOPM};
-  if (kernel < 0 || kernel > 5) return fail(MSW_ERR_INVALID, "unknown kernel id");
+  static const int kind_of[] = {L_HOP, L_EDGE_HOP, L_POOL, L_ENCODE, L_EDGE_HOP};
+  if (kernel < 0 || kernel > 4) return fail(MSW_ERR_INVALID, "unknown kernel id");
   const bool unpool = kernel == 4;  // the intra-scale (unpooling) layer into `scale`
   const Launch* src = nullptr;
   for (const Launch& L : P->sched_roll)
@@ -1677,7 +1481,6 @@ int bench_kernel(msw_plan* P, int kernel, int scale, int iters, int64_t* units, 
   const ScaleCSR& g = P->sc[scale];
   int64_t rows = g.ns, edges = g.E;
   if (L.kind == L_HOP && L.hop.last) { L.hop.last = 0; L.hop.out = P->T[1]; }
-  if (L.kind == L_HOPM && L.hopm.last) { L.hopm.last = 0; L.hopm.out = P->T[1]; L.hopm.wfloats = 0; }
   if (L.kind == L_EDGE_HOP && L.eh.last && !unpool) { L.eh.last = 0; L.eh.out = P->T[1]; }
   if (L.kind == L_EDGE_HOP || L.kind == L_EDGE_MLP) L.eh.step_inc = nullptr;  // the rollout's step counter stays put
   if (unpool) edges = P->lv[scale].I;  // the unpool epilogue only writes the next layer's U/V/O
@@ -1798,25 +1601,13 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     return fail(MSW_ERR_INVALID, "MSGNN needs S-1 intra-scale layers");
   if (m->model_type == 1 && m->num_processors < 1) return fail(MSW_ERR_INVALID, "GNN needs >= 1 layer");
 
-  if (const char* es = getenv("MSW_EPI_SPLIT_TILES")) P->epi_split_tiles = atoi(es);
-  if (const char* gs = getenv("MSW_GRAPH_STEPS")) P->graph_steps = std::max(1, atoi(gs));
-  if (const char* xm = getenv("MSW_XCD_MAX")) P->xcd_max = std::max(0, atoi(xm));
+  P->kn = knobs_from_env();
+  if (P->kn.epi_split_tiles >= 0) P->epi_split_tiles = P->kn.epi_split_tiles;
+  P->xcd_max = std::max(0, P->kn.xcd_max);
   // F = 64: four-wave cooperative kernels on every scale whose grid stays resident
   // (zenodo4_f64 +3.3 %, profiles/r02_v1/ab_coop_f64.txt); F = 32 keeps 1024 (no gain above)
   if (P->NT == 4) P->coop_waves = 4096;
-  if (const char* cw = getenv("MSW_COOP_WAVES")) P->coop_waves = std::max(0, atoi(cw));
-  {
-    const char* kinds[3] = {"MSW_COOP_WAVES_EH", "MSW_COOP_WAVES_HOP", "MSW_COOP_WAVES_POOL"};
-    for (int k = 0; k < 3; ++k) {
-      const char* v = getenv(kinds[k]);
-      P->coop_w[k] = v ? std::max(0, atoi(v)) : P->coop_waves;
-    }
-  }
-  if (const char* cm = getenv("MSW_HOP_CHAINS")) {  // a chain's halo is m-1 rings deep: not on parts
-    P->chain_max = std::max(2, std::min(kChainMax, atoi(cm)));
-    P->hop_pairs = xch ? 0 : 1;
-    if (const char* ct = getenv("MSW_HOP_CHAIN_TILES")) P->chain_max_tiles = std::max(0, atoi(ct));
-  }
+  if (P->kn.coop_waves >= 0) P->coop_waves = P->kn.coop_waves;
   P->part_rank = xch ? rank : -1;
   int rc = build_graph_plan(P.get(), g);
   if (rc) return rc;
@@ -1984,7 +1775,7 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     for (const RowMlpArgs& ra : P->edge_jobs) HIP_TRY(rowmlp_dispatch(P->NT, ra));
   }
   HIP_TRY(hipDeviceSynchronize());
-  if (xch) P->use_graph = getenv("MSW_PART_GRAPH") ? 1 : 0;  // exchanges run eagerly by default
+  if (xch) P->use_graph = 0;  // partitioned plans: the RCCL exchanges run eagerly
   *out_plan = P.release();
   return MSW_OK;
 }
@@ -2294,7 +2085,7 @@ int msw_set_trace(msw_plan* P, uint64_t* buf) {
   if (!P) return fail(MSW_ERR_INVALID, "null plan");
   // MSW_TRACE_ENCODE: the encoder launches only (a rollout then leaves the marks of its last
   // step's encoder: the deferred decoder + encoders, tools/trace_kernels.py)
-  const bool enc_only = getenv("MSW_TRACE_ENCODE") != nullptr;
+  const bool enc_only = P->kn.trace_encode != 0;
   for (auto* q : {&P->sched_fwd, &P->sched_roll})
     for (Launch& L : *q)
       L.common().trace = (!enc_only || L.kind == L_ENCODE) ? reinterpret_cast<unsigned long long*>(buf) : nullptr;

@@ -288,7 +288,7 @@ class EnginePlan:
                                          self._stream()))
         return dst
 
-    KERNELS = {"hop": 0, "edge_hop": 1, "pool": 2, "encode": 3, "unpool": 4, "hopm": 5}  # plan.hip bench_kernel (hopm: opt-in hop chains)
+    KERNELS = {"hop": 0, "edge_hop": 1, "pool": 2, "encode": 3, "unpool": 4}  # plan.hip bench_kernel
 
     def bench_kernel(self, kernel, scale, iters):
         """Enqueue `iters` launches of one kernel on the current stream -> units (rows, edges)

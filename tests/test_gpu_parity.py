@@ -82,23 +82,6 @@ def test_rollout48_vs_reference(cuda, ck, K, F):
     assert st["rollout_steps"] >= 48
 
 
-@pytest.mark.parametrize("chain", ["2", "3"])
-def test_hop_chains_match_single_hops(cuda, chain, monkeypatch):
-    """Opt-in hop chains (MSW_HOP_CHAINS, several hops per launch with the halo recomputed
-    in LDS) against the reference fixture and the default one-launch-per-hop schedule."""
-    fx = golden("fx_small_K4_F32_rollout48")
-    g = make_multiscale_mesh(**mesh_config("small"), T=48).to(cuda)
-    base = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
-    r0 = base.rollout(g).cpu()
-    n0 = _stats(base, g)["kernels_per_step"]
-    monkeypatch.setenv("MSW_HOP_CHAINS", chain)
-    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
-    r = m.rollout(g).cpu()
-    assert _stats(m, g)["kernels_per_step"] < n0  # the chains were scheduled
-    assert per_step_rel(r, torch.from_numpy(fx["rollout"])) <= REL_TOL
-    assert per_step_rel(r, r0) <= 1e-6
-
-
 @pytest.mark.parametrize("model", ["msgnn_K4_F32", "msgnn_K2_F16", "gnn"])
 def test_row_epilogue_split_matches_fused(cuda, model, monkeypatch):
     """Last hop + row epilogue launch (engine.h EpiArgs; forced on every scale with
@@ -532,7 +515,7 @@ def test_upwind_mode_vs_oracle(cuda):
     assert per_step_rel(m.rollout(gs.to(cuda)).cpu(), ref) <= REL_TOL
 
 
-@pytest.mark.parametrize("F", [64, 32])
+@pytest.mark.parametrize("F", [64])
 def test_split_edge_mlp_matches_fused(cuda, F, monkeypatch):
     """MSW_SPLIT_EDGE_MLP=1: each processor's edge MLP over dense 16-edge chunks (k_edge_mlp,
     padding slots skipped, the last chunk partly filled) + hop 1 as a k_hop launch -- the
@@ -823,25 +806,21 @@ def test_fused_pooling_matches_pooling_launch(cuda, monkeypatch, F, act, coop2):
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
 
 
-@pytest.mark.parametrize("F,kw,coop2", [(32, {}, None), (32, {"mlp_activation": "relu"}, None),
-                                        (32, {"skip_connections": False}, None), (64, {}, None),
-                                        (64, {"mlp_activation": "relu"}, "2")])
-def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, F, kw, coop2):
+@pytest.mark.parametrize("F,kw", [(32, {}), (32, {"mlp_activation": "relu"}), (32, {"skip_connections": False})])
+def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, F, kw):
     """The unpooling layer (intra-scale SWEGNN, own rows zero, + skip, + projection of the next
-    processor) fused into the fine scale's first edge-MLP + hop launch (k_edge_coop<.., 2>,
-    k_edge_coop4<.., 2> at F = 64 -- four or, with MSW_COOP2_F64=2, two waves per tile;
-    MSW_UNPOOL_FUSE=1, the default on small scales at F = 32; =2 at F = 64) == the separate
-    unpooling launch (MSW_UNPOOL_FUSE=0), bit for bit: forward, rollout, a batch of two meshes;
-    fewer launches; and the oracle."""
-    if coop2:
-        monkeypatch.setenv("MSW_COOP2_F64", coop2)
+    processor) fused into the fine scale's first edge-MLP + hop launch (k_edge_coop<.., 2>;
+    MSW_UNPOOL_FUSE=1, the default on small scales at F = 32) == the separate unpooling launch
+    (MSW_UNPOOL_FUSE=0), bit for bit: forward, rollout, a batch of two meshes; fewer launches;
+    and the oracle.  F = 64 keeps the unpooling launch (the fused F = 64 variant measured
+    -2.5 %, profiles/r03/ab_unpool_fuse_f64.txt, and was removed)."""
     from mswegnn.batch import collate
     from mswegnn.rollout import rollout_test
     ga = _reparent(wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=23))
     gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=24, T=6), seed=24)
     outs, kps = {}, {}
-    for sv in ("0", "1"):  # F = 64 fuses only on request (MSW_UNPOOL_FUSE=2)
-        monkeypatch.setenv("MSW_UNPOOL_FUSE", sv if sv == "0" or F == 32 else "2")
+    for sv in ("0", "1"):
+        monkeypatch.setenv("MSW_UNPOOL_FUSE", sv)
         m = _hip(build_msgnn(4, F, 4, **kw), cuda)
         gd = ga.to(cuda)
         with torch.no_grad():

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing of engine variants on the GPU box: one bench run per environment setting.
-#   bash tools/ab.sh "" "MSW_HOP_CHAINS=2" "MSW_HOP_CHAINS=3" [-- bench args]
+#   bash tools/ab.sh "" "MSW_POOL_FUSE=0" "MSW_UNPOOL_FUSE=0" [-- bench args]
 # Each run has its own time limit; a failure stops the script.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out

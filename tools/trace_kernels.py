@@ -78,14 +78,14 @@ def main():
     S = desc["num_scales"]
     cases = [("encode", 0)] + [(k, s) for s in range(S) for k in ("edge_hop", "hop")] + \
         [("pool", s) for s in range(1, S)] + [("unpool", s) for s in range(S - 1)] + \
-        [("hopm", s) for s in range(1, S)] + [("hop", s) for s in range(S)]
+        [("hop", s) for s in range(S)]
     for kern, scale in cases:
         try:
             for rep in range(3):  # the last repetition is reported (warm caches)
                 buf.zero_()
                 plan.bench_kernel(kern, scale, 1)
                 torch.cuda.synchronize()
-        except RuntimeError as e:  # e.g. no hop chain on that scale (chains are opt-in: MSW_HOP_CHAINS)
+        except RuntimeError as e:  # e.g. pooling fused into the coarse scale's first launch
             print(f"{kern:9s} scale {scale}: n/a ({e})")
             continue
         t = buf.cpu().tolist()
