@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = ["csrc/kernels_nt1.hip", "csrc/kernels_nt2.hip", "csrc/kernels_nt4.hip",
        "csrc/kernels_common.hip", "csrc/plan.hip", "csrc/metrics.hip", "csrc/train.hip"]
-HDR = ["csrc/engine.h", "csrc/kernels_impl.h", "csrc/tiling.h", os.path.join(ROOT, "include", "mswegnn.h")]
+HDR = ["csrc/engine.h", "csrc/kernels_impl.h", "csrc/tiling.h", "csrc/graph_build.h", os.path.join(ROOT, "include", "mswegnn.h")]
 ARCH = os.environ.get("MSW_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
          "-I", os.path.join(ROOT, "include")]

@@ -5,16 +5,16 @@
 #include <stdint.h>
 #include <algorithm>
 
+#include "graph_build.h"  // kRowsPerWave, kMaxScales and the host-built records (LaneRec, ...)
+
 namespace msw {
 
 constexpr int kMaxLayers = 4;
-constexpr int kRowsPerWave = 16;  // v_mfma_f32_16x16x4_f32: 16 rows (nodes / edges) per wave
 #ifndef MSW_WAVES
 #define MSW_WAVES 4
 #endif
 constexpr int kWaves = MSW_WAVES;  // waves per block (tiles per workgroup)
 constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
-constexpr int kMaxScales = 8;
 
 // One packed layer of an MFMA chain.  `a_off` indexes the packed A operand
 // [tout][tin][lane][4] (floats, 16-feature tiles) in the weight blob, `b_off` a bias
@@ -125,28 +125,6 @@ struct EncodeArgs {
   int coop;                // = NT: k_encode_coop (NT waves per 16-row tile), else k_encode
 };
 
-// Edge tile: whole destination neighbourhoods, <= 16 edges and <= 16 destinations (host).
-struct TileRange {
-  int node0, nnode, edge0, nedge;  // local node index / local CSR edge index
-};
-// What lane j of a tile's wave needs, one 16-B load: as edge lane, edge slot j of the tile
-// (source row, local lane of its destination); as node lane, destination j (row, slot
-// range [q & 255, q >> 8) of its in-edges).  Per-edge arrays (Pe, s) are tile-padded:
-// edge slot j of tile t lives at row 16 t + j.
-// Dense edge chunks of a scale (k_edge_mlp): 16 consecutive real edges of the tile order,
-// padding slots skipped; src / dst internal rows and the edge's tile-padded slot p
-// (-1 = past the last edge).
-struct EdgeChunk {
-  int src, dst, p, pad;
-};
-
-struct LaneRec {
-  int src;  // internal source row, -1 = no edge in this slot
-  int dl;   // destination lane (0..15) of the edge
-  int n;    // internal destination row, -1 = no node in this lane
-  int q;    // q0 | q1 << 8
-};
-
 struct Epilogue {
   int post_act; float post_slope;  // GNN: gnn_activation after every SWEGNN layer
   NpDesc np;                       // projection of the next layer from [x_s; out]
@@ -156,22 +134,7 @@ struct Epilogue {
 
 // Fused: edge MLP (s_ij for every edge, stored for the later hops) + hop 1
 // (+ epilogue when the layer has K = 1; intra-scale unpooling is such a layer).
-// Children of one coarse row (32 B, one 16-B + one 8-B load): the first kPoolInline
-// internal fine rows, the count, and where the full list starts in PoolArgs::child.
-constexpr int kPoolInline = 4;
-struct alignas(16) PoolRec {
-  int c[kPoolInline];
-  int cnt, off, pad[2];
-};
-
-// Pooling fused into the coarse scale's first edge-MLP + hop launch (k_edge_coop, POOL):
-// per tile-padded edge slot of the coarse scale, the children of the slot's source (edge
-// lane) and of the lane's destination (node lane), as PoolRec (absent: cnt 0, children =
-// a safe fine row).  The launch forms the mean of the children and the projection of the
-// processor (U, V, O) itself instead of reading them from a pooling launch's output.
-struct alignas(16) PoolSlot {
-  PoolRec src, dst;
-};
+// Records built on the host (graph_build.h): LaneRec, EdgeChunk, PoolRec, PoolSlot.
 struct PoolFuse {
   const PoolSlot* slots;           // [ntiles][16], null = not fused
   const int* child;                // internal fine rows, reference order (PoolArgs::child)

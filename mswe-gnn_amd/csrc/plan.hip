@@ -43,7 +43,6 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 inline int tiles16(int n) { return (n + 15) / 16; }
-inline int round64(int n) { return (n + kRowsPerBlock - 1) / kRowsPerBlock * kRowsPerBlock; }
 
 struct Blob {
   std::vector<float> h;
@@ -136,52 +135,6 @@ hipError_t rowmlp_dispatch(int NT, const RowMlpArgs& ra, hipStream_t st = nullpt
     case 2: return launch_rowmlp<2>(ra, st);
     default: return launch_rowmlp<4>(ra, st);
   }
-}
-
-// Edge tiles over a CSR by destination: consecutive destinations with <= 16 in-edges and
-// <= 16 destinations per tile (whole neighbourhoods, so hop 1 fuses into the edge MLP).
-int build_tiles(const std::vector<int>& rowptr, std::vector<TileRange>& out) {
-  out.clear();
-  const int ns = (int)rowptr.size() - 1;
-  int a = 0;
-  while (a < ns) {
-    int b = a, edges = 0;
-    while (b < ns && b - a < kRowsPerWave) {
-      const int d = rowptr[b + 1] - rowptr[b];
-      if (d > kRowsPerWave) return fail(MSW_ERR_UNSUPPORTED, "node with more than 16 in-edges");
-      if (edges + d > kRowsPerWave) break;
-      edges += d;
-      ++b;
-    }
-    out.push_back(TileRange{a, b - a, rowptr[a], edges});
-    a = b;
-  }
-  return MSW_OK;
-}
-
-// Per-lane tile records (engine.h LaneRec) of a CSR by destination: `src` = source row of
-// CSR edge i (internal numbering), `n0` = first internal row of the destination scale.
-// porig (optional) receives, per tile-padded edge slot, the CSR position or -1.
-std::vector<LaneRec> make_recs(const std::vector<int>& rowptr, const std::vector<int>& src, int n0,
-                               const std::vector<TileRange>& tiles, std::vector<int>* porig) {
-  std::vector<LaneRec> r(tiles.size() * kRowsPerWave, LaneRec{-1, 0, -1, 0});
-  if (porig) porig->assign(tiles.size() * kRowsPerWave, -1);
-  for (size_t t = 0; t < tiles.size(); ++t) {
-    const TileRange& tr = tiles[t];
-    LaneRec* L = &r[t * kRowsPerWave];
-    for (int j = 0; j < tr.nnode; ++j) {
-      const int k = tr.node0 + j;
-      const int q0 = rowptr[k] - tr.edge0, q1 = rowptr[k + 1] - tr.edge0;
-      L[j].n = n0 + k;
-      L[j].q = q0 | (q1 << 8);
-      for (int q = q0; q < q1; ++q) {
-        L[q].src = src[tr.edge0 + q];
-        L[q].dl = j;
-        if (porig) (*porig)[t * kRowsPerWave + q] = tr.edge0 + q;
-      }
-    }
-  }
-  return r;
 }
 
 }  // namespace
@@ -453,17 +406,14 @@ int pupload(msw_plan* P, T** p, const std::vector<T>& v) {
   if (!rc) P->owned.push_back(*p);
   return rc;
 }
-
-// Stable counting sort by key in [0, nkeys): rowptr + order (original indices).
-void csr_build(int nkeys, const std::vector<int>& key, std::vector<int>& rowptr,
-               std::vector<int>& order) {
-  rowptr.assign(nkeys + 1, 0);
-  for (int k : key) rowptr[k + 1]++;
-  for (int i = 0; i < nkeys; ++i) rowptr[i + 1] += rowptr[i];
-  std::vector<int> pos(rowptr.begin(), rowptr.end() - 1);
-  order.assign(key.size(), 0);
-  for (size_t e = 0; e < key.size(); ++e) order[pos[key[e]]++] = (int)e;
+// host I2 pairs (graph_build.h) into a device int2 array (same layout)
+int pupload(msw_plan* P, int2** p, const std::vector<I2>& v) {
+  static_assert(sizeof(I2) == sizeof(int2), "I2 mirrors int2");
+  int rc = palloc(P, p, v.size());
+  if (!rc && !v.empty()) HIP_TRY(hipMemcpy(*p, v.data(), v.size() * sizeof(I2), hipMemcpyHostToDevice));
+  return rc;
 }
+
 
 // SWEGNN layer -> packed Proc (gnn.py:352-445).
 int build_proc(msw_plan* P, const msw_swegnn& g, int scale, bool intra, Proc& pr) {
@@ -1276,184 +1226,40 @@ void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
 }
 
 int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
-  const int S = P->S, G = g->num_graphs;
-  if (S > kMaxScales) return fail(MSW_ERR_UNSUPPORTED, "more than 8 scales");
-  if (g->num_nodes <= 0 || g->num_nodes > (1LL << 30)) return fail(MSW_ERR_INVALID, "num_nodes out of range");
-  if (g->num_edges < 0 || g->num_edges > (1LL << 31) - 64) return fail(MSW_ERR_INVALID, "num_edges out of range");
-  if (G < 1 || !g->node_ptr) return fail(MSW_ERR_INVALID, "node_ptr missing");
-  if (g->num_scales != S) return fail(MSW_ERR_INVALID, "graph num_scales != model num_scales");
-  const int N = (int)g->num_nodes;
-  P->N = N;
-  P->E = g->num_edges;
-  // internal numbering: scale-major (graph-major inside a scale), scale starts padded to
-  // multiples of 16 rows so that every 16-row wave tile lies in one scale
-  // (each graph's destinations of a scale in pack_order; MSW_TILE_PACK=0: graph order)
-  P->perm.clear();
+  // the host plan (graph_build.h: numbering, CSRs, tiles, records -- also built by the
+  // sanitizer harness tests/asan/host_plan_check.cpp), then its device copies
+  HostGraph H;
+  std::string err;
+  int rc = build_host_graph(g, P->S, kRowsPerBlock, P->kn.tile_pack != 0,
+                            row_hops_forced(P) ? 0 : kRowHopMinTiles, H, err);
+  if (rc) return fail(rc, err);
+  P->N = H.N;
+  P->E = H.E;
+  P->Npad = H.Npad;
+  P->perm = std::move(H.perm);
+  P->iperm = std::move(H.iperm);
+  const int S = P->S;
   P->sc.assign(S, ScaleCSR{});
-  const bool pack = P->kn.tile_pack != 0;
-  std::vector<int> indeg(pack ? N : 0, 0);
-  if (pack)
-    for (int64_t e = 0; e < g->num_edges; ++e) {
-      const int64_t cl = g->edge_index[g->num_edges + e];
-      if (cl >= 0 && cl < N) ++indeg[cl];
-    }
   for (int s = 0; s < S; ++s) {
-    P->sc[s].n0 = (int)P->perm.size();
-    for (int gi = 0; gi < G; ++gi) {
-      const int64_t a = g->node_ptr[gi * (S + 1) + s], b = g->node_ptr[gi * (S + 1) + s + 1];
-      if (a < 0 || b < a || b > N) return fail(MSW_ERR_INVALID, "node_ptr out of range");
-      if (pack) {
-        std::vector<int> d((size_t)(b - a));
-        for (int64_t v = a; v < b; ++v) d[v - a] = indeg[v];
-        for (int k : pack_order(d)) P->perm.push_back((int)(a + k));
-      } else {
-        for (int64_t v = a; v < b; ++v) P->perm.push_back((int)v);
-      }
-    }
-    P->sc[s].ns = (int)P->perm.size() - P->sc[s].n0;
-    P->perm.resize(round64((int)P->perm.size()), -1);
-  }
-  P->Npad = (int)P->perm.size();
-  P->iperm.assign(N, -1);
-  int covered = 0;
-  for (int i = 0; i < P->Npad; ++i) {
-    if (P->perm[i] < 0) continue;
-    if (P->iperm[P->perm[i]] != -1) return fail(MSW_ERR_INVALID, "node_ptr ranges overlap");
-    P->iperm[P->perm[i]] = i;
-    ++covered;
-  }
-  if (covered != N) return fail(MSW_ERR_INVALID, "node_ptr does not cover every node exactly once");
-  // per-scale CSR by destination + edge tiles
-  const int64_t E = g->num_edges;
-  if (g->edge_ptr[0] != 0 || g->edge_ptr[S] != E) return fail(MSW_ERR_INVALID, "edge_ptr must span [0, E]");
-  int rc;
-  for (int s = 0; s < S; ++s) {
+    HostScale& h = H.sc[s];
     ScaleCSR& c = P->sc[s];
-    const int64_t a = g->edge_ptr[s], b = g->edge_ptr[s + 1];
-    if (b < a) return fail(MSW_ERR_INVALID, "edge_ptr not monotone");
-    c.E = (int)(b - a);
-    std::vector<int> key(c.E), srcv(c.E);
-    for (int64_t e = a; e < b; ++e) {
-      const int64_t r = g->edge_index[e], cl = g->edge_index[E + e];
-      if (r < 0 || r >= N || cl < 0 || cl >= N) return fail(MSW_ERR_INVALID, "edge_index out of range");
-      const int ri = P->iperm[r], ci = P->iperm[cl];
-      if (ri < c.n0 || ri >= c.n0 + c.ns || ci < c.n0 || ci >= c.n0 + c.ns)
-        return fail(MSW_ERR_INVALID, "edge of scale " + std::to_string(s) + " leaves the scale");
-      key[e - a] = ci - c.n0;
-      srcv[e - a] = ri;
-    }
-    std::vector<int> rowptr, order;
-    csr_build(c.ns, key, rowptr, order);
-    std::vector<int> so(c.E);
-    for (int i = 0; i < c.E; ++i) so[i] = srcv[order[i]];
-    std::vector<TileRange> tl;
-    if ((rc = build_tiles(rowptr, tl))) return rc;
-    c.ntiles = (int)tl.size();
-    std::vector<int> pcsr;
-    const std::vector<LaneRec> recs = make_recs(rowptr, so, c.n0, tl, &pcsr);
-    c.porig.assign(pcsr.size(), -1);
-    for (size_t q = 0; q < pcsr.size(); ++q)
-      if (pcsr[q] >= 0) c.porig[q] = (int)(a + order[pcsr[q]]);
-    if ((rc = pupload(P, &c.recs, recs))) return rc;
-    c.hrecs = recs;
-    {
-      std::vector<EdgeChunk> ck;
-      for (size_t q = 0; q < recs.size(); ++q)
-        if (recs[q].src >= 0)
-          ck.push_back(EdgeChunk{recs[q].src, recs[q / kRowsPerWave * kRowsPerWave + recs[q].dl].n, (int)q, 0});
-      c.nchunks = (int)((ck.size() + kRowsPerWave - 1) / kRowsPerWave);
-      ck.resize((size_t)c.nchunks * kRowsPerWave, EdgeChunk{-1, -1, -1, 0});
-      if (c.nchunks > 0 && (rc = pupload(P, &c.chunks, ck))) return rc;
-    }
-    if (c.ntiles >= kRowHopMinTiles || row_hops_forced(P)) {  // row-layout middle hops: CSR + s slots
-      std::vector<int> slot_of_csr(c.E, -1);
-      for (size_t q = 0; q < pcsr.size(); ++q)
-        if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
-      std::vector<int2> re(std::max(c.E, 1));
-      for (int i = 0; i < c.E; ++i) re[i] = int2{so[i], slot_of_csr[i]};
-      if ((rc = pupload(P, &c.rptr, rowptr)) || (rc = pupload(P, &c.redge, re))) return rc;
-    }
+    c.n0 = h.n0; c.ns = h.ns; c.E = h.E; c.ntiles = h.ntiles; c.nchunks = h.nchunks;
+    if ((rc = pupload(P, &c.recs, h.recs))) return rc;
+    if (c.nchunks > 0 && (rc = pupload(P, &c.chunks, h.chunks))) return rc;
+    if (!h.rptr.empty() && ((rc = pupload(P, &c.rptr, h.rptr)) || (rc = pupload(P, &c.redge, h.redge)))) return rc;
+    c.porig = std::move(h.porig);
+    c.hrecs = std::move(h.recs);
   }
-  // intra-scale levels
   P->lv.assign(S > 1 ? S - 1 : 0, LevelMaps{});
-  if (S > 1) {
-    if (!g->intra_edge_index || !g->intra_edge_ptr) return fail(MSW_ERR_INVALID, "intra edges missing");
-    const int64_t I = g->num_intra_edges;
-    for (int l = 0; l < S - 1; ++l) {
-      LevelMaps& m = P->lv[l];
-      const ScaleCSR& cs = P->sc[l + 1];
-      const ScaleCSR& fs = P->sc[l];
-      const int64_t a = g->intra_edge_ptr[l], b = g->intra_edge_ptr[l + 1];
-      if (a < 0 || b < a || b > I) return fail(MSW_ERR_INVALID, "intra_edge_ptr out of range");
-      m.I = (int)(b - a);
-      std::vector<int> ck(m.I), fk(m.I), cv(m.I), fv(m.I);
-      for (int64_t e = a; e < b; ++e) {
-        const int64_t co = g->intra_edge_index[e], fi = g->intra_edge_index[I + e];
-        if (co < 0 || co >= N || fi < 0 || fi >= N) return fail(MSW_ERR_INVALID, "intra edge out of range");
-        const int ci = P->iperm[co], fii = P->iperm[fi];
-        if (ci < cs.n0 || ci >= cs.n0 + cs.ns || fii < fs.n0 || fii >= fs.n0 + fs.ns)
-          return fail(MSW_ERR_INVALID, "intra edge of level " + std::to_string(l) + " not (coarse, fine)");
-        ck[e - a] = ci - cs.n0;
-        fk[e - a] = fii - fs.n0;
-        cv[e - a] = ci;
-        fv[e - a] = fii;
-      }
-      std::vector<int> rp, order;
-      csr_build(cs.ns, ck, rp, order);
-      std::vector<int> child(m.I);
-      for (int i = 0; i < m.I; ++i) child[i] = fv[order[i]];
-      std::vector<PoolRec> pr((size_t)(cs.ns + 15) / 16 * 16);
-      for (size_t i = 0; i < pr.size(); ++i) {
-        PoolRec& r = pr[i];
-        const int b = i < (size_t)cs.ns ? rp[i] : 0, e = i < (size_t)cs.ns ? rp[i + 1] : 0;
-        r.cnt = e - b;
-        r.off = b;
-        for (int k = 0; k < kPoolInline; ++k) r.c[k] = k < e - b ? child[b + k] : -1;
-      }
-      std::vector<TileRange> pt;
-      if ((rc = build_tiles(rp, pt))) return rc;
-      m.pool_etiles = (int)pt.size();
-      if ((rc = pupload(P, &m.pool_erecs, make_recs(rp, child, cs.n0, pt, nullptr)))) return rc;
-      if (child.empty()) child.push_back(0);
-      if ((rc = pupload(P, &m.pool_recs, pr)) || (rc = pupload(P, &m.pool_child, child))) return rc;
-      if (!cs.hrecs.empty()) {  // fused pooling: the records of each slot's two coarse nodes
-        auto rec_of = [&](int row) {
-          PoolRec r{};
-          r.cnt = 0; r.off = 0;
-          if (row >= cs.n0 && row < cs.n0 + cs.ns) r = pr[row - cs.n0];
-          const int safe = r.cnt > 0 ? r.c[0] : fs.n0;  // absent children re-read a real row
-          for (int k = 0; k < kPoolInline; ++k) if (k >= r.cnt) r.c[k] = safe;
-          return r;
-        };
-        std::vector<PoolSlot> ps(cs.hrecs.size());
-        for (size_t q = 0; q < ps.size(); ++q) {
-          ps[q].src = rec_of(cs.hrecs[q].src);
-          ps[q].dst = rec_of(cs.hrecs[q].n);
-        }
-        if ((rc = pupload(P, &m.pool_slots, ps))) return rc;
-      }
-      csr_build(fs.ns, fk, rp, order);
-      std::vector<int> us(m.I);
-      for (int i = 0; i < m.I; ++i) us[i] = cv[order[i]];
-      std::vector<TileRange> tl;
-      if ((rc = build_tiles(rp, tl))) return rc;
-      m.un_ntiles = (int)tl.size();
-      if ((rc = pupload(P, &m.un_recs, make_recs(rp, us, fs.n0, tl, nullptr)))) return rc;
-      {  // fused unpooling: one parent per fine node at most (else the launch stays)
-        bool one = true;
-        std::vector<int> par(fs.ns, -1);
-        for (int i = 0; i < fs.ns; ++i) {
-          if (rp[i + 1] - rp[i] > 1) one = false;
-          if (rp[i + 1] > rp[i]) par[i] = us[rp[i]];
-        }
-        if (one && !fs.hrecs.empty()) {
-          auto par_of = [&](int row) { return row >= fs.n0 && row < fs.n0 + fs.ns ? par[row - fs.n0] : -1; };
-          std::vector<int2> pv(fs.hrecs.size());
-          for (size_t q = 0; q < pv.size(); ++q) pv[q] = int2{par_of(fs.hrecs[q].src), par_of(fs.hrecs[q].n)};
-          if ((rc = pupload(P, &m.parent_slots, pv))) return rc;
-        }
-      }
-    }
+  for (int l = 0; l + 1 < S; ++l) {
+    HostLevel& h = H.lv[l];
+    LevelMaps& m = P->lv[l];
+    m.I = h.I; m.pool_etiles = h.pool_etiles; m.un_ntiles = h.un_ntiles;
+    if ((rc = pupload(P, &m.pool_erecs, h.pool_erecs)) || (rc = pupload(P, &m.pool_recs, h.pool_recs)) ||
+        (rc = pupload(P, &m.pool_child, h.pool_child)) || (rc = pupload(P, &m.un_recs, h.un_recs)))
+      return rc;
+    if (!h.pool_slots.empty() && (rc = pupload(P, &m.pool_slots, h.pool_slots))) return rc;
+    if (!h.parent_slots.empty() && (rc = pupload(P, &m.parent_slots, h.parent_slots))) return rc;
   }
   return MSW_OK;
 }
@@ -1529,42 +1335,27 @@ namespace {
 
 // Partitioned mesh: per-scale receive / send row lists (local graph rows -> internal rows).
 int build_exchange(msw_plan* P, const msw_exchange_desc* d) {
+  // the lists (graph_build.h build_host_exchange, validated against the plan's numbering)
+  HostGraph H;  // the numbering only
+  H.N = P->N;
+  H.iperm = P->iperm;
+  H.sc.resize(P->S);
+  for (int s = 0; s < P->S; ++s) { H.sc[s].n0 = P->sc[s].n0; H.sc[s].ns = P->sc[s].ns; }
+  std::vector<HostXchScale> X;
+  std::string err;
+  int rc = build_host_exchange(H, P->part_rank, d, X, err);
+  if (rc) return fail(rc, err);
   P->xch.assign(P->S, msw_plan::XchScale{});
-  std::vector<std::vector<int>> rr(P->S), ss(P->S);
-  for (int i = 0; i < d->num_entries; ++i) {
-    const int s = d->scale[i];
-    if (s < 0 || s >= P->S) return fail(MSW_ERR_INVALID, "exchange entry with a bad scale");
-    const ScaleCSR& c = P->sc[s];
-    msw_plan::XchPeer pe{d->peer[i], (int)rr[s].size(), (int)(d->recv_ptr[i + 1] - d->recv_ptr[i]),
-                         (int)ss[s].size(), (int)(d->send_ptr[i + 1] - d->send_ptr[i])};
-    if (pe.peer < 0 || pe.peer == P->part_rank) return fail(MSW_ERR_INVALID, "exchange entry with a bad peer");
-    auto conv = [&](const int32_t* rows, int64_t a, int64_t b, std::vector<int>& dst) -> int {
-      for (int64_t k = a; k < b; ++k) {
-        const int r = rows[k];
-        if (r < 0 || r >= P->N) return fail(MSW_ERR_INVALID, "exchange row out of range");
-        const int in = P->iperm[r];
-        if (in < c.n0 || in >= c.n0 + c.ns) return fail(MSW_ERR_INVALID, "exchange row not on the entry's scale");
-        dst.push_back(in);
-      }
-      return MSW_OK;
-    };
-    int rc;
-    if ((rc = conv(d->recv_rows, d->recv_ptr[i], d->recv_ptr[i + 1], rr[s])) ||
-        (rc = conv(d->send_rows, d->send_ptr[i], d->send_ptr[i + 1], ss[s])))
-      return rc;
-    P->xch[s].peers.push_back(pe);
-  }
   size_t most = 1;
   for (int s = 0; s < P->S; ++s) {
-    msw_plan::XchScale& X = P->xch[s];
-    X.nrecv = (int)rr[s].size();
-    X.nsend = (int)ss[s].size();
-    int rc;
-    if ((rc = pupload(P, &X.recv_rows, rr[s])) || (rc = pupload(P, &X.send_rows, ss[s]))) return rc;
-    most = std::max(most, (size_t)std::max(X.nrecv, X.nsend));
+    msw_plan::XchScale& Y = P->xch[s];
+    Y.nrecv = (int)X[s].recv_rows.size();
+    Y.nsend = (int)X[s].send_rows.size();
+    for (const XchPeer& pe : X[s].peers) Y.peers.push_back(msw_plan::XchPeer{pe.peer, pe.roff, pe.rcount, pe.soff, pe.scount});
+    if ((rc = pupload(P, &Y.recv_rows, X[s].recv_rows)) || (rc = pupload(P, &Y.send_rows, X[s].send_rows))) return rc;
+    most = std::max(most, (size_t)std::max(Y.nrecv, Y.nsend));
   }
   const size_t floats = most * 2 * P->F;  // widest exchanged row: U (2F)
-  int rc;
   if ((rc = palloc(P, &P->xsend, floats)) || (rc = palloc(P, &P->xrecv, floats))) return rc;
   return MSW_OK;
 }
