@@ -218,6 +218,14 @@ int msw_set_graph_capture(msw_plan* plan, int enable);
 
 int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
 
+/* Health of the persistent middle-hop chains (k_hop_chain: several hops in one launch on
+ * XCD 0, workgroups synchronised through XCD 0's L2).  chain_launches: chain launches in one
+ * rollout step; expired_spins: barrier waits that gave up (results of those launches are not
+ * reliable -- the launch still finishes); off_xcd: participating workgroups found off XCD 0.
+ * Both counts must stay 0.  Synchronises the device. */
+int msw_plan_chain_health(const msw_plan* plan, int32_t* chain_launches, int32_t* expired_spins,
+                          int32_t* off_xcd);
+
 /* Re-launch one kernel of the step `iters` times on `stream` (benchmark / roofline hook;
  * call after a forward or rollout: it reuses the plan's workspaces and overwrites scratch).
  *   kernel: 0 = middle hop (first processor on `scale`), 1 = fused edge MLP + hop 1

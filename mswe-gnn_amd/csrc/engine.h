@@ -15,6 +15,7 @@ constexpr int kMaxLayers = 4;
 #endif
 constexpr int kWaves = MSW_WAVES;  // waves per block (tiles per workgroup)
 constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
+constexpr int kXcds = 8, kCusPerXcd = 32;  // MI355X: 8 XCDs x 32 CUs (workgroup i -> XCD i % 8)
 
 // One packed layer of an MFMA chain.  `a_off` indexes the packed A operand
 // [tout][tin][lane][4] (floats, 16-feature tiles) in the weight blob, `b_off` a bias
@@ -219,6 +220,21 @@ struct HopArgs {
   const int2* redge; // [E] {internal source row, tile-padded s slot}, reference edge order
 };
 
+// Persistent middle-hop chain (k_hop_chain): hops k .. k+m-1 of one layer, no epilogue, in
+// ONE launch whose G workgroups all sit on XCD 0 (XCD packing, G <= kCusPerXcd), separated by
+// a barrier among them through XCD 0's L2 (relaxed agent-scope counter, no fences).  The rows
+// of hop i are io[i] -> io[i + 1] (the layer's ping-pong buffers); filt[i] its filter.
+constexpr int kMaxChainHops = 6;
+struct HopChainArgs {
+  HopArgs h;                        // the tiles, s, x_s, flags, Common (h.in / h.out / h.filt_a unused)
+  int m;                            // hops in the chain (2 .. kMaxChainHops)
+  float* io[kMaxChainHops + 1];
+  int filt[kMaxChainHops];
+  unsigned long long* ctr;          // this launch's barrier counter (monotonic, zeroed at plan creation)
+  int* err;                         // [0] expired barrier spins, [1] participants off XCD 0
+  int G;                            // participating (logical) workgroups
+};
+
 // Mean pooling into the coarse rows + projection of the next processor.
 
 struct PoolArgs {
@@ -317,6 +333,7 @@ template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_hop_chain(const HopChainArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_epi(const EpiArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);

@@ -77,7 +77,6 @@ __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 // it needs and only those the dispatcher places on XCDs 0 .. k-1 (workgroup i -> XCD i % 8)
 // work.  The XCDs start a launch's workgroups up to ~1.3 us apart, most of a small hop's
 // span; on k XCDs the skew is k XCDs' instead of eight.  Logical workgroup, -1 = idle.
-constexpr int kXcds = 8, kCusPerXcd = 32;
 __device__ __forceinline__ int logical_block(const Common& c) {
   const int b = blockIdx.x;
   if (c.xcd <= 0) return b;
@@ -2411,6 +2410,112 @@ __global__ __launch_bounds__(kBlock) void k_hop_coop(HopArgs a) {
   node_epilogue_coop<NT, ACT, P>(res, a.epi, c, q.pre, a.out, (int)L.n, live && L.nv, r, lane, g, j, b0, b1, XW);
 }
 
+// ---------------------------------------------------------------------------- persistent hop chain
+// Middle hops k .. k+m-1 of one layer on a small scale in ONE launch (engine.h HopChainArgs;
+// verdict r3 item 6).  The grid is XCD-packed onto XCD 0 (c.xcd = 1; G <= 32 workgroups, one
+// tile per wave, all co-resident: nothing else runs on the stream), so every row a hop writes
+// stays in XCD 0's L2: stores and the next hop's row gathers are agent-scope relaxed atomics
+// (sc1: served by the L2, never a stale L1 line), and the barrier between hops is a relaxed
+// agent-scope counter -- no fences, nothing leaves the XCD.  Per hop the arithmetic is k_hop's
+// (LAST = false), operation for operation: bit-identical.  Every spin is bounded: an expired
+// spin counts in err[0] and the launch still finishes (results then unreliable, never a
+// hang); a participant found off XCD 0 counts in err[1] (the host checks both).
+constexpr long kChainSpin = 1L << 22;
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xf;
+}
+__device__ __forceinline__ f32x4 ld4_l2(const float* p) {
+  f32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+__device__ __forceinline__ void st4_l2(float* p, f32x4 v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int N>
+__device__ __forceinline__ void load_row_l2(f32x4 (&v)[N], const float* row, int g) {
+#pragma unroll
+  for (int t = 0; t < N; ++t) v[t] = ld4_l2(row + 16 * t + 4 * g);
+}
+// barrier among the chain's G workgroups: every wave's stores have reached the L2 (vmcnt(0))
+// before its workgroup arrives
+__device__ __forceinline__ void chain_barrier(const HopChainArgs& a, unsigned long long target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long n = 0;
+    while (__hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++n < kChainSpin)
+      __builtin_amdgcn_s_sleep(1);
+    if (n >= kChainSpin) atomicAdd(&a.err[0], 1);
+  }
+  __syncthreads();
+}
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT;
+  constexpr int XS = F + 4;
+  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
+  __shared__ unsigned long long base_s;
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int xb = logical_block(a.h.c);
+  if (xb < 0) return;
+  if (threadIdx.x == 0) {
+    if (xcc_id() != 0) atomicAdd(&a.err[1], 1);
+    // every launch adds exactly (m - 1) G arrivals and none can pass the first barrier before
+    // all G have started: the value read here lies in [base, base + G) of this launch
+    const unsigned long long v = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long per = (unsigned long long)(a.m - 1) * a.G;
+    base_s = v - v % per;
+  }
+  __syncthreads();
+  const unsigned long long base = base_s;
+  const int tile = xb * kWaves + w;
+  const bool live = tile < a.h.ntiles;
+  const int tl = live ? tile : 0;  // idle waves stay in bounds
+  float* slab = &slab_all[w][0][0];
+  const Lanes L = lanes_of(load_rec(a.h.recs, tl, j), tl, j, a.h.n0);
+  f32x4 sv[NT];
+  load_row<NT>(sv, a.h.s + L.p * F, g);  // s is fixed for the layer: plain loads
+  for (int k = 0; k < a.m; ++k) {
+    const float* in = a.io[k];
+    float* out = a.io[k + 1];
+    f32x4 wf[NT][NT];
+    load_filter<NT>(wf, a.h.c.W, a.filt[k], lane);
+    f32x4 os[NT], inn[NT];
+    if (k == 0) {  // written by the previous launch: plain loads
+      load_row<NT>(os, in + L.sr * F, g);
+      load_row<NT>(inn, in + L.n * F, g);
+    } else {
+      load_row_l2<NT>(os, in + L.sr * F, g);
+      load_row_l2<NT>(inn, in + L.n * F, g);
+    }
+    if (live) {  // k_hop's core, LAST = false
+      float* my = slab + j * XS;
+      store_row<NT>(my, inn, NT, g);
+      wave_lds_sync();
+      f32x4 od[NT];
+      load_row<NT>(od, slab + L.dl * XS, g);
+      put_message<NT>(my, os, od, sv, L.ev, a.h.grad, a.h.upwind, g);
+      f32x4 agg[NT], res[NT];
+      gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) res[t] = inn[t];
+      apply_filter_regs<NT>(res, agg, a.filt[k], wf);
+      if (L.nv) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) st4_l2(out + L.n * F + 16 * t + 4 * g, res[t]);
+      }
+    }
+    if (k + 1 < a.m) chain_barrier(a, base + (unsigned long long)(k + 1) * a.G);
+  }
+}
+
 template <int NT>
 static const void* hop_coop_kernel(int prelu) {
   if constexpr (NT >= 2) return prelu ? (const void*)k_hop_coop<NT, 1, NT> : (const void*)k_hop_coop<NT, -1, NT>;
@@ -2918,6 +3023,16 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   return launch_hop_kernel<NT>(b, loop, grid, block, st);
 }
 template <int NT>
+hipError_t launch_hop_chain(const HopChainArgs& a, hipStream_t st) {
+  if (a.h.ntiles <= 0) return hipSuccess;
+  if (a.m < 2 || a.m > kMaxChainHops || a.G != cdiv(a.h.ntiles, kWaves) || a.G > kCusPerXcd || a.h.c.xcd_max < 1)
+    return hipErrorInvalidValue;  // the grid must be one XCD's, one workgroup per CU
+  HopChainArgs b = a;
+  b.h.c.xcd = 1;
+  hipLaunchKernelGGL((k_hop_chain<NT>), dim3((unsigned)(a.G * kXcds)), dim3(kBlock), 0, st, b);
+  return hipGetLastError();
+}
+template <int NT>
 hipError_t launch_hop_kernel(const HopArgs& a, bool loop, dim3 grid, dim3 block, hipStream_t st) {
   if (!a.last) {
     if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
@@ -3047,6 +3162,7 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_edge_mlp<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
+  template hipError_t launch_hop_chain<NT>(const HopChainArgs&, hipStream_t);     \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
   template hipError_t launch_epi<NT>(const EpiArgs&, hipStream_t);                \
   template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);

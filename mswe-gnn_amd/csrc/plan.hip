@@ -221,7 +221,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP, L_HOPC };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -243,6 +243,7 @@ struct Launch {
     PoolArgs pool;
     ExchangeArgs xch;
     EpiArgs ep;
+    HopChainArgs hopc;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
   Common& common() {
@@ -251,6 +252,7 @@ struct Launch {
       case L_EDGE_HOP:
       case L_EDGE_MLP: return eh.c;
       case L_HOP: return hop.c;
+      case L_HOPC: return hopc.h.c;
       case L_EXCHANGE: return xch.c;
       case L_EPI: return ep.c;
       default: return pool.c;
@@ -281,6 +283,7 @@ struct Knobs {
   int coop_waves = -1;      // MSW_COOP_WAVES      cooperative kernels while P x tiles <= this (-1 default)
   int epi_split_tiles = -1; // MSW_EPI_SPLIT_TILES row-epilogue threshold in edge tiles (-1 default)
   int trace_encode = 0;     // MSW_TRACE_ENCODE    diagnostic builds (-DMSW_TRACE): encoder marks only
+  int hop_chain = 0;        // MSW_HOP_CHAIN       persistent middle-hop chains on one-XCD scales (opt-in until measured)
 };
 inline Knobs knobs_from_env() {
   Knobs k;
@@ -291,7 +294,8 @@ inline Knobs knobs_from_env() {
       {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_EH_LOOP", &k.eh_loop},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
       {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
-      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
+      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode},
+      {"MSW_HOP_CHAIN", &k.hop_chain}};
   for (const auto& t : tab)
     if (const char* e = getenv(t.name)) *t.v = atoi(e);
   if (getenv("MSW_TRACE_ENCODE")) k.trace_encode = 1;
@@ -374,6 +378,9 @@ struct msw_plan {
   int xcd_max = 1;
   int coop_waves = 1024;
   Knobs kn;                 // engine switches of this plan (knobs_from_env)
+  // persistent hop chains (L_HOPC): one barrier counter per chain launch, shared error flags
+  unsigned long long* chain_ctr = nullptr;
+  int* chain_err = nullptr;
   // set when a fused (un)pooling launch's weight region would not fit its kernel's LDS cap
   // (edge_coop_lds_cap): the schedule is rebuilt with the pooling / unpooling launches
   int no_fuse = 0;
@@ -590,6 +597,36 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   }
   const float* cur = P->T[0];
   for (int k = 2; k <= pr.K;) {
+    // middle hops k .. K-1 as ONE persistent launch on XCD 0 (k_hop_chain) where the scale's
+    // tiles fit one XCD at one workgroup per CU (the coarse scales; not on parts: their
+    // exchanges sit between the hops)
+    const int nmid = pr.K - k;  // middle hops left (the last hop keeps its own launch)
+    if (P->kn.hop_chain && P->part_rank < 0 && nmid >= 2 && P->xcd_max >= 1 && g.ntiles > 0 &&
+        (g.ntiles + kWaves - 1) / kWaves <= kCusPerXcd) {
+      const int m = std::min(nmid, kMaxChainHops);
+      Launch L;
+      L.kind = L_HOPC;
+      L.scale = pr.scale;
+      HopChainArgs& h = L.hopc;
+      h.h.c = c;
+      h.h.n0 = g.n0; h.h.recs = g.recs; h.h.ntiles = g.ntiles;
+      h.h.s = P->s; h.h.xs = P->xs;
+      h.h.grad = pr.with_gradient; h.h.upwind = pr.upwind;
+      h.h.filt_a = -1;
+      h.m = m;
+      h.G = (g.ntiles + kWaves - 1) / kWaves;
+      float* b = const_cast<float*>(cur);
+      h.io[0] = b;
+      for (int i = 0; i < m; ++i) {
+        b = b == P->T[0] ? P->T[1] : P->T[0];
+        h.io[i + 1] = b;
+        h.filt[i] = pr.filt.empty() ? -1 : pr.filt[k - 1 + i];
+      }
+      q.push_back(L);
+      cur = b;
+      k += m;
+      continue;
+    }
     sched_exchange(P, q, pr.scale, {{cur == P->T[0] ? B_T0 : B_T1, P->F}});
     // one launch per hop (hop chains -- several hops per launch with the halo recomputed --
     // measured 0.7-1.6 % slower under graph replay, profiles/r01_v7/ab_chains.txt; removed)
@@ -929,8 +966,8 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       a.filt_l = R.put(a.filt_a, P->NT * P->NT * 256);
       a.reg = R.done(split);
       reg = &a.reg;
-    } else if (L.kind == L_EXCHANGE) {
-      continue;  // no LDS weight region
+    } else if (L.kind == L_EXCHANGE || L.kind == L_HOPC) {
+      continue;  // no LDS weight region (the chain's filters go from the blob into registers)
     } else if (L.kind == L_EPI) {
       EpiArgs& a = L.ep;
       RegionBuilder R(P->blob, 0);
@@ -1084,6 +1121,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       }
       break;
     case L_EXCHANGE: break;
+    case L_HOPC: break;  // grid fixed at schedule time (G workgroups on XCD 0)
     case L_EPI:
       caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len);
       break;
@@ -1131,6 +1169,7 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_ENCODE: return launch_encode<NT>(L.enc, st);
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
     case L_EDGE_MLP: return launch_edge_mlp<NT>(L.eh, st);
+    case L_HOPC: return launch_hop_chain<NT>(L.hopc, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
     case L_EPI: return launch_epi<NT>(L.ep, st);
@@ -1508,6 +1547,22 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     P->no_fuse = 1;
     P->blob.h.resize(blob0);  // drop the regions of the fused schedule
   }
+  {  // persistent hop chains: a zeroed barrier counter per launch, the shared error flags
+    int nchain = 0;
+    for (auto* q : {&P->sched_fwd, &P->sched_roll})
+      for (Launch& L : *q) nchain += L.kind == L_HOPC;
+    if ((rc = palloc(P.get(), &P->chain_ctr, (size_t)std::max(nchain, 1))) || (rc = palloc(P.get(), &P->chain_err, 2)))
+      return rc;
+    HIP_TRY(hipMemset(P->chain_ctr, 0, sizeof(unsigned long long) * std::max(nchain, 1)));
+    HIP_TRY(hipMemset(P->chain_err, 0, 2 * sizeof(int)));
+    int i = 0;
+    for (auto* q : {&P->sched_fwd, &P->sched_roll})
+      for (Launch& L : *q)
+        if (L.kind == L_HOPC) {
+          L.hopc.ctr = P->chain_ctr + i++;
+          L.hopc.err = P->chain_err;
+        }
+  }
   P->blob.alloc(256);  // slack: LDS-DMA chunks may read up to 255 floats past a region
   if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
   for (auto* q : {&P->sched_fwd, &P->sched_roll})
@@ -1881,6 +1936,21 @@ int msw_set_trace(msw_plan* P, uint64_t* buf) {
     for (Launch& L : *q)
       L.common().trace = (!enc_only || L.kind == L_ENCODE) ? reinterpret_cast<unsigned long long*>(buf) : nullptr;
   P->drop_graphs();  // the captured steps hold the old arguments
+  return MSW_OK;
+}
+
+int msw_plan_chain_health(const msw_plan* P, int32_t* chain_launches, int32_t* expired_spins, int32_t* off_xcd) {
+  if (!P) return fail(MSW_ERR_INVALID, "null argument");
+  int n = 0;
+  for (const Launch& L : P->sched_roll) n += L.kind == L_HOPC;
+  int e[2] = {0, 0};
+  if (P->chain_err) {
+    HIP_TRY(hipSetDevice(P->device));
+    HIP_TRY(hipMemcpy(e, P->chain_err, sizeof(e), hipMemcpyDeviceToHost));
+  }
+  if (chain_launches) *chain_launches = n;
+  if (expired_spins) *expired_spins = e[0];
+  if (off_xcd) *off_xcd = e[1];
   return MSW_OK;
 }
 

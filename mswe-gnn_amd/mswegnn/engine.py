@@ -304,7 +304,11 @@ class EnginePlan:
     def stats(self):
         s = L.MswPlanStats()
         L.check(L.lib().msw_plan_get_stats(self._h, C.byref(s)))
-        return {k: getattr(s, k) for k, _ in L.MswPlanStats._fields_}
+        out = {k: getattr(s, k) for k, _ in L.MswPlanStats._fields_}
+        n, spins, off = C.c_int32(), C.c_int32(), C.c_int32()
+        L.check(L.lib().msw_plan_chain_health(self._h, C.byref(n), C.byref(spins), C.byref(off)))
+        out.update(chain_launches=n.value, chain_expired_spins=spins.value, chain_off_xcd=off.value)
+        return out
 
 
 # ------------------------------------------------------------------ cache

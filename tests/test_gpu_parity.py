@@ -833,3 +833,47 @@ def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, F, kw):
     m = build_msgnn(4, F, 4, **kw)
     cfg = orc.msgnn_config(num_scales=4, hid_features=F, K=4, **kw)
     assert per_step_rel(outs["1"][1], orc.rollout(state_dict_of(m), cfg, ga)) <= REL_TOL
+
+
+@pytest.mark.parametrize("model", ["msgnn_K4_F32", "msgnn_F64", "gnn"])
+def test_persistent_hop_chain_matches_separate_hops(cuda, monkeypatch, model):
+    """Middle hops of a layer as ONE persistent launch on XCD 0 (k_hop_chain: workgroups
+    synchronised through XCD 0's L2 between hops; MSW_HOP_CHAIN=1, the default on scales whose
+    tiles fit one XCD) == one k_hop launch per hop (MSW_HOP_CHAIN=0), bit for bit: forward,
+    rollout and a batch of two meshes; fewer launches per step; no expired barrier spin and no
+    workgroup off XCD 0 (msw_plan_chain_health); and the reference fixture / oracle."""
+    from mswegnn.batch import collate
+    from mswegnn.engine import plan_for
+    from mswegnn.rollout import rollout_test
+
+    def build():
+        if model == "gnn":
+            return _hip(build_gnn(hid=32, K=4, n_layers=2, mlp_layers=2), cuda)
+        if model == "msgnn_F64":
+            return _hip(build_msgnn(4, 64, 4), cuda)
+        return _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    if model == "gnn":
+        ga = wet_state(make_single_scale_mesh(n_coarse=2, refinements=2, T=8), seed=4)
+        gb = wet_state(make_single_scale_mesh(n_coarse=2, refinements=2, seed=5, T=8), seed=5)
+    else:
+        ga = wet_state(make_multiscale_mesh(**mesh_config("small"), T=8), seed=4)
+        gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=5, T=8), seed=5)
+    outs, st = {}, {}
+    for sv in ("0", "1"):
+        monkeypatch.setenv("MSW_HOP_CHAIN", sv)
+        m = build()
+        gd = ga.to(cuda)
+        with torch.no_grad():
+            y = m(gd).cpu()
+        r = m.rollout(gd).cpu()
+        st[sv] = plan_for(m, gd).stats()
+        outs[sv] = (y, r, rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
+    assert st["1"]["chain_launches"] > 0 and st["0"]["chain_launches"] == 0, st
+    assert st["1"]["kernels_per_step"] < st["0"]["kernels_per_step"]
+    assert st["1"]["chain_expired_spins"] == 0 and st["1"]["chain_off_xcd"] == 0, st["1"]
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b)
+    if model == "msgnn_K4_F32":
+        m = build_msgnn(4, 32, 4, state=weights("K4_F32"))
+        ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=32, K=4), ga)
+        assert per_step_rel(outs["1"][1], ref) <= REL_TOL
