@@ -2455,13 +2455,17 @@ __device__ __forceinline__ void chain_barrier(const HopChainArgs& a, unsigned lo
   }
   __syncthreads();
 }
-template <int NT>
+// LASTPH: the chain's final hop is the layer's last hop (k_hop<.., LAST = true>'s path: its
+// epilogue operands -- projections of the next layer, unpool U, forward-mode decoder -- are
+// staged into LDS at kernel start, behind the middle hops).
+template <int NT, int ACT, bool LASTPH>
 __global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
   constexpr int XS = F + 4;
   __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   __shared__ unsigned long long base_s;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int xb = logical_block(a.h.c);
   if (xb < 0) return;
@@ -2479,9 +2483,15 @@ __global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
   const bool live = tile < a.h.ntiles;
   const int tl = live ? tile : 0;  // idle waves stay in bounds
   float* slab = &slab_all[w][0][0];
+  Common c = a.h.c;
   const Lanes L = lanes_of(load_rec(a.h.recs, tl, j), tl, j, a.h.n0);
   f32x4 sv[NT];
   load_row<NT>(sv, a.h.s + L.p * F, g);  // s is fixed for the layer: plain loads
+  [[maybe_unused]] EpiPre<NT> pre;
+  if constexpr (LASTPH) {
+    if constexpr (kStaged<NT>) stage_glds<kWaves>(smem, c.W, a.h.reg, 0, a.h.reg.len);
+    epi_prefetch<NT>(pre, a.h.epi, c, a.h.xs, L.n, g);  // static inputs (x_s rows, X, BC)
+  }
   for (int k = 0; k < a.m; ++k) {
     const float* in = a.io[k];
     float* out = a.io[k + 1];
@@ -2507,7 +2517,10 @@ __global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) res[t] = inn[t];
       apply_filter_regs<NT>(res, agg, a.filt[k], wf);
-      if (L.nv) {
+      if (LASTPH && k + 1 == a.m) {  // the layer's last hop: k_hop<.., LAST = true>'s finish
+        if constexpr (kStaged<NT>) c.W = smem;  // staged at kernel start (every wave passed a barrier since)
+        node_epilogue<NT, ACT>(res, a.h.epi, c, pre, out, L.n, L.nv, lane, g);
+      } else if (L.nv) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) st4_l2(out + L.n * F + 16 * t + 4 * g, res[t]);
       }
@@ -2857,6 +2870,11 @@ hipError_t prepare_kernels() {
           if (e != hipSuccess) return e;
         }
   }
+  // persistent hop chains whose final phase is the layer's last hop (epilogue region in LDS)
+  for (const void* f : {(const void*)k_hop_chain<NT, 1, true>, (const void*)k_hop_chain<NT, -1, true>}) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
+    if (e != hipSuccess) return e;
+  }
   return hipSuccess;
 }
 
@@ -3029,7 +3047,16 @@ hipError_t launch_hop_chain(const HopChainArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;  // the grid must be one XCD's, one workgroup per CU
   HopChainArgs b = a;
   b.h.c.xcd = 1;
-  hipLaunchKernelGGL((k_hop_chain<NT>), dim3((unsigned)(a.G * kXcds)), dim3(kBlock), 0, st, b);
+  const dim3 grid((unsigned)(a.G * kXcds)), block(kBlock);
+  if (!a.h.last) {
+    hipLaunchKernelGGL((k_hop_chain<NT, 1, false>), grid, block, 0, st, b);
+  } else {
+    const size_t sh = lds_bytes<NT>(a.h.reg.len);
+    if (a.h.c.prelu)
+      hipLaunchKernelGGL((k_hop_chain<NT, 1, true>), grid, block, sh, st, b);
+    else
+      hipLaunchKernelGGL((k_hop_chain<NT, -1, true>), grid, block, sh, st, b);
+  }
   return hipGetLastError();
 }
 template <int NT>

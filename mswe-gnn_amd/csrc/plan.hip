@@ -600,10 +600,14 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
     // middle hops k .. K-1 as ONE persistent launch on XCD 0 (k_hop_chain) where the scale's
     // tiles fit one XCD at one workgroup per CU (the coarse scales; not on parts: their
     // exchanges sit between the hops)
-    const int nmid = pr.K - k;  // middle hops left (the last hop keeps its own launch)
+    // (MSW_HOP_CHAIN=2: the layer's last hop joins the chain as its final phase, k_hop's
+    // epilogue path, instead of its own -- cooperative -- launch)
+    const int with_last = P->kn.hop_chain >= 2 && pr.K - k + 1 <= kMaxChainHops ? 1 : 0;
+    const int nmid = pr.K - k + with_last;  // hops the chain would take
     if (P->kn.hop_chain && P->part_rank < 0 && nmid >= 2 && P->xcd_max >= 1 && g.ntiles > 0 &&
         (g.ntiles + kWaves - 1) / kWaves <= kCusPerXcd) {
       const int m = std::min(nmid, kMaxChainHops);
+      const bool last = with_last && k + m - 1 == pr.K;
       Launch L;
       L.kind = L_HOPC;
       L.scale = pr.scale;
@@ -613,13 +617,15 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
       h.h.s = P->s; h.h.xs = P->xs;
       h.h.grad = pr.with_gradient; h.h.upwind = pr.upwind;
       h.h.filt_a = -1;
+      h.h.last = last ? 1 : 0;
+      if (last) h.h.epi = epi;
       h.m = m;
       h.G = (g.ntiles + kWaves - 1) / kWaves;
       float* b = const_cast<float*>(cur);
       h.io[0] = b;
       for (int i = 0; i < m; ++i) {
         b = b == P->T[0] ? P->T[1] : P->T[0];
-        h.io[i + 1] = b;
+        h.io[i + 1] = (last && i + 1 == m) ? out : b;
         h.filt[i] = pr.filt.empty() ? -1 : pr.filt[k - 1 + i];
       }
       q.push_back(L);
@@ -966,8 +972,15 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       a.filt_l = R.put(a.filt_a, P->NT * P->NT * 256);
       a.reg = R.done(split);
       reg = &a.reg;
-    } else if (L.kind == L_EXCHANGE || L.kind == L_HOPC) {
-      continue;  // no LDS weight region (the chain's filters go from the blob into registers)
+    } else if (L.kind == L_EXCHANGE) {
+      continue;  // no LDS weight region
+    } else if (L.kind == L_HOPC) {
+      HopArgs& a = L.hopc.h;  // the filters go from the blob into registers
+      if (!a.last) continue;  // ... and a final last hop stages its epilogue operands
+      RegionBuilder R(P->blob, 0);
+      rl.epi(R, a.epi);
+      a.reg = R.done();
+      reg = &a.reg;
     } else if (L.kind == L_EPI) {
       EpiArgs& a = L.ep;
       RegionBuilder R(P->blob, 0);
@@ -1256,7 +1269,7 @@ void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
   for (Launch& L : q) {
     if (L.kind == L_ENCODE) L.enc.x = x;
     Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi
-                 : L.kind == L_EPI ? &L.ep.epi : nullptr;
+                 : L.kind == L_HOPC ? &L.hopc.h.epi : L.kind == L_EPI ? &L.ep.epi : nullptr;
     if (e && e->dec.on) {
       e->dec.X = x;
       e->dec.y = y;

@@ -838,10 +838,11 @@ def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, F, kw):
 @pytest.mark.parametrize("model", ["msgnn_K4_F32", "msgnn_F64", "gnn"])
 def test_persistent_hop_chain_matches_separate_hops(cuda, monkeypatch, model):
     """Middle hops of a layer as ONE persistent launch on XCD 0 (k_hop_chain: workgroups
-    synchronised through XCD 0's L2 between hops; MSW_HOP_CHAIN=1, the default on scales whose
-    tiles fit one XCD) == one k_hop launch per hop (MSW_HOP_CHAIN=0), bit for bit: forward,
-    rollout and a batch of two meshes; fewer launches per step; no expired barrier spin and no
-    workgroup off XCD 0 (msw_plan_chain_health); and the reference fixture / oracle."""
+    synchronised through XCD 0's L2 between hops; MSW_HOP_CHAIN=1 on scales whose tiles fit one
+    XCD; =2 also the layer's last hop with its epilogue as the chain's final phase) == one
+    launch per hop (MSW_HOP_CHAIN=0), bit for bit: forward, rollout and a batch of two meshes;
+    fewer launches per step; no expired barrier spin and no workgroup off XCD 0
+    (msw_plan_chain_health); and the oracle."""
     from mswegnn.batch import collate
     from mswegnn.engine import plan_for
     from mswegnn.rollout import rollout_test
@@ -859,7 +860,7 @@ def test_persistent_hop_chain_matches_separate_hops(cuda, monkeypatch, model):
         ga = wet_state(make_multiscale_mesh(**mesh_config("small"), T=8), seed=4)
         gb = wet_state(make_multiscale_mesh(n_coarse=2, num_scales=4, seed=5, T=8), seed=5)
     outs, st = {}, {}
-    for sv in ("0", "1"):
+    for sv in ("0", "1", "2"):
         monkeypatch.setenv("MSW_HOP_CHAIN", sv)
         m = build()
         gd = ga.to(cuda)
@@ -869,10 +870,11 @@ def test_persistent_hop_chain_matches_separate_hops(cuda, monkeypatch, model):
         st[sv] = plan_for(m, gd).stats()
         outs[sv] = (y, r, rollout_test(m, collate([ga, gb]).to(cuda)).cpu())
     assert st["1"]["chain_launches"] > 0 and st["0"]["chain_launches"] == 0, st
-    assert st["1"]["kernels_per_step"] < st["0"]["kernels_per_step"]
-    assert st["1"]["chain_expired_spins"] == 0 and st["1"]["chain_off_xcd"] == 0, st["1"]
-    for a, b in zip(outs["0"], outs["1"]):
-        assert torch.equal(a, b)
+    assert st["2"]["kernels_per_step"] < st["1"]["kernels_per_step"] < st["0"]["kernels_per_step"], st
+    for sv in ("1", "2"):
+        assert st[sv]["chain_expired_spins"] == 0 and st[sv]["chain_off_xcd"] == 0, st[sv]
+        for a, b in zip(outs["0"], outs[sv]):
+            assert torch.equal(a, b), sv
     if model == "msgnn_K4_F32":
         m = build_msgnn(4, 32, 4, state=weights("K4_F32"))
         ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=32, K=4), ga)
