@@ -242,7 +242,9 @@ int msw_bench_kernel(msw_plan* plan, int32_t kernel, int32_t scale, int32_t iter
  * [num_sims][2], the finest-scale row range of each simulation (node_ptr[g][0],
  * node_ptr[g][1]); thresholds: host float [n_thr] (n_thr <= 4) water-depth thresholds;
  * area: device float [N] cell areas by graph row (data.area), or NULL.
- * Outputs (device, ZEROED by the caller, accumulated with atomics):
+ * Outputs (device): sums written (fp64, workgroup partials added in a fixed order -- bit-
+ * reproducible; stream-ordered scratch from hipMallocAsync), counts ZEROED by the caller
+ * (exact integer atomics):
  *   sums   double [num_sims][T][10]: sum|dh|, sum|dv|, sum dh^2, sum dv^2, the same four
  *          over rows with dh != 0 or dv != 0 (mask_on_water), that row count, and the
  *          stored volume sum(area * h_pred) (0 when area is NULL);

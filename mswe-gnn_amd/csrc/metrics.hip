@@ -7,8 +7,11 @@
 //   stored water volume sum(area * h) per step, the core of the mass-conservation metric
 //   get_mass_conservation_loss / conservation_loss      utils/miscellaneous.py:116-121,
 //                                                         training/loss.py:120-169
-// The kernel produces per-(simulation, step) partial sums in fp64 and exact integer counts;
-// the host side (mswegnn/metrics.py) forms the reference's ratios.
+// The kernels produce per-(simulation, step) sums in fp64 and exact integer counts; the host
+// side (mswegnn/metrics.py) forms the reference's ratios.  No floating-point atomics: each
+// workgroup writes its partial sums (waves combined in a fixed order), a second kernel adds the
+// workgroups' partials in order -- the metrics are bit-reproducible run to run.  (The
+// integer confusion counts use integer atomics: exact in any order.)
 #include <hip/hip_runtime.h>
 
 #include "../../include/mswegnn.h"
@@ -39,7 +42,7 @@ struct MetricArgs {
   int row0, nrows;  // fine-scale rows [row0, row0 + nrows) of this simulation
   int nthr;
   float thr[kMaxThr];
-  double* sums;                 // this simulation's [T][kSums]
+  double* part;                 // this simulation's [nblocks][T][kSums] workgroup partials
   unsigned long long* counts;   // this simulation's [T][nthr][4]
 };
 
@@ -47,7 +50,8 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
   const int i = blockIdx.x * kThreads + threadIdx.x;
   const bool valid = i < a.nrows;
   const size_t n = (size_t)a.row0 + (valid ? i : 0);
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ double wsum[kThreads / 64][kSums];
   const int t0 = blockIdx.y * kTChunk;
   const double ar = valid && a.area ? (double)a.area[n] : 0.0;
   for (int t = t0; t < t0 + kTChunk && t < a.T; ++t) {
@@ -74,8 +78,16 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
     for (int k = 0; k < kSums; ++k) v[k] = wave_sum(v[k]);
     if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < kSums; ++k) atomicAdd(a.sums + (size_t)t * kSums + k, v[k]);
+      for (int k = 0; k < kSums; ++k) wsum[w][k] = v[k];
     }
+    __syncthreads();
+    if (threadIdx.x < kSums) {  // the waves' sums in a fixed order
+      double b = 0.0;
+#pragma unroll
+      for (int q = 0; q < kThreads / 64; ++q) b += wsum[q][threadIdx.x];
+      a.part[((size_t)blockIdx.x * a.T + t) * kSums + threadIdx.x] = b;
+    }
+    __syncthreads();
     for (int k = 0; k < a.nthr; ++k) {
       const bool p = ph > a.thr[k], r = rh > a.thr[k];
       const unsigned long long tp = __popcll(__ballot(valid && p && r));
@@ -91,6 +103,16 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
       }
     }
   }
+}
+
+// sums[t][k] = sum over the workgroups b = 0, 1, ... (in order) of part[b][t][k]
+__global__ __launch_bounds__(kThreads) void k_metrics_reduce(const double* __restrict__ part, int nblocks, long count,
+                                                             double* __restrict__ sums) {
+  const long i = blockIdx.x * (long)kThreads + threadIdx.x;
+  if (i >= count) return;
+  double v = 0.0;
+  for (int b = 0; b < nblocks; ++b) v += part[(size_t)b * count + i];
+  sums[i] = v;
 }
 
 }  // namespace
@@ -116,13 +138,26 @@ extern "C" int msw_rollout_metrics(const float* pred, const float* real, int32_t
     if (a.nrows < 0) return msw::set_error(MSW_ERR_INVALID, "fine range end < start");
     a.nthr = n_thr;
     for (int k = 0; k < n_thr; ++k) a.thr[k] = thresholds[k];
-    a.sums = sums + (size_t)g * T * kSums;
+    double* out = sums + (size_t)g * T * kSums;
     a.counts = reinterpret_cast<unsigned long long*>(counts) + (size_t)g * T * (n_thr > 0 ? n_thr : 1) * 4;
-    if (a.nrows == 0) continue;
-    const dim3 grid((a.nrows + kThreads - 1) / kThreads, (T + kTChunk - 1) / kTChunk);
-    hipLaunchKernelGGL(k_metrics, grid, dim3(kThreads), 0, st, a);
-    const hipError_t e = hipGetLastError();
+    const long count = (long)T * kSums;
+    if (a.nrows == 0) {  // no fine rows: zero sums (the caller zeroes the counts)
+      if (hipMemsetAsync(out, 0, (size_t)count * sizeof(double), st) != hipSuccess)
+        return msw::set_error(MSW_ERR_HIP, "hipMemsetAsync");
+      continue;
+    }
+    const int nb = (a.nrows + kThreads - 1) / kThreads;
+    double* part = nullptr;  // stream-ordered scratch for the workgroup partials
+    hipError_t e = hipMallocAsync((void**)&part, (size_t)nb * count * sizeof(double), st);
     if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
+    a.part = part;
+    hipLaunchKernelGGL(k_metrics, dim3(nb, (T + kTChunk - 1) / kTChunk), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(k_metrics_reduce, dim3((unsigned)((count + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                       (const double*)part, nb, count, out);
+    e = hipGetLastError();
+    const hipError_t f = hipFreeAsync(part, st);
+    if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
+    if (f != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(f));
   }
   return MSW_OK;
 }
