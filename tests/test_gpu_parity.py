@@ -371,6 +371,10 @@ def test_rollout_metrics_kernel_vs_reference(cuda):
     m2 = rollout_metrics(p2, r2, [(0, n0), (n0, 2 * n0)], thresholds=(0.05,))
     assert rel_err(m2["rmse"].cpu(), fx["loss_RMSE_stack"]) <= 1e-5
     np.testing.assert_allclose(m2["csi"][0.05].cpu().numpy(), fx["csi_0.05_stack"], rtol=1e-6, equal_nan=True)
+    # no floating-point atomics: bit-reproducible run to run
+    m3 = rollout_metrics(p2, r2, [(0, n0), (n0, 2 * n0)], thresholds=(0.05,))
+    for key in ("rmse", "mae", "rmse_water", "mae_water"):
+        assert torch.equal(m2[key], m3[key]), key
 
 
 @pytest.mark.parametrize("parts", [2, 3])
