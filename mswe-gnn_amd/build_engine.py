@@ -20,6 +20,7 @@ ROOT = os.path.dirname(HERE)
 SRC = ["csrc/kernels_nt1.hip", "csrc/kernels_nt2.hip", "csrc/kernels_nt4.hip",
        "csrc/kernels_common.hip", "csrc/plan.hip", "csrc/metrics.hip", "csrc/train.hip"]
 HDR = ["csrc/engine.h", "csrc/kernels_impl.h", "csrc/tiling.h", "csrc/graph_build.h", os.path.join(ROOT, "include", "mswegnn.h")]
+HDR += sorted(os.path.join("csrc", "kernels", f) for f in os.listdir(os.path.join(HERE, "csrc", "kernels")) if f.endswith(".h"))
 ARCH = os.environ.get("MSW_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
          "-I", os.path.join(ROOT, "include")]

@@ -1,0 +1,496 @@
+// gfx950 kernels: message passing, fused edge MLP + hop 1, split edge MLP.
+// Part of kernels_impl.h (included inside namespace msw, in this order); see its header
+// comment for the register layout and conventions.
+#pragma once
+
+// ---------------------------------------------------------------------------- message passing
+// One wave = one edge tile (whole destination neighbourhoods, <= 16 edges, <= 16 nodes).
+// Lane j is edge slot j in the edge phase and destination j in the node phase; per-node
+// rows the edges need (V, out at the destination) are loaded ONCE by the node lanes and
+// handed to the edge lanes through the wave's LDS slab, the messages go back through the
+// same slab (no atomics; every destination sums its messages in the reference's edge
+// order).
+struct Lanes {
+  bool ev, nv;
+  int dl, q0, q1;
+  size_t sr, n;   // source row (edge lane) / destination row (node lane), safe rows if absent
+  size_t p;       // tile-padded edge slot
+};
+__device__ __forceinline__ Lanes lanes_of(const LaneRec& r, int tile, int j, int n0) {
+  Lanes L;
+  L.ev = r.src >= 0;
+  L.nv = r.n >= 0;
+  L.dl = L.ev ? r.dl : 0;
+  L.sr = (size_t)(L.ev ? r.src : n0);
+  L.n = (size_t)(L.nv ? r.n : n0);
+  L.q0 = r.q & 255;
+  L.q1 = L.nv ? (r.q >> 8) : L.q0;
+  L.p = (size_t)tile * kRowsPerWave + j;
+  return L;
+}
+__device__ __forceinline__ LaneRec load_rec(const LaneRec* recs, int tile, int j) {
+  const int4 v = reinterpret_cast<const int4*>(recs)[(size_t)tile * kRowsPerWave + j];
+  return LaneRec{v.x, v.y, v.z, v.w};
+}
+
+// msg_e = active(e) * (out[col] - out[row]) * s_e  (or s_e * out[row])   (gnn.py:406-435)
+template <int NT>
+__device__ __forceinline__ void put_message(float* slab_row, const f32x4 (&os)[NT], const f32x4 (&od)[NT],
+                                            const f32x4 (&sv)[NT], bool ev, int grad, int upwind, int g) {
+#pragma clang fp contract(off)
+  float rs = 0.f, rd = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    rs += hsum(os[t]);
+    rd += hsum(od[t]);
+  }
+  const bool act = (row_sum(rs) != 0.f) || (row_sum(rd) != 0.f);  // gnn.py:408-411
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    f32x4 gv;
+    if (grad) {
+      gv = od[t] - os[t];  // out[col] - out[row]
+      if (upwind) {
+        gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
+        gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
+      }
+    } else {
+      gv = os[t];          // s_ij * out[row]
+    }
+    const f32x4 m = gv * sv[t];
+    st4(slab_row + 16 * t + 4 * g, (ev && act) ? m : zero4());
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Node phase: agg = sum of the node's messages (edge order).
+template <int NT, int STRIDE>
+__device__ __forceinline__ void gather_messages(f32x4 (&agg)[NT], const float* slab, int q0, int q1, int g) {
+#pragma clang fp contract(off)
+  wave_lds_sync();
+#pragma unroll
+  for (int t = 0; t < NT; ++t) agg[t] = zero4();
+  for (int q = q0; q < q1; ++q) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) agg[t] = agg[t] + ld4(slab + q * STRIDE + 16 * t + 4 * g);
+  }
+}
+
+// res += W agg (filter; agg is already in B-operand layout) or res += agg
+template <int NT>
+__device__ __forceinline__ void apply_filter(f32x4 (&res)[NT], const f32x4 (&agg)[NT], int filt_a,
+                                             const float* W, int lane) {
+#pragma clang fp contract(off)
+  if (filt_a >= 0) {
+    f32x4 acc[NT];
+    proj<NT, NT>(agg, acc, W + filt_a, lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + agg[t];
+  }
+}
+
+// Tile kernels: LOOP = false -> one tile per wave, the tile's HBM gathers issued before the
+// weight staging (latency-bound meshes); LOOP = true -> grid capped at the resident
+// workgroups, each stages its weight region ONCE and walks tiles grid-stride (large
+// meshes).  In the loop the lane id is made opaque per iteration so that the compiler does
+// not hoist every lane-derived weight address out of the loop (it pinned ~55 VGPRs).
+__device__ __forceinline__ int opaque_lane() {
+  int ln = (int)(threadIdx.x & 63);
+  asm volatile("" : "+v"(ln));
+  return ln;
+}
+
+// Filter A operand straight from the blob into registers (small: NT x NT tiles), issued at
+// kernel start; apply_filter_regs = apply_filter with the operand already in registers.
+template <int NT>
+__device__ __forceinline__ void load_filter(f32x4 (&wf)[NT][NT], const float* W, int filt_a, int lane) {
+  const int fa = filt_a >= 0 ? filt_a : 0;  // unconditional (unused without a filter)
+#pragma unroll
+  for (int to = 0; to < NT; ++to)
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) wf[to][ti] = ld4(W + fa + ((size_t)(to * NT + ti) * 64 + lane) * 4);
+}
+template <int NT>
+__device__ __forceinline__ void apply_filter_regs(f32x4 (&res)[NT], const f32x4 (&agg)[NT], int filt_a,
+                                                  const f32x4 (&wf)[NT][NT]) {
+#pragma clang fp contract(off)
+  if (filt_a >= 0) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int to = 0; to < NT; ++to) acc[to] = zero4();
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int to = 0; to < NT; ++to) acc[to] = MSW_MFMA(wf[to][ti][r], agg[ti][r], acc[to]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + acc[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + agg[t];
+  }
+}
+
+// ---------------------------------------------------------------------------- edge MLP + hop 1
+//  edges: s_ij = normalize(MLP(x_s[row], x_s[col], x_d[row], x_d[col], e_ij))
+//         (gnn.py:414-426; first layer pre-split: h1 = act(U[row] + V[col] + Pe[e]));
+//         computed ONCE per layer -- its inputs do not change across the K hops.
+//  nodes: out_1 = out_0 + W_1 agg [+ skip] -> store, or the epilogue when K = 1.
+template <int NT>
+struct EdgeHopRows {  // everything one tile reads from HBM
+  Lanes L;
+  f32x4 Us[2 * NT], Ps[2 * NT], Vn[2 * NT], os[NT], inn[NT], sk[NT];
+  EpiPre<NT> pre;  // a.last only
+};
+// LST = 0: the launch never runs an epilogue (compiled out: fewer live scalars, no SGPR
+// spills into VGPR lanes in the grid-stride loop); LST = 1: a.last decides.
+template <int NT, int LST>
+__device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHopArgs& a, const LaneRec& rec,
+                                                int tile, int j, int g) {
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  r.L = lanes_of(rec, tile, j, a.n0);
+  const Lanes& L = r.L;
+  const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  const float* Ub = a.U + L.sr * hs;
+  const float* Vb = a.V + L.n * hs;
+  const float* Pb = a.Pe ? a.Pe + L.p * hs : z;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
+    const int off = 16 * t + 4 * g;
+    const bool on = t < a.h1t;
+    r.Us[t] = ld4((on ? Ub : z) + off);
+    r.Vn[t] = ld4((on ? Vb : z) + off);
+    r.Ps[t] = ld4((on ? Pb : z) + off);
+  }
+  load_row<NT>(r.os, a.in + L.sr * F, g);
+  load_row<NT>(r.inn, a.own_zero ? z : a.in + L.n * F, g);
+  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
+  if (LST && a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
+}
+template <int NT, int LST>
+__device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
+  edge_hop_gather<NT, LST>(r, a, load_rec(a.recs, tile, j), tile, j, g);
+}
+// Wm: the MLP operands (b1, layers 2..L) -- the staged region; c.W: everything else (the
+// same region for F <= 32, the blob for F = 64, whose epilogue operands do not fit in LDS).
+template <int NT, int ACT, int XS, bool FREG = true>
+__device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
+                                              const float* Wm, const f32x4 (&wf)[NT][NT], float* slab, int j,
+                                              int lane, int g, f32x4 (&res_out)[NT]) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  const Lanes& L = r.L;
+  // node rows -> edge lanes
+  float* my = slab + j * XS;
+  store_row<T2>(my, r.Vn, T2, g);
+  store_row<NT>(my + 16 * T2, r.inn, NT, g);
+  wave_lds_sync();
+  const float* dr = slab + L.dl * XS;
+  f32x4 H[T2], od[NT];
+  // unconditional LDS reads + selects: reads under the run-time h1t / Pe flags compiled to
+  // a branch and an lgkmcnt(0) wait per tile
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  f32x4 vr[T2], br[T2];
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    vr[t] = ld4(dr + off);
+    br[t] = ld4(Wm + b1 + off);
+  }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const f32x4 p = a.Pe ? r.Ps[t] : br[t];
+    H[t] = (t < a.h1t) ? (r.Us[t] + vr[t]) + p : zero4();
+  }
+  load_row<NT>(od, dr + 16 * T2, g);
+  MSW_MARK(c, 4);
+  act_tiles<ACT, T2>(H, a.act1, a.slope1);
+  f32x4 sv[NT];
+  if (a.rest.n > 0) {
+    run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, lane, g);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sv[t] = H[t];
+  }
+  MSW_MARK(c, 5);
+  if (a.normalize) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+    const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 q = sv[t] / nrm;
+      q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+      q.y = (q.y == q.y) ? q.y : 0.f;
+      q.z = (q.z == q.z) ? q.z : 0.f;
+      q.w = (q.w == q.w) ? q.w : 0.f;
+      sv[t] = q;
+    }
+  }
+  if (a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);  // padding slots too: never read
+  put_message<NT>(my, r.os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
+  MSW_MARK(c, 6);
+  f32x4 agg[NT], res[NT];
+  gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
+  MSW_MARK(c, 7);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) res[t] = r.inn[t];
+  if constexpr (FREG)
+    apply_filter_regs<NT>(res, agg, a.filt_a, wf);
+  else  // filter operand in the staged LDS region (fewer live registers in the loop)
+    apply_filter<NT>(res, agg, a.filt_l, c.W, lane);
+  MSW_MARK(c, 8);
+  if (a.skip) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) res[t] = res[t] + r.sk[t];
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) res_out[t] = res[t];
+}
+template <int NT, int ACT, int LST>
+__device__ __forceinline__ void edge_hop_finish(f32x4 (&res)[NT], const EdgeHopRows<NT>& r, const EdgeHopArgs& a,
+                                                const Common& c, int lane, int g) {
+  constexpr int F = 16 * NT;
+  const Lanes& L = r.L;
+  if (LST && a.last) {
+    node_epilogue<NT, ACT>(res, a.epi, c, r.pre, a.out, L.n, L.nv, lane, g);
+  } else if (L.nv && a.out) {
+    store_row<NT>(a.out + L.n * F, res, NT, g);
+  }
+}
+template <int NT, int ACT, bool LOOP, int LST>
+__global__ __launch_bounds__((64 * edge_waves<NT, LOOP, LST>())) __attribute__((amdgpu_waves_per_eu(edge_eu<NT, LOOP, LST>())))
+void k_edge_hop(EdgeHopArgs a) {
+  constexpr int WV = edge_waves<NT, LOOP, LST>();
+  // slab row: V | out, +4 floats so the 16 rows of a b128 access hit distinct LDS banks
+  constexpr int XS = 16 * 2 * NT + 16 * NT + 4;
+  __shared__ __attribute__((aligned(16))) float slab[WV][kRowsPerWave][XS];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
+  const int stride = gridDim.x * WV;
+  const int xb = logical_block(a.c);
+  if (xb < 0) return;
+  int tile = xb * WV + w;
+  Common c = a.c;
+  MSW_MARK(c, 0);
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
+  f32x4 wf[NT][NT];
+  if constexpr (!LOOP || !kStaged<NT>)
+    load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
+  if constexpr (!LOOP) {
+    const bool live = tile < a.ntiles;
+    EdgeHopRows<NT> r;
+    edge_hop_load<NT, LST>(r, a, live ? tile : 0, j, g);  // idle waves stay in bounds
+    MSW_MARK(c, 1);
+    // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
+    // stream into LDS behind the MLP and are waited for at the epilogue barrier
+    const bool split = kStaged<NT> && a.reg.split < a.reg_nf;
+    const float* Wm = c.W;
+    if constexpr (kStaged<NT>) {
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.split);
+      __syncthreads();
+      c.W = smem;
+      Wm = smem;
+      if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
+    } else if (a.reg.len > 0) {  // F = 64: the MLP region alone (plan.hip relocate)
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      Wm = smem;
+    }
+    MSW_MARK(c, 2);
+    f32x4 res[NT];
+    if (live) edge_hop_core<NT, ACT, XS>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
+    if (split) __syncthreads();  // every wave: the epilogue operands have landed
+    if (live) edge_hop_finish<NT, ACT, LST>(res, r, a, c, lane, g);
+  } else {
+    const float* Wm = c.W;
+    if constexpr (kStaged<NT>) {
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      c.W = smem;
+      Wm = smem;
+    } else if (a.reg.len > 0) {  // F = 64: the MLP region alone
+      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+      __syncthreads();
+      Wm = smem;
+    }
+    for (; tile < a.ntiles; tile += stride) {
+      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+      EdgeHopRows<NT> q;
+      edge_hop_load<NT, LST>(q, a, tile, jj, gg);
+      f32x4 res[NT];
+      edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, Wm, wf, &slab[w][0][0], jj, ln, gg, res);
+      edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
+    }
+  }
+  MSW_MARK(c, 9);
+}
+
+// ---------------------------------------------------------------------------- edge MLP alone
+// F = 64 scales whose edge tiles exceed one round of the fused kernel (plan.hip sched_proc,
+// MSW_SPLIT_EDGE_MLP): the edge MLP of a layer's first hop on its own, s for every edge;
+// hop 1 then runs as a k_hop launch.  Without the hop state (source / own rows, filter,
+// node -> edge slab) the kernel fits two waves per SIMD where the fused kernel runs one, and
+// it needs no whole neighbourhoods: it walks dense chunks of 16 real edges (EdgeChunk), so
+// the last partly filled round of the tile order disappears (zenodo4: 2,050 tiles on 1,024
+// fused waves = three rounds; 1,927 chunks on 2,048 waves = one).  The arithmetic is
+// edge_hop_core's, operation for operation: s is bit-identical.
+constexpr int kMlpWaves = 8;
+template <int NT, int ACT>
+__global__ __launch_bounds__(64 * kMlpWaves) __attribute__((amdgpu_waves_per_eu(2)))
+void k_edge_mlp(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = wave_id();
+  const int stride = gridDim.x * kMlpWaves;
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
+  const float* Wm = a.c.W;
+  if (a.reg.len > 0) {
+    stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
+    __syncthreads();
+    Wm = smem;
+  }
+  const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  for (int ch = blockIdx.x * kMlpWaves + w; ch < a.nchunks; ch += stride) {
+    const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+    const int4 e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+    const bool ev = e.z >= 0;
+    const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
+    const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
+    const float* Pb = a.Pe && ev ? a.Pe + (size_t)e.z * hs : z;
+    f32x4 H[T2];
+#pragma unroll
+    for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
+      const int off = 16 * t + 4 * g;
+      const bool on = t < a.h1t;
+      const f32x4 u = ld4((on ? Ub : z) + off);
+      const f32x4 v = ld4((on ? Vb : z) + off);
+      const f32x4 pe = ld4((on ? Pb : z) + off);
+      const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
+      H[t] = on ? (u + v) + p : zero4();
+    }
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 q = sv[t] / nrm;
+        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+        q.y = (q.y == q.y) ? q.y : 0.f;
+        q.z = (q.z == q.z) ? q.z : 0.f;
+        q.w = (q.w == q.w) ? q.w : 0.f;
+        sv[t] = q;
+      }
+    }
+    if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  }
+}
+
+// k_edge_mlp software-pipelined (F = 64, MSW_MLP_PIPE): one wave per SIMD, each wave walks
+// ~2 chunks and issues the next chunk's U / V / Pe gathers (1.5 KB per edge) before the
+// current chunk's MLP (384 MFMAs), so the gathers of chunk n+1 run under the MFMA chain of
+// chunk n instead of every wave of the launch gathering, then multiplying, in lockstep.  Same
+// operations on the same operands as k_edge_mlp: s is bit-identical.
+constexpr int kMlpPipeWaves = 4;
+template <int NT>
+struct MlpFetch {
+  f32x4 u[2 * NT], v[2 * NT], p[2 * NT];
+  int4 e;
+};
+template <int NT>
+__device__ __forceinline__ void mlp_fetch(MlpFetch<NT>& f, const EdgeHopArgs& a, int ch, int j, int g) {
+  constexpr int T2 = 2 * NT;
+  const int hs = 16 * a.h1t;
+  const float* z = a.c.zrow;
+  f.e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+  const bool ev = f.e.z >= 0;
+  const float* Ub = a.U + (size_t)(ev ? f.e.x : a.n0) * hs;
+  const float* Vb = a.V + (size_t)(ev ? f.e.y : a.n0) * hs;
+  const float* Pb = a.Pe && ev ? a.Pe + (size_t)f.e.z * hs : z;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    const bool on = t < a.h1t;
+    f.u[t] = ld4((on ? Ub : z) + off);
+    f.v[t] = ld4((on ? Vb : z) + off);
+    f.p[t] = ld4((on ? Pb : z) + off);
+  }
+}
+template <int NT, int ACT>
+__global__ __launch_bounds__(64 * kMlpPipeWaves) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_edge_mlp_pipe(EdgeHopArgs a) {
+#pragma clang fp contract(off)
+  constexpr int F = 16 * NT, T2 = 2 * NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = wave_id();
+  const int stride = gridDim.x * kMlpPipeWaves;
+  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
+  const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+  int ch = blockIdx.x * kMlpPipeWaves + w;
+  MlpFetch<NT> f;
+  if (ch < a.nchunks) mlp_fetch<NT>(f, a, ch, j, g);  // in flight during the weight staging
+  const float* Wm = a.c.W;
+  if (a.reg.len > 0) {
+    stage_glds<kMlpPipeWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
+    __syncthreads();
+    Wm = smem;
+  }
+  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+  for (; ch < a.nchunks; ch += stride) {
+    f32x4 H[T2];
+#pragma unroll
+    for (int t = 0; t < T2; ++t) {
+      const f32x4 p = a.Pe ? f.p[t] : ld4(Wm + b1 + 16 * t + 4 * g);
+      H[t] = t < a.h1t ? (f.u[t] + f.v[t]) + p : zero4();
+    }
+    const int4 e = f.e;
+    if (ch + stride < a.nchunks) mlp_fetch<NT>(f, a, ch + stride, j, g);
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 q = sv[t] / nrm;
+        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+        q.y = (q.y == q.y) ? q.y : 0.f;
+        q.z = (q.z == q.z) ? q.z : 0.f;
+        q.w = (q.w == q.w) ? q.w : 0.f;
+        sv[t] = q;
+      }
+    }
+    if (e.z >= 0) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  }
+}

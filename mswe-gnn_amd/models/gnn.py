@@ -136,7 +136,9 @@ class SWEGNN(nn.Module):
             else:
                 msg = s * out[row]
             msg = torch.where(active, msg, torch.zeros_like(msg))
-            agg = torch.zeros_like(out).index_add_(0, col, msg)
+            # the sum takes the message's dtype (under autocast msg may be wider or narrower
+            # than out), as PyG's scatter does: src.new_zeros(...).scatter_add_
+            agg = msg.new_zeros((out.shape[0], msg.shape[1])).index_add_(0, col, msg)
             if self.with_filter_matrix:
                 agg = self.filter_matrix[k + 1](agg)
             out = out + agg
@@ -367,10 +369,10 @@ class MSGNN(_EngineMixin, BaseFloodModel):
     def _pooling(self, x, row_fine, col_coarse, reduce='mean', learnable=False):
         """Mean of the children of every coarse node; rows without children -> 0."""
         src = self.pooling_mlp(torch.cat((x[row_fine], x[col_coarse]), -1)) if learnable else x[row_fine]
-        out = torch.zeros_like(x).index_add_(0, col_coarse, src)
+        out = src.new_zeros((x.shape[0], src.shape[1])).index_add_(0, col_coarse, src)
         if reduce == 'mean':
-            cnt = torch.zeros(x.shape[0], dtype=x.dtype, device=x.device).index_add_(
-                0, col_coarse, torch.ones_like(col_coarse, dtype=x.dtype))
+            cnt = torch.zeros(x.shape[0], dtype=out.dtype, device=x.device).index_add_(
+                0, col_coarse, torch.ones_like(col_coarse, dtype=out.dtype))
             out = out / cnt.clamp(min=1).unsqueeze(1)
         return out
 

@@ -346,7 +346,9 @@ def test_hip_training_step_under_autocast_fp16(cuda, sname, R):
     print(f"autocast fp16 {sname} R={R}: global rel vs fp64 -- HIP {g_hip:.2e}, torch AMP {g_amp:.2e}, "
           f"reference fp32 {g_ref:.2e}")
     assert g_hip <= max(TOL, 3 * g_ref) or g_hip <= 0.1 * g_amp, (g_hip, g_amp, g_ref)
-    assert g_amp <= 5e-2, g_amp
+    # fp16 rounding compounds over the rollout (CPU fp16 autocast measures 1.9e-2 at R=1 and
+    # 9.9e-2 at R=4): a loose sanity bound on the reported torch-AMP figure
+    assert g_amp <= 0.2, g_amp
 
 
 def test_autograd_caches_follow_graph_lifetime_and_guards(cuda):

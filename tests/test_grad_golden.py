@@ -49,6 +49,20 @@ def test_training_step_gradients_vs_reference(sname, R):
           f"fp64 rule for {rule64}")
 
 
+def test_torch_path_trains_under_autocast():
+    """The reference trains under precision='16-mixed' (main.py:106-110).  Under autocast the
+    drop-in's torch path mixes dtypes between the edge MLP (reduced precision) and the node
+    state; the scatter sums take the message's dtype (as PyG's scatter does) instead of
+    failing.  Bound: the gradients stay within reduced-precision distance of the reference's
+    float64 gradients."""
+    for dt, bound in ((torch.bfloat16, 0.3), (torch.float16, 0.05)):
+        with torch.autocast("cpu", dtype=dt):
+            ours, fx = gc.training_step_case(CPU, "b2", 1, engine="torch")
+        g = gc.global_rel(ours, fx, "b2_R1_fp64__")
+        print(f"CPU autocast {dt}: global rel vs fp64 {g:.2e}")
+        assert g <= bound, (dt, g)
+
+
 @pytest.mark.parametrize("R", [1, 2])
 def test_gnn_training_step_gradients_vs_reference(R):
     ours, fx = gc.gnn_training_step_case(CPU, R)
