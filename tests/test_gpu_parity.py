@@ -6,6 +6,8 @@ by the reference itself (oracle/gen_golden.py) or, for configurations without a 
 the oracle (bit-identical to the reference on CPU, pinned by test_oracle_golden.py).
 Tolerance: max|ours - ref| / max|ref| <= 1e-4 at every step (BASELINE.json north star).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -698,6 +700,32 @@ def test_grid_stride_edge_hops_match_one_tile_per_wave(cuda, monkeypatch, S, F, 
         outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
         plan.close()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("variant", ["ehpipe8"])
+def test_build_variant_matches_default_bitwise(variant):
+    """A library build variant (build_engine.py --variant=<name>, loaded with MSW_LIB_VARIANT)
+    == the default library bit for bit: a 3-step rollout of the dk15-size mesh with the
+    grid-stride edge hops forced (MSW_EH_LOOP=1: ~4.3 k finest tiles, so the 8-wave
+    workgroups of ehpipe8 walk 2-3 tiles per wave through the software pipeline), one child
+    process per library (a process loads one).  Skipped when the variant is not built."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "mswe-gnn_amd", "lib", f"libmswegnn_{variant}.so")):
+        pytest.skip(f"build variant {variant} not built")
+    res = []
+    for v in ("", variant):
+        env = {k: x for k, x in os.environ.items() if not k.startswith("MSW_")}
+        if v:
+            env["MSW_LIB_VARIANT"] = v
+        r = subprocess.run([sys.executable, os.path.join(root, "tools", "rollout_digest.py"), "--mesh", "dk15",
+                            "--T", "3", "--eh-loop"], capture_output=True, text=True, env=env, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    print(res)
+    assert res[0]["sha256"] == res[1]["sha256"], res
 
 
 @pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct"])
