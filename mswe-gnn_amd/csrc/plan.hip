@@ -1033,8 +1033,10 @@ bool row_hops_forced(const msw_plan* P) { return P->kn.hop_rows == 2; }
 constexpr long kEncCoopWaves = 4096;
 void set_grid_cap(msw_plan* P, Launch& L) {
   // XCD packing (Common::xcd_max) applies to the hop, edge-hop, pooling and row-epilogue
-  // launches (the only one-round grids small enough to fit one XCD)
-  if (L.kind != L_HOP && L.kind != L_EDGE_HOP && L.kind != L_POOL && L.kind != L_EPI) L.common().xcd_max = 0;
+  // launches (the only one-round grids small enough to fit one XCD) and to the persistent hop
+  // chains (always on XCD 0)
+  if (L.kind != L_HOP && L.kind != L_EDGE_HOP && L.kind != L_POOL && L.kind != L_EPI && L.kind != L_HOPC)
+    L.common().xcd_max = 0;
   switch (L.kind) {
     case L_ENCODE: {
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
