@@ -230,8 +230,9 @@ struct HopChainArgs {
   int m;                            // hops in the chain (2 .. kMaxChainHops)
   float* io[kMaxChainHops + 1];
   int filt[kMaxChainHops];
-  unsigned long long* ctr;          // this launch's barrier counter (monotonic, zeroed at plan creation)
-  int* err;                         // [0] expired barrier spins, [1] participants off XCD 0
+  unsigned long long* ctr;          // [0] this launch's barrier counter (monotonic, zeroed at plan creation),
+                                    // [1] the XCD of its logical block 0
+  int* err;                         // [0] expired barrier spins, [1] participants on another XCD than block 0
   int G;                            // participating (logical) workgroups
 };
 

@@ -462,14 +462,16 @@ __global__ __launch_bounds__(kBlock) void k_hop_coop(HopArgs a) {
 
 // ---------------------------------------------------------------------------- persistent hop chain
 // Middle hops k .. k+m-1 of one layer on a small scale in ONE launch (engine.h HopChainArgs;
-// verdict r3 item 6).  The grid is XCD-packed onto XCD 0 (c.xcd = 1; G <= 32 workgroups, one
-// tile per wave, all co-resident: nothing else runs on the stream), so every row a hop writes
-// stays in XCD 0's L2: stores and the next hop's row gathers are agent-scope relaxed atomics
-// (sc1: served by the L2, never a stale L1 line), and the barrier between hops is a relaxed
-// agent-scope counter -- no fences, nothing leaves the XCD.  Per hop the arithmetic is k_hop's
+// verdict r3 item 6).  G <= 32 workgroups, one tile per wave, all co-resident (nothing else
+// runs on the stream).  The rows a hop writes and the next hop gathers are agent-scope relaxed
+// atomic stores / loads (sc1: device-coherent, never a stale L1 line) and the barrier between
+// hops is a relaxed agent-scope counter -- no fences.  Agent scope is the whole device, so the
+// results do not depend on where the dispatcher puts the workgroups; the grid is launched
+// XCD-packed (c.xcd = 1: every 8th workgroup participates) so that the participants share one
+// XCD and its L2, and err[1] counts participants found on another XCD than the launch's
+// logical block 0 (placement health, a speed property).  Per hop the arithmetic is k_hop's
 // (LAST = false), operation for operation: bit-identical.  Every spin is bounded: an expired
-// spin counts in err[0] and the launch still finishes (results then unreliable, never a
-// hang); a participant found off XCD 0 counts in err[1] (the host checks both).
+// spin counts in err[0] and the launch still finishes (results then unreliable, never a hang).
 constexpr long kChainSpin = 1L << 22;
 __device__ __forceinline__ unsigned xcc_id() {
   unsigned v;
@@ -519,8 +521,11 @@ __global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int xb = logical_block(a.h.c);
   if (xb < 0) return;
+  const unsigned xcc = xcc_id();
   if (threadIdx.x == 0) {
-    if (xcc_id() != 0) atomicAdd(&a.err[1], 1);
+    // logical block 0 publishes its XCD before its first barrier arrival (chain_barrier waits
+    // for the store); the others compare after that barrier
+    if (xb == 0) __hip_atomic_store(a.ctr + 1, (unsigned long long)xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every launch adds exactly (m - 1) G arrivals and none can pass the first barrier before
     // all G have started: the value read here lies in [base, base + G) of this launch
     const unsigned long long v = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -576,6 +581,9 @@ __global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
       }
     }
     if (k + 1 < a.m) chain_barrier(a, base + (unsigned long long)(k + 1) * a.G);
+    if (k == 0 && threadIdx.x == 0 &&
+        __hip_atomic_load(a.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)xcc)
+      atomicAdd(&a.err[1], 1);
   }
 }
 

@@ -1566,15 +1566,16 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     int nchain = 0;
     for (auto* q : {&P->sched_fwd, &P->sched_roll})
       for (Launch& L : *q) nchain += L.kind == L_HOPC;
-    if ((rc = palloc(P.get(), &P->chain_ctr, (size_t)std::max(nchain, 1))) || (rc = palloc(P.get(), &P->chain_err, 2)))
-      return rc;
-    HIP_TRY(hipMemset(P->chain_ctr, 0, sizeof(unsigned long long) * std::max(nchain, 1)));
+    // per launch: [0] the barrier counter, [1] the XCD of the launch's logical block 0
+    const size_t nslot = 2 * (size_t)std::max(nchain, 1);
+    if ((rc = palloc(P.get(), &P->chain_ctr, nslot)) || (rc = palloc(P.get(), &P->chain_err, 2))) return rc;
+    HIP_TRY(hipMemset(P->chain_ctr, 0, sizeof(unsigned long long) * nslot));
     HIP_TRY(hipMemset(P->chain_err, 0, 2 * sizeof(int)));
     int i = 0;
     for (auto* q : {&P->sched_fwd, &P->sched_roll})
       for (Launch& L : *q)
         if (L.kind == L_HOPC) {
-          L.hopc.ctr = P->chain_ctr + i++;
+          L.hopc.ctr = P->chain_ctr + 2 * i++;
           L.hopc.err = P->chain_err;
         }
   }
@@ -1954,7 +1955,7 @@ int msw_set_trace(msw_plan* P, uint64_t* buf) {
   return MSW_OK;
 }
 
-int msw_plan_chain_health(const msw_plan* P, int32_t* chain_launches, int32_t* expired_spins, int32_t* off_xcd) {
+int msw_plan_chain_health(const msw_plan* P, int32_t* chain_launches, int32_t* expired_spins, int32_t* xcd_spread) {
   if (!P) return fail(MSW_ERR_INVALID, "null argument");
   int n = 0;
   for (const Launch& L : P->sched_roll) n += L.kind == L_HOPC;
@@ -1965,7 +1966,7 @@ int msw_plan_chain_health(const msw_plan* P, int32_t* chain_launches, int32_t* e
   }
   if (chain_launches) *chain_launches = n;
   if (expired_spins) *expired_spins = e[0];
-  if (off_xcd) *off_xcd = e[1];
+  if (xcd_spread) *xcd_spread = e[1];
   return MSW_OK;
 }
 

@@ -869,12 +869,12 @@ def test_fused_unpooling_matches_unpooling_launch(cuda, monkeypatch, F, kw):
 
 @pytest.mark.parametrize("model", ["msgnn_K4_F32", "msgnn_F64", "gnn"])
 def test_persistent_hop_chain_matches_separate_hops(cuda, monkeypatch, model):
-    """Middle hops of a layer as ONE persistent launch on XCD 0 (k_hop_chain: workgroups
-    synchronised through XCD 0's L2 between hops; MSW_HOP_CHAIN=1 on scales whose tiles fit one
-    XCD; =2 also the layer's last hop with its epilogue as the chain's final phase) == one
-    launch per hop (MSW_HOP_CHAIN=0), bit for bit: forward, rollout and a batch of two meshes;
-    fewer launches per step; no expired barrier spin and no workgroup off XCD 0
-    (msw_plan_chain_health); and the oracle."""
+    """Middle hops of a layer as ONE persistent launch (k_hop_chain: workgroups synchronised
+    by an agent-scope counter between hops, launched XCD-packed; MSW_HOP_CHAIN=1 on scales whose
+    tiles fit one XCD; =2 also the layer's last hop with its epilogue as the chain's final
+    phase) == one launch per hop (MSW_HOP_CHAIN=0), bit for bit: forward, rollout and a batch
+    of two meshes; fewer launches per step; no expired barrier spin (msw_plan_chain_health;
+    the XCD placement it reports is printed); and the oracle."""
     from mswegnn.batch import collate
     from mswegnn.engine import plan_for
     from mswegnn.rollout import rollout_test
@@ -904,9 +904,12 @@ def test_persistent_hop_chain_matches_separate_hops(cuda, monkeypatch, model):
     assert st["1"]["chain_launches"] > 0 and st["0"]["chain_launches"] == 0, st
     assert st["2"]["kernels_per_step"] < st["1"]["kernels_per_step"] < st["0"]["kernels_per_step"], st
     for sv in ("1", "2"):
-        assert st[sv]["chain_expired_spins"] == 0 and st[sv]["chain_off_xcd"] == 0, st[sv]
         for a, b in zip(outs["0"], outs[sv]):
             assert torch.equal(a, b), sv
+        assert st[sv]["chain_expired_spins"] == 0, st[sv]
+        # placement health (speed only: agent-scope accesses are device-coherent)
+        print(f"MSW_HOP_CHAIN={sv}: {st[sv]['chain_launches']} chain launches per step, "
+              f"{st[sv]['chain_xcd_spread']} participants on another XCD than their block 0")
     if model == "msgnn_K4_F32":
         m = build_msgnn(4, 32, 4, state=weights("K4_F32"))
         ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=32, K=4), ga)
