@@ -143,13 +143,16 @@ def global_rel(ours, fx, prefix):
     return (num / den) ** 0.5
 
 
-def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0):
+def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0, yard=None):
     """The gradient bar: every tensor within `tol` (relative: max|ours - ref| / max|ref|) of
     the reference's fp32 result, or -- for a tensor the fp32 reference itself does not
     resolve to `tol` (a PReLU slope's gradient sums every element of its layer; a mask flip
     of _mask_small_WD forks a rollout) -- no further from the reference's float64 result than
-    `slack` x the fp32 reference is.  Returns (worst error vs fp32, {tensor: (ours vs fp64,
-    fp32 ref vs fp64)} for the tensors that took the fp64 rule); asserts."""
+    `slack` x an fp32 yardstick is: the reference's own fp32 run, or (`yard`, optional) the
+    same algorithm in fp32 on the device under test (the drop-in's torch path), whichever
+    lands further from float64 -- how well fp32 arithmetic resolves that tensor at all.
+    Returns (worst error vs fp32, {tensor: (ours vs fp64, fp32 ref vs fp64[, yard vs fp64])}
+    for the tensors that took the fp64 rule); asserts."""
     errs = compare(ours, fx, prefix)
     worst = max(errs.values())
     rule64, bad = {}, {}
@@ -163,7 +166,11 @@ def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0):
         e_o = rel_err(ours.get(k, ours.get(prefix + k)), ref64)
         e_r = rel_err(torch.from_numpy(fx[prefix + k]), ref64)
         rule64[k] = (e_o, e_r)
+        if yard is not None:
+            e_y = rel_err(yard.get(k, yard.get(prefix + k)), ref64)
+            rule64[k] = (e_o, e_r, e_y)
+            e_r = max(e_r, e_y)
         if not e_o <= max(tol, slack * e_r):
-            bad[k] = (e, e_o, e_r)
+            bad[k] = (e, *rule64[k])
     assert not bad, (prefix, bad)
     return worst, rule64
