@@ -218,15 +218,6 @@ int msw_set_graph_capture(msw_plan* plan, int enable);
 
 int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
 
-/* Health of the persistent middle-hop chains (k_hop_chain: several hops in one launch, the
- * workgroups synchronised by an agent-scope counter, launched XCD-packed).  chain_launches:
- * chain launches in one rollout step; expired_spins: barrier waits that gave up (results of
- * those launches are not reliable -- the launch still finishes; must stay 0); xcd_spread:
- * participating workgroups found on another XCD than their launch's logical block 0 (the
- * placement the packing aims at: a speed property, results are device-coherent either way).
- * Synchronises the device. */
-int msw_plan_chain_health(const msw_plan* plan, int32_t* chain_launches, int32_t* expired_spins,
-                          int32_t* xcd_spread);
 
 /* Re-launch one kernel of the step `iters` times on `stream` (benchmark / roofline hook;
  * call after a forward or rollout: it reuses the plan's workspaces and overwrites scratch).

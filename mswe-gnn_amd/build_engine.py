@@ -62,9 +62,7 @@ def build(force=False, verbose=True, variant=""):
              "ew8": ["-DMSW_EDGE_WAVES=8"], "ew4": ["-DMSW_EDGE_WAVES=4"],
              "e0w12": ["-DMSW_EDGE_WAVES0=12"], "hw4": ["-DMSW_HOP_WAVES=4"],
              "hw10": ["-DMSW_HOP_WAVES=10"], "hw16": ["-DMSW_HOP_WAVES=16"],
-             "rdc2": ["-DMSW_ROW_DC=2"], "rdc4": ["-DMSW_ROW_DC=4"],
-             "ehpipe8": ["-DMSW_EH_PIPE=1", "-DMSW_EDGE_WAVES0=8"],
-             "ehpipe12": ["-DMSW_EH_PIPE=1", "-DMSW_EDGE_WAVES0=12"]}.get(variant, [])
+             "rdc2": ["-DMSW_ROW_DC=2"], "rdc4": ["-DMSW_ROW_DC=4"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     out = lib_path(variant)

@@ -220,22 +220,6 @@ struct HopArgs {
   const int2* redge; // [E] {internal source row, tile-padded s slot}, reference edge order
 };
 
-// Persistent middle-hop chain (k_hop_chain): hops k .. k+m-1 of one layer, no epilogue, in
-// ONE launch whose G workgroups all sit on XCD 0 (XCD packing, G <= kCusPerXcd), separated by
-// a barrier among them through XCD 0's L2 (relaxed agent-scope counter, no fences).  The rows
-// of hop i are io[i] -> io[i + 1] (the layer's ping-pong buffers); filt[i] its filter.
-constexpr int kMaxChainHops = 6;
-struct HopChainArgs {
-  HopArgs h;                        // the tiles, s, x_s, flags, Common (h.in / h.out / h.filt_a unused)
-  int m;                            // hops in the chain (2 .. kMaxChainHops)
-  float* io[kMaxChainHops + 1];
-  int filt[kMaxChainHops];
-  unsigned long long* ctr;          // [0] this launch's barrier counter (monotonic, zeroed at plan creation),
-                                    // [1] the XCD of its logical block 0
-  int* err;                         // [0] expired barrier spins, [1] participants on another XCD than block 0
-  int G;                            // participating (logical) workgroups
-};
-
 // Mean pooling into the coarse rows + projection of the next processor.
 
 struct PoolArgs {
@@ -334,7 +318,6 @@ template <int NT> hipError_t launch_encode(const EncodeArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
-template <int NT> hipError_t launch_hop_chain(const HopChainArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_epi(const EpiArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);

@@ -324,35 +324,6 @@ void k_edge_hop(EdgeHopArgs a) {
       __syncthreads();
       Wm = smem;
     }
-#if MSW_EH_PIPE
-    // build variant (MSW_EH_PIPE, with fewer waves per SIMD for the registers): k_hop's software
-    // pipeline -- tile i+1's gathers and tile i+2's lane record in flight while tile i runs
-    // its MLP chain (verdict r3 item 4: the gathers and the MFMA chains barely overlap)
-    if constexpr (!LST) {
-      if (tile < a.ntiles) {
-        EdgeHopRows<NT> q;
-        edge_hop_load<NT, LST>(q, a, tile, j, g);
-        int t1 = tile + stride;
-        LaneRec rn = load_rec(a.recs, t1 < a.ntiles ? t1 : tile, j);
-        for (;;) {
-          const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
-          const bool more = t1 < a.ntiles;
-          EdgeHopRows<NT> qn;
-          if (more) {
-            edge_hop_gather<NT, LST>(qn, a, rn, t1, jj, gg);
-            const int t2 = t1 + stride;
-            rn = load_rec(a.recs, t2 < a.ntiles ? t2 : t1, jj);
-          }
-          f32x4 res[NT];
-          edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, Wm, wf, &slab[w][0][0], jj, ln, gg, res);
-          edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
-          if (!more) break;
-          q = qn;
-          t1 += stride;
-        }
-      }
-    } else
-#endif
     for (; tile < a.ntiles; tile += stride) {
       const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
       EdgeHopRows<NT> q;

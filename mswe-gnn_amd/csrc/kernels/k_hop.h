@@ -1,4 +1,4 @@
-// gfx950 kernels: hops 2..K: edge tiles, row layout, feature split, cooperative last hop, persistent chain.
+// gfx950 kernels: hops 2..K: edge tiles, row layout, feature split, cooperative last hop.
 // Part of kernels_impl.h (included inside namespace msw, in this order); see its header
 // comment for the register layout and conventions.
 #pragma once
@@ -458,133 +458,6 @@ __global__ __launch_bounds__(kBlock) void k_hop_coop(HopArgs a) {
   coop_exchange<NT, P>(rs, res, b0, XW, r, j, g);  // its barrier also lands the staged operands
   if constexpr (kStaged<NT>) c.W = smem;
   node_epilogue_coop<NT, ACT, P>(res, a.epi, c, q.pre, a.out, (int)L.n, live && L.nv, r, lane, g, j, b0, b1, XW);
-}
-
-// ---------------------------------------------------------------------------- persistent hop chain
-// Middle hops k .. k+m-1 of one layer on a small scale in ONE launch (engine.h HopChainArgs;
-// verdict r3 item 6).  G <= 32 workgroups, one tile per wave, all co-resident (nothing else
-// runs on the stream).  The rows a hop writes and the next hop gathers are agent-scope relaxed
-// atomic stores / loads (sc1: device-coherent, never a stale L1 line) and the barrier between
-// hops is a relaxed agent-scope counter -- no fences.  Agent scope is the whole device, so the
-// results do not depend on where the dispatcher puts the workgroups; the grid is launched
-// XCD-packed (c.xcd = 1: every 8th workgroup participates) so that the participants share one
-// XCD and its L2, and err[1] counts participants found on another XCD than the launch's
-// logical block 0 (placement health, a speed property).  Per hop the arithmetic is k_hop's
-// (LAST = false), operation for operation: bit-identical.  Every spin is bounded: an expired
-// spin counts in err[0] and the launch still finishes (results then unreliable, never a hang).
-constexpr long kChainSpin = 1L << 22;
-__device__ __forceinline__ unsigned xcc_id() {
-  unsigned v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-  return v & 0xf;
-}
-__device__ __forceinline__ f32x4 ld4_l2(const float* p) {
-  f32x4 v;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return v;
-}
-__device__ __forceinline__ void st4_l2(float* p, f32x4 v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <int N>
-__device__ __forceinline__ void load_row_l2(f32x4 (&v)[N], const float* row, int g) {
-#pragma unroll
-  for (int t = 0; t < N; ++t) v[t] = ld4_l2(row + 16 * t + 4 * g);
-}
-// barrier among the chain's G workgroups: every wave's stores have reached the L2 (vmcnt(0))
-// before its workgroup arrives
-__device__ __forceinline__ void chain_barrier(const HopChainArgs& a, unsigned long long target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(a.ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    long n = 0;
-    while (__hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++n < kChainSpin)
-      __builtin_amdgcn_s_sleep(1);
-    if (n >= kChainSpin) atomicAdd(&a.err[0], 1);
-  }
-  __syncthreads();
-}
-// LASTPH: the chain's final hop is the layer's last hop (k_hop<.., LAST = true>'s path: its
-// epilogue operands -- projections of the next layer, unpool U, forward-mode decoder -- are
-// staged into LDS at kernel start, behind the middle hops).
-template <int NT, int ACT, bool LASTPH>
-__global__ __launch_bounds__(kBlock) void k_hop_chain(HopChainArgs a) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT;
-  constexpr int XS = F + 4;
-  __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
-  __shared__ unsigned long long base_s;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int xb = logical_block(a.h.c);
-  if (xb < 0) return;
-  const unsigned xcc = xcc_id();
-  if (threadIdx.x == 0) {
-    // logical block 0 publishes its XCD before its first barrier arrival (chain_barrier waits
-    // for the store); the others compare after that barrier
-    if (xb == 0) __hip_atomic_store(a.ctr + 1, (unsigned long long)xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every launch adds exactly (m - 1) G arrivals and none can pass the first barrier before
-    // all G have started: the value read here lies in [base, base + G) of this launch
-    const unsigned long long v = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long per = (unsigned long long)(a.m - 1) * a.G;
-    base_s = v - v % per;
-  }
-  __syncthreads();
-  const unsigned long long base = base_s;
-  const int tile = xb * kWaves + w;
-  const bool live = tile < a.h.ntiles;
-  const int tl = live ? tile : 0;  // idle waves stay in bounds
-  float* slab = &slab_all[w][0][0];
-  Common c = a.h.c;
-  const Lanes L = lanes_of(load_rec(a.h.recs, tl, j), tl, j, a.h.n0);
-  f32x4 sv[NT];
-  load_row<NT>(sv, a.h.s + L.p * F, g);  // s is fixed for the layer: plain loads
-  [[maybe_unused]] EpiPre<NT> pre;
-  if constexpr (LASTPH) {
-    if constexpr (kStaged<NT>) stage_glds<kWaves>(smem, c.W, a.h.reg, 0, a.h.reg.len);
-    epi_prefetch<NT>(pre, a.h.epi, c, a.h.xs, L.n, g);  // static inputs (x_s rows, X, BC)
-  }
-  for (int k = 0; k < a.m; ++k) {
-    const float* in = a.io[k];
-    float* out = a.io[k + 1];
-    f32x4 wf[NT][NT];
-    load_filter<NT>(wf, a.h.c.W, a.filt[k], lane);
-    f32x4 os[NT], inn[NT];
-    if (k == 0) {  // written by the previous launch: plain loads
-      load_row<NT>(os, in + L.sr * F, g);
-      load_row<NT>(inn, in + L.n * F, g);
-    } else {
-      load_row_l2<NT>(os, in + L.sr * F, g);
-      load_row_l2<NT>(inn, in + L.n * F, g);
-    }
-    if (live) {  // k_hop's core, LAST = false
-      float* my = slab + j * XS;
-      store_row<NT>(my, inn, NT, g);
-      wave_lds_sync();
-      f32x4 od[NT];
-      load_row<NT>(od, slab + L.dl * XS, g);
-      put_message<NT>(my, os, od, sv, L.ev, a.h.grad, a.h.upwind, g);
-      f32x4 agg[NT], res[NT];
-      gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) res[t] = inn[t];
-      apply_filter_regs<NT>(res, agg, a.filt[k], wf);
-      if (LASTPH && k + 1 == a.m) {  // the layer's last hop: k_hop<.., LAST = true>'s finish
-        if constexpr (kStaged<NT>) c.W = smem;  // staged at kernel start (every wave passed a barrier since)
-        node_epilogue<NT, ACT>(res, a.h.epi, c, pre, out, L.n, L.nv, lane, g);
-      } else if (L.nv) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) st4_l2(out + L.n * F + 16 * t + 4 * g, res[t]);
-      }
-    }
-    if (k + 1 < a.m) chain_barrier(a, base + (unsigned long long)(k + 1) * a.G);
-    if (k == 0 && threadIdx.x == 0 &&
-        __hip_atomic_load(a.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)xcc)
-      atomicAdd(&a.err[1], 1);
-  }
 }
 
 template <int NT>

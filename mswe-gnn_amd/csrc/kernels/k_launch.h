@@ -88,11 +88,6 @@ hipError_t prepare_kernels() {
           if (e != hipSuccess) return e;
         }
   }
-  // persistent hop chains whose final phase is the layer's last hop (epilogue region in LDS)
-  for (const void* f : {(const void*)k_hop_chain<NT, 1, true>, (const void*)k_hop_chain<NT, -1, true>}) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx(kWaves));
-    if (e != hipSuccess) return e;
-  }
   return hipSuccess;
 }
 
@@ -259,25 +254,6 @@ hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   return launch_hop_kernel<NT>(b, loop, grid, block, st);
 }
 template <int NT>
-hipError_t launch_hop_chain(const HopChainArgs& a, hipStream_t st) {
-  if (a.h.ntiles <= 0) return hipSuccess;
-  if (a.m < 2 || a.m > kMaxChainHops || a.G != cdiv(a.h.ntiles, kWaves) || a.G > kCusPerXcd || a.h.c.xcd_max < 1)
-    return hipErrorInvalidValue;  // the grid must be one XCD's, one workgroup per CU
-  HopChainArgs b = a;
-  b.h.c.xcd = 1;
-  const dim3 grid((unsigned)(a.G * kXcds)), block(kBlock);
-  if (!a.h.last) {
-    hipLaunchKernelGGL((k_hop_chain<NT, 1, false>), grid, block, 0, st, b);
-  } else {
-    const size_t sh = lds_bytes<NT>(a.h.reg.len);
-    if (a.h.c.prelu)
-      hipLaunchKernelGGL((k_hop_chain<NT, 1, true>), grid, block, sh, st, b);
-    else
-      hipLaunchKernelGGL((k_hop_chain<NT, -1, true>), grid, block, sh, st, b);
-  }
-  return hipGetLastError();
-}
-template <int NT>
 hipError_t launch_hop_kernel(const HopArgs& a, bool loop, dim3 grid, dim3 block, hipStream_t st) {
   if (!a.last) {
     if (loop) hipLaunchKernelGGL((k_hop<NT, 1, false, true>), grid, block, 0, st, a);
@@ -407,7 +383,6 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_edge_hop<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_edge_mlp<NT>(const EdgeHopArgs&, hipStream_t);       \
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
-  template hipError_t launch_hop_chain<NT>(const HopChainArgs&, hipStream_t);     \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
   template hipError_t launch_epi<NT>(const EpiArgs&, hipStream_t);                \
   template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);

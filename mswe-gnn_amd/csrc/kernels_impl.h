@@ -36,9 +36,10 @@ constexpr int waves_of() { return LOOP && NT <= 2 ? 8 : kWaves; }
 #endif
 template <int NT, bool LOOP>
 constexpr int hop_waves() { return LOOP && NT <= 2 ? MSW_HOP_WAVES : kWaves; }
-// the fused edge MLP + hop keeps one tile per wave in flight in its grid-stride loop:
-// a software-pipelined loop (next tile's gathers during the MLP) needs > 256 registers,
-// i.e. one wave per SIMD, and measured 24 % slower on the 1M-node mesh
+// the fused edge MLP + hop keeps one tile per wave in flight in its grid-stride loop: a
+// software-pipelined loop (tile i+1's gathers and tile i+2's record during tile i's MLP) fits
+// two waves per SIMD (212 VGPRs, no spills) and measured 5 % slower on the 1M-node mesh than
+// four waves per SIMD without it (673 vs 639 us, profiles/r04/ab_eh_pipe_hbm1m.txt; removed)
 #ifndef MSW_EDGE_WAVES
 #define MSW_EDGE_WAVES 12   // grid-stride, with epilogue (LST = 1): 3 waves per SIMD
 #endif

@@ -221,7 +221,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP, L_HOPC };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -243,7 +243,6 @@ struct Launch {
     PoolArgs pool;
     ExchangeArgs xch;
     EpiArgs ep;
-    HopChainArgs hopc;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
   Common& common() {
@@ -252,7 +251,6 @@ struct Launch {
       case L_EDGE_HOP:
       case L_EDGE_MLP: return eh.c;
       case L_HOP: return hop.c;
-      case L_HOPC: return hopc.h.c;
       case L_EXCHANGE: return xch.c;
       case L_EPI: return ep.c;
       default: return pool.c;
@@ -283,7 +281,6 @@ struct Knobs {
   int coop_waves = -1;      // MSW_COOP_WAVES      cooperative kernels while P x tiles <= this (-1 default)
   int epi_split_tiles = -1; // MSW_EPI_SPLIT_TILES row-epilogue threshold in edge tiles (-1 default)
   int trace_encode = 0;     // MSW_TRACE_ENCODE    diagnostic builds (-DMSW_TRACE): encoder marks only
-  int hop_chain = 0;        // MSW_HOP_CHAIN       persistent middle-hop chains on one-XCD scales (opt-in until measured)
 };
 inline Knobs knobs_from_env() {
   Knobs k;
@@ -294,8 +291,7 @@ inline Knobs knobs_from_env() {
       {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_EH_LOOP", &k.eh_loop},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
       {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
-      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode},
-      {"MSW_HOP_CHAIN", &k.hop_chain}};
+      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
   for (const auto& t : tab)
     if (const char* e = getenv(t.name)) *t.v = atoi(e);
   if (getenv("MSW_TRACE_ENCODE")) k.trace_encode = 1;
@@ -378,9 +374,6 @@ struct msw_plan {
   int xcd_max = 1;
   int coop_waves = 1024;
   Knobs kn;                 // engine switches of this plan (knobs_from_env)
-  // persistent hop chains (L_HOPC): one barrier counter per chain launch, shared error flags
-  unsigned long long* chain_ctr = nullptr;
-  int* chain_err = nullptr;
   // set when a fused (un)pooling launch's weight region would not fit its kernel's LDS cap
   // (edge_coop_lds_cap): the schedule is rebuilt with the pooling / unpooling launches
   int no_fuse = 0;
@@ -597,42 +590,6 @@ void sched_proc(msw_plan* P, std::vector<Launch>& q, const Proc& pr, float* out,
   }
   const float* cur = P->T[0];
   for (int k = 2; k <= pr.K;) {
-    // middle hops k .. K-1 as ONE persistent launch on XCD 0 (k_hop_chain) where the scale's
-    // tiles fit one XCD at one workgroup per CU (the coarse scales; not on parts: their
-    // exchanges sit between the hops)
-    // (MSW_HOP_CHAIN=2: the layer's last hop joins the chain as its final phase, k_hop's
-    // epilogue path, instead of its own -- cooperative -- launch)
-    const int with_last = P->kn.hop_chain >= 2 && pr.K - k + 1 <= kMaxChainHops ? 1 : 0;
-    const int nmid = pr.K - k + with_last;  // hops the chain would take
-    if (P->kn.hop_chain && P->part_rank < 0 && nmid >= 2 && P->xcd_max >= 1 && g.ntiles > 0 &&
-        (g.ntiles + kWaves - 1) / kWaves <= kCusPerXcd) {
-      const int m = std::min(nmid, kMaxChainHops);
-      const bool last = with_last && k + m - 1 == pr.K;
-      Launch L;
-      L.kind = L_HOPC;
-      L.scale = pr.scale;
-      HopChainArgs& h = L.hopc;
-      h.h.c = c;
-      h.h.n0 = g.n0; h.h.recs = g.recs; h.h.ntiles = g.ntiles;
-      h.h.s = P->s; h.h.xs = P->xs;
-      h.h.grad = pr.with_gradient; h.h.upwind = pr.upwind;
-      h.h.filt_a = -1;
-      h.h.last = last ? 1 : 0;
-      if (last) h.h.epi = epi;
-      h.m = m;
-      h.G = (g.ntiles + kWaves - 1) / kWaves;
-      float* b = const_cast<float*>(cur);
-      h.io[0] = b;
-      for (int i = 0; i < m; ++i) {
-        b = b == P->T[0] ? P->T[1] : P->T[0];
-        h.io[i + 1] = (last && i + 1 == m) ? out : b;
-        h.filt[i] = pr.filt.empty() ? -1 : pr.filt[k - 1 + i];
-      }
-      q.push_back(L);
-      cur = b;
-      k += m;
-      continue;
-    }
     sched_exchange(P, q, pr.scale, {{cur == P->T[0] ? B_T0 : B_T1, P->F}});
     // one launch per hop (hop chains -- several hops per launch with the halo recomputed --
     // measured 0.7-1.6 % slower under graph replay, profiles/r01_v7/ab_chains.txt; removed)
@@ -974,13 +931,6 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       reg = &a.reg;
     } else if (L.kind == L_EXCHANGE) {
       continue;  // no LDS weight region
-    } else if (L.kind == L_HOPC) {
-      HopArgs& a = L.hopc.h;  // the filters go from the blob into registers
-      if (!a.last) continue;  // ... and a final last hop stages its epilogue operands
-      RegionBuilder R(P->blob, 0);
-      rl.epi(R, a.epi);
-      a.reg = R.done();
-      reg = &a.reg;
     } else if (L.kind == L_EPI) {
       EpiArgs& a = L.ep;
       RegionBuilder R(P->blob, 0);
@@ -1033,10 +983,8 @@ bool row_hops_forced(const msw_plan* P) { return P->kn.hop_rows == 2; }
 constexpr long kEncCoopWaves = 4096;
 void set_grid_cap(msw_plan* P, Launch& L) {
   // XCD packing (Common::xcd_max) applies to the hop, edge-hop, pooling and row-epilogue
-  // launches (the only one-round grids small enough to fit one XCD) and to the persistent hop
-  // chains (always on XCD 0)
-  if (L.kind != L_HOP && L.kind != L_EDGE_HOP && L.kind != L_POOL && L.kind != L_EPI && L.kind != L_HOPC)
-    L.common().xcd_max = 0;
+  // launches (the only one-round grids small enough to fit one XCD)
+  if (L.kind != L_HOP && L.kind != L_EDGE_HOP && L.kind != L_POOL && L.kind != L_EPI) L.common().xcd_max = 0;
   switch (L.kind) {
     case L_ENCODE: {
       L.enc.max_blocks = resident_of(P->NT, 0, L.enc.c.prelu, 0, (size_t)L.enc.lds_floats * 4, 0);
@@ -1136,7 +1084,6 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       }
       break;
     case L_EXCHANGE: break;
-    case L_HOPC: break;  // grid fixed at schedule time (G workgroups on XCD 0)
     case L_EPI:
       caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len);
       break;
@@ -1184,7 +1131,6 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_ENCODE: return launch_encode<NT>(L.enc, st);
     case L_EDGE_HOP: return launch_edge_hop<NT>(L.eh, st);
     case L_EDGE_MLP: return launch_edge_mlp<NT>(L.eh, st);
-    case L_HOPC: return launch_hop_chain<NT>(L.hopc, st);
     case L_HOP: return launch_hop<NT>(L.hop, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
     case L_EPI: return launch_epi<NT>(L.ep, st);
@@ -1271,7 +1217,7 @@ void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
   for (Launch& L : q) {
     if (L.kind == L_ENCODE) L.enc.x = x;
     Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi
-                 : L.kind == L_HOPC ? &L.hopc.h.epi : L.kind == L_EPI ? &L.ep.epi : nullptr;
+                 : L.kind == L_EPI ? &L.ep.epi : nullptr;
     if (e && e->dec.on) {
       e->dec.X = x;
       e->dec.y = y;
@@ -1561,23 +1507,6 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
                                            std::to_string(eh_lds_bytes(bad->eh.reg_nf)) + " B)");
     P->no_fuse = 1;
     P->blob.h.resize(blob0);  // drop the regions of the fused schedule
-  }
-  {  // persistent hop chains: a zeroed barrier counter per launch, the shared error flags
-    int nchain = 0;
-    for (auto* q : {&P->sched_fwd, &P->sched_roll})
-      for (Launch& L : *q) nchain += L.kind == L_HOPC;
-    // per launch: [0] the barrier counter, [1] the XCD of the launch's logical block 0
-    const size_t nslot = 2 * (size_t)std::max(nchain, 1);
-    if ((rc = palloc(P.get(), &P->chain_ctr, nslot)) || (rc = palloc(P.get(), &P->chain_err, 2))) return rc;
-    HIP_TRY(hipMemset(P->chain_ctr, 0, sizeof(unsigned long long) * nslot));
-    HIP_TRY(hipMemset(P->chain_err, 0, 2 * sizeof(int)));
-    int i = 0;
-    for (auto* q : {&P->sched_fwd, &P->sched_roll})
-      for (Launch& L : *q)
-        if (L.kind == L_HOPC) {
-          L.hopc.ctr = P->chain_ctr + 2 * i++;
-          L.hopc.err = P->chain_err;
-        }
   }
   P->blob.alloc(256);  // slack: LDS-DMA chunks may read up to 255 floats past a region
   if ((rc = pupload(P.get(), &P->dW, P->blob.h))) return rc;
@@ -1952,21 +1881,6 @@ int msw_set_trace(msw_plan* P, uint64_t* buf) {
     for (Launch& L : *q)
       L.common().trace = (!enc_only || L.kind == L_ENCODE) ? reinterpret_cast<unsigned long long*>(buf) : nullptr;
   P->drop_graphs();  // the captured steps hold the old arguments
-  return MSW_OK;
-}
-
-int msw_plan_chain_health(const msw_plan* P, int32_t* chain_launches, int32_t* expired_spins, int32_t* xcd_spread) {
-  if (!P) return fail(MSW_ERR_INVALID, "null argument");
-  int n = 0;
-  for (const Launch& L : P->sched_roll) n += L.kind == L_HOPC;
-  int e[2] = {0, 0};
-  if (P->chain_err) {
-    HIP_TRY(hipSetDevice(P->device));
-    HIP_TRY(hipMemcpy(e, P->chain_err, sizeof(e), hipMemcpyDeviceToHost));
-  }
-  if (chain_launches) *chain_launches = n;
-  if (expired_spins) *expired_spins = e[0];
-  if (xcd_spread) *xcd_spread = e[1];
   return MSW_OK;
 }
 

@@ -122,7 +122,6 @@ SYMBOLS = [
     ("msw_debug_buffer", C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_void_p]),
     ("msw_set_graph_capture", C.c_int, [C.c_void_p, C.c_int]),
     ("msw_plan_get_stats", C.c_int, [C.c_void_p, C.POINTER(MswPlanStats)]),
-    ("msw_plan_chain_health", C.c_int, [C.c_void_p, c_int32_p, c_int32_p, c_int32_p]),
     ("msw_last_error", C.c_char_p, []),
     ("msw_abi_version", C.c_int, []),
     ("msw_struct_size", C.c_int64, [C.c_char_p]),

@@ -305,9 +305,6 @@ class EnginePlan:
         s = L.MswPlanStats()
         L.check(L.lib().msw_plan_get_stats(self._h, C.byref(s)))
         out = {k: getattr(s, k) for k, _ in L.MswPlanStats._fields_}
-        n, spins, off = C.c_int32(), C.c_int32(), C.c_int32()
-        L.check(L.lib().msw_plan_chain_health(self._h, C.byref(n), C.byref(spins), C.byref(off)))
-        out.update(chain_launches=n.value, chain_expired_spins=spins.value, chain_xcd_spread=off.value)
         return out
 
 
