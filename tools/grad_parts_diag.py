@@ -22,6 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sets", nargs="+", default=["b1"])
     ap.add_argument("--R", nargs="+", type=int, default=[1, 4])
+    ap.add_argument("--all-tensors", action="store_true", help="report every parameter tensor")
+    ap.add_argument("--subsets", default="", help="comma list of subsets (default: all of them)")
     ap.add_argument("names", nargs="*")
     a = ap.parse_args()
     import torch
@@ -32,7 +34,10 @@ def main():
     fx = gc.golden("fx_grad_train_K4_F32")
     orig = (ag.supported, ag.mlp_supported, ag.pool_supported)
     off = lambda *args: False  # noqa: E731
-    subsets = {"all": (1, 1, 1), "swegnn": (1, 0, 0), "mlp": (0, 1, 0), "pool": (0, 0, 1), "none": (0, 0, 0)}
+    subsets = {"all": (1, 1, 1), "swegnn": (1, 0, 0), "mlp": (0, 1, 0), "pool": (0, 0, 1), "none": (0, 0, 0),
+               "swegnn+mlp": (1, 1, 0), "swegnn+pool": (1, 0, 1), "mlp+pool": (0, 1, 1)}
+    if a.subsets:
+        subsets = {k: v for k, v in subsets.items() if k in a.subsets.split(",")}
     for sname in a.sets:
         for R in a.R:
             p64 = f"{sname}_R{R}_fp64__"
@@ -43,11 +48,12 @@ def main():
                 ours, _ = gc.training_step_case(dev, sname, R)
                 if not names and label == "all":
                     names = [k[len("g__"):] for k in ours if k.startswith("g__") and
-                             rel_err(ours[k], torch.from_numpy(fx[p64 + k])) > 1e-4]
+                             (a.all_tensors or rel_err(ours[k], torch.from_numpy(fx[p64 + k])) > 1e-4)]
                 errs = {n: rel_err(ours["g__" + n], torch.from_numpy(fx[p64 + "g__" + n])) for n in names}
                 ref = {n: rel_err(torch.from_numpy(fx[f"{sname}_R{R}__g__{n}"]), torch.from_numpy(fx[p64 + "g__" + n]))
                        for n in names}
-                print(json.dumps({"set": sname, "R": R, "hip_parts": label, "global_vs_fp64": gc.global_rel(ours, fx, p64),
+                print(json.dumps({"set": sname, "R": R, "hip_parts": label, "loss": float(ours["loss"]),
+                                  "loss_ref": float(fx[f"{sname}_R{R}__loss"]), "global_vs_fp64": gc.global_rel(ours, fx, p64),
                                   "tensor_vs_fp64": errs, "reference_fp32_vs_fp64": ref}), flush=True)
     ag.supported, ag.mlp_supported, ag.pool_supported = orig
 
