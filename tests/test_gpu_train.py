@@ -297,10 +297,14 @@ def test_hip_msgnn_gradients_vs_reference_fixture(cuda):
 def test_hip_training_step_vs_reference_fixture(cuda, sname, R):
     """The reference's training_step (config.yaml trainer_options; one- and two-graph batches,
     1 and 4 rollout steps) with every layer on the HIP training kernels: loss and every
-    parameter gradient against the reference's (1e-4 per tensor, else the fp64 rule, whose
-    fp32 yardstick also counts the drop-in's torch path on this GPU: tensors whose gradient
-    is ~1e-5 of the whole -- PReLU slopes and biases summed over every edge -- are resolved
-    only to ~1e-4 by ANY fp32 summation order)."""
+    parameter gradient against the reference's (1e-4 per tensor, else an absolute error
+    within 1e-6 x the model's largest gradient entry, else the fp64 rule whose fp32
+    yardstick also counts the drop-in's torch path on this GPU; grad_cases.check).  Tensors
+    whose gradient is ~1e-4 of the model's -- PReLU slopes and biases summed over every edge
+    -- are resolved only to ~1e-4 relative by ANY fp32 summation order: switching the HIP
+    layer kinds on one at a time scatters their error over 1.8e-4 .. 5.8e-4 on b1 (the
+    reference's own fp32 run 1.8e-4; tools/grad_parts_diag.py,
+    profiles/r04/grad_parts_b1_R1_all_tensors.jsonl)."""
     import grad_cases as gc
     from mswegnn import autograd as ag
     calls = ag.MLP_CALLS[0]
