@@ -90,10 +90,7 @@ struct Common {
   const float* zrow;       // kZeroRow zeros: the address of a load a flag switches off
   unsigned long long* trace;  // diagnostic builds (-DMSW_TRACE): per-phase timestamps of wave 0
   int xcd_max;             // XCD packing of small grids: at most this many XCDs (0 = off)
-  int xcd;                 // set by the launcher: this launch runs on xcd XCDs (0 = all): XCDs
-                           // 0 .. xcd-1, or the xcd XCDs of xcd_mask
-  int xcd_mask;            // packing onto these XCDs (bit x = XCD x; 0 = the lowest ones)
-  int xcd_wgcu;            // workgroups per CU a packed grid may put on its XCDs (>= 1)
+  int xcd;                 // set by the launcher: this launch runs on XCDs 0 .. xcd-1 (0 = all)
 };
 
 // Encoder.  Scale ranges start at multiples of 64 rows, so a workgroup has one scale.

@@ -30,10 +30,6 @@ __device__ __forceinline__ int logical_block(const Common& c) {
   const int b = blockIdx.x;
   if (c.xcd <= 0) return b;
   const int x = b % kXcds;
-  if (c.xcd_mask) {
-    if (!((c.xcd_mask >> x) & 1)) return -1;
-    return (b / kXcds) * c.xcd + __builtin_popcount((unsigned)c.xcd_mask & ((1u << x) - 1u));
-  }
   return x < c.xcd ? (b / kXcds) * c.xcd + x : -1;
 }
 __device__ __forceinline__ int wave_row0() { return (blockIdx.x * kWaves + wave_id()) * kRowsPerWave; }

@@ -147,20 +147,10 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
 }
 
 // XCD packing of a one-round grid of g workgroups (b: the launch's argument copy): the
-// fewest XCDs (1, 2, 4 <= c.xcd_max) that hold one workgroup per CU, else all eight; with an
-// XCD mask (MSW_XCD_MASK, diagnostics), the mask's XCDs when they hold the grid at
-// c.xcd_wgcu workgroups per CU
+// fewest XCDs (1, 2, 4 <= c.xcd_max) that hold one workgroup per CU, else all eight
 template <class A>
 static inline dim3 xcd_grid(A& b, long g) {
   b.c.xcd = 0;
-  if (b.c.xcd_mask && b.c.xcd_max > 0) {
-    const int k = __builtin_popcount((unsigned)b.c.xcd_mask);
-    if (g <= (long)kCusPerXcd * k * std::max(1, b.c.xcd_wgcu)) {
-      b.c.xcd = k;
-      return dim3((unsigned)(cdiv(g, k) * kXcds));
-    }
-    return dim3((unsigned)g);
-  }
   for (int k = 1; k <= b.c.xcd_max && k < kXcds; k *= 2)
     if (g <= (long)kCusPerXcd * k) {
       b.c.xcd = k;

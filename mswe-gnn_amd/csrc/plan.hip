@@ -278,8 +278,6 @@ struct Knobs {
   int pool_wide = 1;        // MSW_POOL_WIDE       2F / 16 waves per pooling tile
   int tile_pack = 1;        // MSW_TILE_PACK       degree-aware destination order
   int xcd_max = 1;          // MSW_XCD_MAX         XCD packing of small grids (0 = all eight XCDs)
-  int xcd_mask = 0;         // MSW_XCD_MASK        pack onto these XCDs (bit x = XCD x, e.g. 0x1e; 0 = lowest)
-  int xcd_wgcu = 1;         // MSW_XCD_WGCU        workgroups per CU a masked packing may use
   int coop_waves = -1;      // MSW_COOP_WAVES      cooperative kernels while P x tiles <= this (-1 default)
   int epi_split_tiles = -1; // MSW_EPI_SPLIT_TILES row-epilogue threshold in edge tiles (-1 default)
   int trace_encode = 0;     // MSW_TRACE_ENCODE    diagnostic builds (-DMSW_TRACE): encoder marks only
@@ -292,11 +290,10 @@ inline Knobs knobs_from_env() {
       {"MSW_COOP2_DIRECT", &k.coop2_direct}, {"MSW_COOP2_F64", &k.coop2_f64}, {"MSW_ENC_COOP", &k.enc_coop},
       {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_EH_LOOP", &k.eh_loop},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
-      {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_XCD_MASK", &k.xcd_mask}, {"MSW_XCD_WGCU", &k.xcd_wgcu},
-      {"MSW_COOP_WAVES", &k.coop_waves},
+      {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
       {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
   for (const auto& t : tab)
-    if (const char* e = getenv(t.name)) *t.v = (int)strtol(e, nullptr, 0);  // decimal or 0x hex
+    if (const char* e = getenv(t.name)) *t.v = atoi(e);
   if (getenv("MSW_TRACE_ENCODE")) k.trace_encode = 1;
   return k;
 }
@@ -502,8 +499,6 @@ Common common_of(msw_plan* P) {
   Common c{};
   c.W = P->dW; c.perm = P->perm_d; c.nnf = P->nnf; c.dyn = P->dyn; c.p = P->p; c.zrow = P->zrow_d;
   c.xcd_max = P->xcd_max;
-  c.xcd_mask = P->kn.xcd_mask & 0xff;
-  c.xcd_wgcu = std::max(1, P->kn.xcd_wgcu);
   c.nstat_raw = P->nstat_raw; c.with_wl = P->with_wl; c.prelu = P->prelu;
   return c;
 }
