@@ -3,7 +3,8 @@
 # roofline timing summary + step breakdown), the two PMC passes (-> HBM traffic summary), both
 # copied into profiles/ on the box so that the closing bench line reads sources measured on
 # the library it loads (roofline.rocprof / traffic_source: stale = false), then that bench
-# line, the F = 64 and config-5 lines.  Every GPU step has its own time limit.
+# line, the F = 64 and config-5 lines, a two-rank gloo rehearsal of the N > 1 line.  Every GPU
+# step has its own time limit.
 #   bash tools/gpu_final_r04.sh OUTDIR
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -31,4 +32,8 @@ cp $OUT/roofline_rocprof.json profiles/roofline_rocprof.json && cp $OUT/pmc_summ
 step bench 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 step bench_f64 300 python bench.py --workload zenodo4_f64 --no-roofline-large > $OUT/bench_f64.json 2> $OUT/bench_f64.err
 step bench_hbm1m 400 python bench.py --workload hbm1m --no-cpu-baseline --steps 3 --warmup 1 > $OUT/bench_hbm1m.json 2> $OUT/bench_hbm1m.err
+# the N > 1 path rehearsed on the one-GPU box: two ranks over gloo sharing cuda:0, the
+# post-timed extras inside one --extras-budget (per-section wall_s, skipped sections marked)
+step rehearsal 420 env MSW_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --extras-budget 180 > $OUT/rehearsal_2rank_gloo.json 2> $OUT/rehearsal_2rank_gloo.err
 echo done >> $OUT/steps.log
