@@ -52,6 +52,25 @@ def runs_of(path):
     return out
 
 
+def roles_of(runs):
+    """bench.py's timing runs by role, in its order: the default workload's finest middle hop
+    (k_hop), fused edge MLP + hop (k_edge_hop), pooling (k_pool*, when the schedule has a
+    pooling launch), then the ~1M-node mesh's middle hop (k_hop / k_hop_rows) and edge MLP +
+    hop -- matched by kernel kind, so a role the run does not time is absent, never shifted."""
+    ours = [r for r in runs if r["kernel"].startswith("k_")]  # engine kernels only
+    kind = {"hop": ("k_hop<", "k_hop_rows", "k_hop_split"), "edge_hop": ("k_edge_hop",), "pool": ("k_pool",)}
+    want = [("hop", "hop"), ("edge_hop", "edge_hop"), ("pool", "pool"), ("hop_large", "hop"),
+            ("edge_hop_large", "edge_hop")]
+    out, i = {}, 0
+    for role, k in want:
+        for j in range(i, len(ours)):
+            if ours[j]["kernel"].startswith(kind[k]):
+                out[role] = ours[j]
+                i = j + 1
+                break
+    return out
+
+
 def main(argv):
     path = argv[1]
     runs = runs_of(path)
@@ -60,10 +79,9 @@ def main(argv):
               f"avg duration {r['avg_duration_us']:9.2f} us  period {r['period_us']:9.2f} us")
     if "--json" in argv:
         out = argv[argv.index("--json") + 1]
-        ours = [r for r in runs if r["kernel"].startswith("k_")]  # engine kernels only
         with open(out, "w") as f:
             json.dump({"source": path, "library_sha256": library_sha256(), "runs": runs,
-                       "by_role": {ROLES[i]: r for i, r in enumerate(ours[:len(ROLES)])}}, f, indent=1)
+                       "by_role": roles_of(runs)}, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -11,8 +11,10 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 kps = int(sys.argv[2]) if len(sys.argv) > 2 else None
 starts = [i for i, r in enumerate(rows) if "k_encode" in r["Kernel_Name"]]
-if kps is None:
-    kps = min(b - a for a, b in zip(starts, starts[1:]))
+if kps is None:  # the most common distance between encoder launches (rollout steps), not the
+    # rollout prologue's shorter one
+    diffs = [b - a for a, b in zip(starts, starts[1:])]
+    kps = max(set(diffs), key=diffs.count)
 dur = defaultdict(list)
 gap = defaultdict(list)
 name = {}
