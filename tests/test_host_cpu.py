@@ -787,3 +787,30 @@ def test_extras_budget_two_ranks_gloo(budget):
     else:
         assert "t1_ms" in sets[3] and "speedup" in sets[3] and sets[3]["gathered_vs_single_gpu_max_rel"] <= 1e-5
         assert "skipped" not in sets[40] or sets[40]["skipped"] == "budget"
+
+
+def test_roofline_roles_match_kernel_kinds(tmp_path):
+    """tools/roofline_check.py maps bench.py's timing runs (>= 20 back-to-back launches of one
+    kernel in the rocprofv3 trace) to roles by kernel KIND, in bench.py's order: a role the
+    run does not time (the pooling launch, fused away) is absent instead of shifting the
+    large-mesh roles onto the wrong kernels (round-4 fix)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import roofline_check as rc
+    seq = [("void msw::k_hop<2, 1, false, false>(msw::HopArgs)", 25, 5),
+           ("void msw::k_edge_hop<2, 1, false, 0>(msw::EdgeHopArgs)", 25, 12),
+           ("void at::native::vectorized_gather_kernel<16, long>(char*)", 30, 4),
+           ("void msw::k_hop_rows<2>(msw::HopArgs)", 21, 144),
+           ("void msw::k_edge_hop<2, 1, true, 0>(msw::EdgeHopArgs)", 20, 630)]
+    path = tmp_path / "trace.csv"
+    t = 0
+    with open(path, "w") as f:
+        f.write("Kernel_Name,Grid_Size,Start_Timestamp,End_Timestamp\n")
+        for name, n, dur in seq:
+            for _ in range(n):
+                f.write(f"\"{name}\",1024,{t},{t + dur * 1000}\n")
+                t += dur * 1000 + 500
+    roles = rc.roles_of(rc.runs_of(str(path)))
+    assert sorted(roles) == ["edge_hop", "edge_hop_large", "hop", "hop_large"]
+    assert roles["hop"]["kernel"].startswith("k_hop<") and roles["edge_hop"]["kernel"].startswith("k_edge_hop<2, 1, false")
+    assert roles["hop_large"]["kernel"] == "k_hop_rows<2>" and abs(roles["hop_large"]["avg_duration_us"] - 144) < 1e-9
+    assert roles["edge_hop_large"]["kernel"].startswith("k_edge_hop<2, 1, true")
