@@ -556,119 +556,130 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   const Lanes& L = q.L;
   // the MLP region: staged in LDS, or (wdirect: two workgroups per CU) read from its blob copy
   if (a.reg.len > 0 && !a.wdirect) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
-  const float* Wm = a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W;
-  float* my = &slab[j][0];
-  if constexpr (FUSE != 0) {
-    // source side -> exchange rows (in xbuf, free until the MLP), destination side -> the
-    // node slab; projection operands from the blob (c.W), its output tiles split over the
-    // ranks of a side
-    constexpr int XPB = 16 * T2 + 16 * NT + 4;
-    static_assert(kRowsPerWave * XPB <= 2 * kRowsPerWave * XW, "exchange rows fit the xbuf pair");
-    float* pb = &xbuf[0][0][0] + j * XPB;
-    f32x4 xp[NT];
-    pool_mean<NT>(xp, pin, a, g);
-    const f32x4(&xsr)[NT] = pin.xs;
-    if (a.pool.np.h1t == T2)
-      pool_project_part<NT, P, T2>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
-    else
-      pool_project_part<NT, P, NT>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
+  // the MLP operands through a pointer the compiler can prove to be LDS when staged (the
+  // run-time LDS-or-blob choice made every weight read a FLAT load, which also waits on vmcnt)
+  auto rest = [&](const float* Wm) __attribute__((always_inline)) {
+    float* my = &slab[j][0];
+    if constexpr (FUSE != 0) {
+      // source side -> exchange rows (in xbuf, free until the MLP), destination side -> the
+      // node slab; projection operands from the blob (c.W), its output tiles split over the
+      // ranks of a side
+      constexpr int XPB = 16 * T2 + 16 * NT + 4;
+      static_assert(kRowsPerWave * XPB <= 2 * kRowsPerWave * XW, "exchange rows fit the xbuf pair");
+      float* pb = &xbuf[0][0][0] + j * XPB;
+      f32x4 xp[NT];
+      pool_mean<NT>(xp, pin, a, g);
+      const f32x4(&xsr)[NT] = pin.xs;
+      if (a.pool.np.h1t == T2)
+        pool_project_part<NT, P, T2>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
+      else
+        pool_project_part<NT, P, NT>(side ? my : pb, xp, xsr, a.pool.np, c.W, lane, g, side, r % (P / 2));
+      __syncthreads();
+      load_row<T2>(q.Us, pb, g);
+      load_row<NT>(q.os, pb + 16 * T2, g);
+    } else if (r == 0) {
+      store_row<T2>(my, q.Vn, T2, g);
+      store_row<NT>(my + 16 * T2, q.inn, NT, g);
+    }
+    __syncthreads();  // node rows and the MLP region have landed (fused pooling: and every rank
+                      // has read its exchange rows before the MLP's exchanges reuse xbuf)
+    const float* dr = &slab[L.dl][0];
+    f32x4 H[T2], od[NT];
+    const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+    f32x4 vr[T2], br[T2];
+#pragma unroll
+    for (int t = 0; t < T2; ++t) {
+      const int off = 16 * t + 4 * g;
+      vr[t] = ld4(dr + off);
+      br[t] = ld4(Wm + b1 + off);
+    }
+#pragma unroll
+    for (int t = 0; t < T2; ++t) {
+      const f32x4 p = a.Pe ? q.Ps[t] : br[t];
+      H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
+    }
+    load_row<NT>(od, dr + 16 * T2, g);
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      coop_run_mlp<T2, T2, NT, ACT, P>(H, sv, a.rest, Wm, lane, g, j, r, &xbuf[0][0][0], &xbuf[1][0][0], XW);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 v = sv[t] / nrm;
+        v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
+        v.y = (v.y == v.y) ? v.y : 0.f;
+        v.z = (v.z == v.z) ? v.z : 0.f;
+        v.w = (v.w == v.w) ? v.w : 0.f;
+        sv[t] = v;
+      }
+    }
+    if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
+    // every rank has read the slab's node rows before the first MLP exchange barrier: rank 0
+    // may overwrite them with the messages (a.rest.n == 0 has no barrier: add one)
+    if (a.rest.n == 0) __syncthreads();
+    if (r == 0) put_message<NT>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
     __syncthreads();
-    load_row<T2>(q.Us, pb, g);
-    load_row<NT>(q.os, pb + 16 * T2, g);
-  } else if (r == 0) {
-    store_row<T2>(my, q.Vn, T2, g);
-    store_row<NT>(my + 16 * T2, q.inn, NT, g);
-  }
-  __syncthreads();  // node rows and the MLP region have landed (fused pooling: and every rank
-                    // has read its exchange rows before the MLP's exchanges reuse xbuf)
-  const float* dr = &slab[L.dl][0];
-  f32x4 H[T2], od[NT];
-  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
-  f32x4 vr[T2], br[T2];
+    f32x4 agg[NT];
+    gather_messages<NT, XS>(agg, &slab[0][0], L.q0, L.q1, g);
+    // this rank's tile of inn / agg / skip by address (a 4-way select over a register array
+    // was turned back into a scratch-indexed load): inn sits past the messages in the slab row
+    f32x4 rs[TS];
 #pragma unroll
-  for (int t = 0; t < T2; ++t) {
-    const int off = 16 * t + 4 * g;
-    vr[t] = ld4(dr + off);
-    br[t] = ld4(Wm + b1 + off);
-  }
+    for (int t = 0; t < TS; ++t) rs[t] = ld4(&slab[j][16 * T2 + 16 * (r * TS + t) + 4 * g]);
+    if (a.filt_a >= 0) {
+      f32x4 acc[TS];
 #pragma unroll
-  for (int t = 0; t < T2; ++t) {
-    const f32x4 p = a.Pe ? q.Ps[t] : br[t];
-    H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
-  }
-  load_row<NT>(od, dr + 16 * T2, g);
-  act_tiles<ACT, T2>(H, a.act1, a.slope1);
-  f32x4 sv[NT];
-  if (a.rest.n > 0) {
-    coop_run_mlp<T2, T2, NT, ACT, P>(H, sv, a.rest, Wm, lane, g, j, r, &xbuf[0][0][0], &xbuf[1][0][0], XW);
-  } else {
+      for (int t = 0; t < TS; ++t) acc[t] = zero4();
 #pragma unroll
-    for (int t = 0; t < NT; ++t) sv[t] = H[t];
-  }
-  if (a.normalize) {
-    float ss = 0.f;
+      for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-    const float nrm = sqrtf(row_sum(ss));
+        for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      f32x4 v = sv[t] / nrm;
-      v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
-      v.y = (v.y == v.y) ? v.y : 0.f;
-      v.z = (v.z == v.z) ? v.z : 0.f;
-      v.w = (v.w == v.w) ? v.w : 0.f;
-      sv[t] = v;
+          for (int t = 0; t < TS; ++t) acc[t] = MSW_MFMA(wr[t][ti][rr], agg[ti][rr], acc[t]);
+#pragma unroll
+      for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < TS; ++t) {
+        f32x4 ag = zero4();
+        for (int qq = L.q0; qq < L.q1; ++qq) ag = ag + ld4(&slab[qq][16 * (r * TS + t) + 4 * g]);
+        rs[t] = rs[t] + ag;
+      }
     }
-  }
-  if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
-  // every rank has read the slab's node rows before the first MLP exchange barrier: rank 0
-  // may overwrite them with the messages (a.rest.n == 0 has no barrier: add one)
-  if (a.rest.n == 0) __syncthreads();
-  if (r == 0) put_message<NT>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
-  __syncthreads();
-  f32x4 agg[NT];
-  gather_messages<NT, XS>(agg, &slab[0][0], L.q0, L.q1, g);
-  // this rank's tile of inn / agg / skip by address (a 4-way select over a register array
-  // was turned back into a scratch-indexed load): inn sits past the messages in the slab row
-  f32x4 rs[TS];
+    if (a.skip) {
 #pragma unroll
-  for (int t = 0; t < TS; ++t) rs[t] = ld4(&slab[j][16 * T2 + 16 * (r * TS + t) + 4 * g]);
-  if (a.filt_a >= 0) {
-    f32x4 acc[TS];
-#pragma unroll
-    for (int t = 0; t < TS; ++t) acc[t] = zero4();
-#pragma unroll
-    for (int ti = 0; ti < NT; ++ti)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-        for (int t = 0; t < TS; ++t) acc[t] = MSW_MFMA(wr[t][ti][rr], agg[ti][rr], acc[t]);
-#pragma unroll
-    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
-  } else {
-#pragma unroll
-    for (int t = 0; t < TS; ++t) {
-      f32x4 ag = zero4();
-      for (int qq = L.q0; qq < L.q1; ++qq) ag = ag + ld4(&slab[qq][16 * (r * TS + t) + 4 * g]);
-      rs[t] = rs[t] + ag;
+      for (int t = 0; t < TS; ++t) rs[t] = rs[t] + ld4(a.skip + L.n * F + 16 * (r * TS + t) + 4 * g);
     }
-  }
-  if (a.skip) {
-#pragma unroll
-    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + ld4(a.skip + L.n * F + 16 * (r * TS + t) + 4 * g);
-  }
-  f32x4 res[NT];
-  coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? &xbuf[1][0][0] : &xbuf[0][0][0], XW, r, j, g);
-  if (LST && a.last) {
-    const Epilogue& e = a.epi;
-    if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
-    if (live && r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
-    if (e.np.h1t == T2)
-      np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv && live, r, lane, g);
+    f32x4 res[NT];
+    coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? &xbuf[1][0][0] : &xbuf[0][0][0], XW, r, j, g);
+    if (LST && a.last) {
+      const Epilogue& e = a.epi;
+      if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
+      if (live && r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
+      if (e.np.h1t == T2)
+        np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv && live, r, lane, g);
+      else
+        np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv && live, r, lane, g);
+    } else if (live && r == 0 && L.nv && a.out) {
+      store_row<NT>(a.out + L.n * F, res, NT, g);
+    }
+  };
+  if constexpr (kLdsW) {
+    if (a.reg.len > 0 && !a.wdirect)
+      rest((const float*)smem);
     else
-      np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, L.nv && live, r, lane, g);
-  } else if (live && r == 0 && L.nv && a.out) {
-    store_row<NT>(a.out + L.n * F, res, NT, g);
+      rest(a.reg.len > 0 ? c.W + a.reg.off : c.W);
+  } else {
+    rest(a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W);
   }
 }
 

@@ -3,6 +3,14 @@
 // comment for the register layout and conventions.
 #pragma once
 
+// F = 64 MLP operands in LDS read through a pointer the compiler can prove to be LDS
+// (ds_read); MSW_FLAT_W=1 builds the round-3 form, one pointer that is LDS or the blob at run
+// time (FLAT loads, which also wait on vmcnt) -- the A/B build variant
+#ifndef MSW_FLAT_W
+#define MSW_FLAT_W 0
+#endif
+constexpr bool kLdsW = !MSW_FLAT_W;
+
 // ---------------------------------------------------------------------------- message passing
 // One wave = one edge tile (whole destination neighbourhoods, <= 16 edges, <= 16 nodes).
 // Lane j is edge slot j in the edge phase and destination j in the node phase; per-node
@@ -309,7 +317,13 @@ void k_edge_hop(EdgeHopArgs a) {
     }
     MSW_MARK(c, 2);
     f32x4 res[NT];
-    if (live) edge_hop_core<NT, ACT, XS>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
+    // F = 64: the MLP operands through a pointer the compiler can prove to be LDS (the run-time
+    // LDS-or-blob choice made every weight read a FLAT load, which also waits on vmcnt)
+    if (kLdsW && !kStaged<NT> && a.reg.len > 0) {
+      if (live) edge_hop_core<NT, ACT, XS>(r, a, c, (const float*)smem, wf, &slab[w][0][0], j, lane, g, res);
+    } else if (live) {
+      edge_hop_core<NT, ACT, XS>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
+    }
     if (split) __syncthreads();  // every wave: the epilogue operands have landed
     if (live) edge_hop_finish<NT, ACT, LST>(res, r, a, c, lane, g);
   } else {
@@ -324,14 +338,20 @@ void k_edge_hop(EdgeHopArgs a) {
       __syncthreads();
       Wm = smem;
     }
-    for (; tile < a.ntiles; tile += stride) {
-      const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
-      EdgeHopRows<NT> q;
-      edge_hop_load<NT, LST>(q, a, tile, jj, gg);
-      f32x4 res[NT];
-      edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, Wm, wf, &slab[w][0][0], jj, ln, gg, res);
-      edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
-    }
+    auto walk = [&](const float* Wl) __attribute__((always_inline)) {
+      for (; tile < a.ntiles; tile += stride) {
+        const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
+        EdgeHopRows<NT> q;
+        edge_hop_load<NT, LST>(q, a, tile, jj, gg);
+        f32x4 res[NT];
+        edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, Wl, wf, &slab[w][0][0], jj, ln, gg, res);
+        edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
+      }
+    };
+    if (kLdsW && !kStaged<NT> && a.reg.len > 0)
+      walk((const float*)smem);  // F = 64: provably LDS (see above)
+    else
+      walk(Wm);
   }
   MSW_MARK(c, 9);
 }
@@ -355,57 +375,67 @@ void k_edge_mlp(EdgeHopArgs a) {
   const int w = wave_id();
   const int stride = gridDim.x * kMlpWaves;
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
-  const float* Wm = a.c.W;
+  // the MLP operands through a pointer the compiler can prove to be LDS (a run-time choice
+  // between LDS and the blob made every weight read a FLAT load, which also waits on vmcnt)
+  auto run = [&](const float* Wm) __attribute__((always_inline)) {
+    const int hs = 16 * a.h1t;
+    const float* z = a.c.zrow;
+    const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+    for (int ch = blockIdx.x * kMlpWaves + w; ch < a.nchunks; ch += stride) {
+      const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+      const int4 e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+      const bool ev = e.z >= 0;
+      const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
+      const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
+      const float* Pb = a.Pe && ev ? a.Pe + (size_t)e.z * hs : z;
+      f32x4 H[T2];
+#pragma unroll
+      for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
+        const int off = 16 * t + 4 * g;
+        const bool on = t < a.h1t;
+        const f32x4 u = ld4((on ? Ub : z) + off);
+        const f32x4 v = ld4((on ? Vb : z) + off);
+        const f32x4 pe = ld4((on ? Pb : z) + off);
+        const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
+        H[t] = on ? (u + v) + p : zero4();
+      }
+      act_tiles<ACT, T2>(H, a.act1, a.slope1);
+      f32x4 sv[NT];
+      if (a.rest.n > 0) {
+        run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) sv[t] = H[t];
+      }
+      if (a.normalize) {
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+        const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x4 q = sv[t] / nrm;
+          q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+          q.y = (q.y == q.y) ? q.y : 0.f;
+          q.z = (q.z == q.z) ? q.z : 0.f;
+          q.w = (q.w == q.w) ? q.w : 0.f;
+          sv[t] = q;
+        }
+      }
+      if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+    }
+  };
   if (a.reg.len > 0) {
     stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
-    Wm = smem;
   }
-  const int hs = 16 * a.h1t;
-  const float* z = a.c.zrow;
-  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
-  for (int ch = blockIdx.x * kMlpWaves + w; ch < a.nchunks; ch += stride) {
-    const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
-    const int4 e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
-    const bool ev = e.z >= 0;
-    const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
-    const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
-    const float* Pb = a.Pe && ev ? a.Pe + (size_t)e.z * hs : z;
-    f32x4 H[T2];
-#pragma unroll
-    for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
-      const int off = 16 * t + 4 * g;
-      const bool on = t < a.h1t;
-      const f32x4 u = ld4((on ? Ub : z) + off);
-      const f32x4 v = ld4((on ? Vb : z) + off);
-      const f32x4 pe = ld4((on ? Pb : z) + off);
-      const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
-      H[t] = on ? (u + v) + p : zero4();
-    }
-    act_tiles<ACT, T2>(H, a.act1, a.slope1);
-    f32x4 sv[NT];
-    if (a.rest.n > 0) {
-      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
-    } else {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) sv[t] = H[t];
-    }
-    if (a.normalize) {
-      float ss = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-      const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 q = sv[t] / nrm;
-        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-        q.y = (q.y == q.y) ? q.y : 0.f;
-        q.z = (q.z == q.z) ? q.z : 0.f;
-        q.w = (q.w == q.w) ? q.w : 0.f;
-        sv[t] = q;
-      }
-    }
-    if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  if constexpr (kLdsW) {
+    if (a.reg.len > 0)
+      run(smem);
+    else
+      run(a.c.W);
+  } else {
+    run(a.reg.len > 0 ? (const float*)smem : a.c.W);
   }
 }
 
@@ -452,45 +482,54 @@ void k_edge_mlp_pipe(EdgeHopArgs a) {
   int ch = blockIdx.x * kMlpPipeWaves + w;
   MlpFetch<NT> f;
   if (ch < a.nchunks) mlp_fetch<NT>(f, a, ch, j, g);  // in flight during the weight staging
-  const float* Wm = a.c.W;
+  // the MLP operands through a pointer the compiler can prove to be LDS (see k_edge_mlp)
+  auto run = [&](const float* Wm) __attribute__((always_inline)) {
+    const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+    for (; ch < a.nchunks; ch += stride) {
+      f32x4 H[T2];
+#pragma unroll
+      for (int t = 0; t < T2; ++t) {
+        const f32x4 p = a.Pe ? f.p[t] : ld4(Wm + b1 + 16 * t + 4 * g);
+        H[t] = t < a.h1t ? (f.u[t] + f.v[t]) + p : zero4();
+      }
+      const int4 e = f.e;
+      if (ch + stride < a.nchunks) mlp_fetch<NT>(f, a, ch + stride, j, g);
+      act_tiles<ACT, T2>(H, a.act1, a.slope1);
+      f32x4 sv[NT];
+      if (a.rest.n > 0) {
+        run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) sv[t] = H[t];
+      }
+      if (a.normalize) {
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+        const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x4 q = sv[t] / nrm;
+          q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+          q.y = (q.y == q.y) ? q.y : 0.f;
+          q.z = (q.z == q.z) ? q.z : 0.f;
+          q.w = (q.w == q.w) ? q.w : 0.f;
+          sv[t] = q;
+        }
+      }
+      if (e.z >= 0) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+    }
+  };
   if (a.reg.len > 0) {
     stage_glds<kMlpPipeWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
-    Wm = smem;
   }
-  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
-  for (; ch < a.nchunks; ch += stride) {
-    f32x4 H[T2];
-#pragma unroll
-    for (int t = 0; t < T2; ++t) {
-      const f32x4 p = a.Pe ? f.p[t] : ld4(Wm + b1 + 16 * t + 4 * g);
-      H[t] = t < a.h1t ? (f.u[t] + f.v[t]) + p : zero4();
-    }
-    const int4 e = f.e;
-    if (ch + stride < a.nchunks) mlp_fetch<NT>(f, a, ch + stride, j, g);
-    act_tiles<ACT, T2>(H, a.act1, a.slope1);
-    f32x4 sv[NT];
-    if (a.rest.n > 0) {
-      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
-    } else {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) sv[t] = H[t];
-    }
-    if (a.normalize) {
-      float ss = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-      const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 q = sv[t] / nrm;
-        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-        q.y = (q.y == q.y) ? q.y : 0.f;
-        q.z = (q.z == q.z) ? q.z : 0.f;
-        q.w = (q.w == q.w) ? q.w : 0.f;
-        sv[t] = q;
-      }
-    }
-    if (e.z >= 0) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  if constexpr (kLdsW) {
+    if (a.reg.len > 0)
+      run(smem);
+    else
+      run(a.c.W);
+  } else {
+    run(a.reg.len > 0 ? (const float*)smem : a.c.W);
   }
 }

@@ -712,9 +712,10 @@ def _built_variants():
 @pytest.mark.parametrize("variant", _built_variants())
 def test_build_variant_matches_default_bitwise(variant):
     """A library build variant (build_engine.py --variant=<name>, loaded with MSW_LIB_VARIANT:
-    workgroup sizes, wave counts -- speed knobs) == the default library bit for bit: a 3-step
-    rollout of the dk15-size mesh with the grid-stride edge hops forced (MSW_EH_LOOP=1, ~4.3 k
-    finest tiles), one child process per library (a process loads one).  Round 4 ran it on the
+    workgroup sizes, wave counts, how the MLP operands are addressed -- speed knobs) == the
+    default library bit for bit: a 3-step rollout of the dk15-size mesh with the grid-stride
+    edge hops forced (MSW_EH_LOOP=1, ~4.3 k finest tiles) and one of zenodo4 at F = 64, one
+    child process per library (a process loads one).  Round 4 ran it on the
     software-pipelined edge hop (ehpipe8, profiles/r04/ab_eh_pipe_hbm1m.txt, rejected).
     Skipped when no variant is built."""
     import json
@@ -723,17 +724,18 @@ def test_build_variant_matches_default_bitwise(variant):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if not os.path.exists(os.path.join(root, "mswe-gnn_amd", "lib", f"libmswegnn_{variant}.so")):
         pytest.skip(f"build variant {variant} not built")
-    res = []
-    for v in ("", variant):
-        env = {k: x for k, x in os.environ.items() if not k.startswith("MSW_")}
-        if v:
-            env["MSW_LIB_VARIANT"] = v
-        r = subprocess.run([sys.executable, os.path.join(root, "tools", "rollout_digest.py"), "--mesh", "dk15",
-                            "--T", "3", "--eh-loop"], capture_output=True, text=True, env=env, timeout=240)
-        assert r.returncode == 0, r.stderr[-3000:]
-        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    print(res)
-    assert res[0]["sha256"] == res[1]["sha256"], res
+    for args in (["--mesh", "dk15", "--T", "3", "--eh-loop"], ["--mesh", "zenodo4", "--T", "3", "--hid", "64"]):
+        res = []
+        for v in ("", variant):
+            env = {k: x for k, x in os.environ.items() if not k.startswith("MSW_")}
+            if v:
+                env["MSW_LIB_VARIANT"] = v
+            r = subprocess.run([sys.executable, os.path.join(root, "tools", "rollout_digest.py")] + args,
+                               capture_output=True, text=True, env=env, timeout=240)
+            assert r.returncode == 0, r.stderr[-3000:]
+            res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+        print(res)
+        assert res[0]["sha256"] == res[1]["sha256"], res
 
 
 @pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct"])

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--mesh", default="dk15")
     ap.add_argument("--T", type=int, default=3)
     ap.add_argument("--eh-loop", action="store_true", help="force the grid-stride edge hops (MSW_EH_LOOP=1)")
+    ap.add_argument("--hid", type=int, default=32, help="hidden width F (32: K4_F32 weights; else seeded init)")
     a = ap.parse_args()
     if a.eh_loop:
         os.environ["MSW_EH_LOOP"] = "1"
@@ -32,14 +33,17 @@ def main():
     dev = torch.device("cuda:0")
     g = wet_state(make_multiscale_mesh(**mesh_config(a.mesh), T=a.T), seed=4).to(dev)
     S = mesh_config(a.mesh)["num_scales"]
-    m = build_msgnn(S, 32, 4, state=weights("K4_F32" if S == 4 else "msgnn3_F32_seed666")).to(dev)
+    if a.hid == 32:
+        m = build_msgnn(S, 32, 4, state=weights("K4_F32" if S == 4 else "msgnn3_F32_seed666")).to(dev)
+    else:
+        m = build_msgnn(S, a.hid, 4).to(dev)
     plan = EnginePlan(m, g, dev)
     out = plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, a.T)
     torch.cuda.synchronize()
     y = out.detach().cpu().contiguous()
     st = plan.stats() if hasattr(plan, "stats") else {}
     plan.close()
-    print(json.dumps({"mesh": a.mesh, "T": a.T, "variant": os.environ.get("MSW_LIB_VARIANT", ""),
+    print(json.dumps({"mesh": a.mesh, "T": a.T, "hid": a.hid, "variant": os.environ.get("MSW_LIB_VARIANT", ""),
                       "eh_loop": a.eh_loop, "sha256": hashlib.sha256(y.numpy().tobytes()).hexdigest(),
                       "max_abs": float(y.abs().max()), "kernels_per_step": st.get("kernels_per_step")}))
 
