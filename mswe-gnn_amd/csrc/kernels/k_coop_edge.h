@@ -673,7 +673,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
       store_row<NT>(a.out + L.n * F, res, NT, g);
     }
   };
-  if constexpr (kLdsW) {
+  // (four ranks per tile only: the two-rank kernels' register count grew past two workgroups
+  // per CU with it, 176 -> 256 VGPRs, and the finest unpooling lost its one-round grid)
+  if constexpr (kLdsW && P == 4) {
     if (a.reg.len > 0 && !a.wdirect)
       rest((const float*)smem);
     else

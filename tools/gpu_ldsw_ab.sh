@@ -14,7 +14,7 @@ rc=$?; [ $rc -ne 0 ] && { echo "tests rc=$rc" >> $OUT/steps.log; exit 3; }
 export AB_KEEP=1
 : > gpurun_out/ab.log
 A="--no-cpu-baseline --no-roofline-large --steps 10 --warmup 3"
-bash tools/ab.sh "" "MSW_LIB_VARIANT=flatw" "" "MSW_LIB_VARIANT=flatw" -- --workload zenodo4_f64 $A || exit 4
+bash tools/ab.sh "" "MSW_MLP_PIPE=0" "MSW_LIB_VARIANT=flatw" "" "MSW_MLP_PIPE=0" "MSW_LIB_VARIANT=flatw" -- --workload zenodo4_f64 $A || exit 4
 bash tools/ab.sh "" "MSW_LIB_VARIANT=flatw" -- $A || exit 5
 cp gpurun_out/ab.log $OUT/ab_ldsw.txt
 rm -rf $OUT/prof
