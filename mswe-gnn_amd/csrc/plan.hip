@@ -272,7 +272,7 @@ struct Knobs {
   int coop2_f64 = 1;        // MSW_COOP2_F64       F = 64 two-wave edge hops: 0 off, 2 also for four
   int enc_coop = -1;        // MSW_ENC_COOP        cooperative encoder: -1 size rule, 0 / 1 force
   int enc_coop_p = 0;       // MSW_ENC_COOP_P      F = 64 cooperative encoder on 2 waves per tile
-  int mlp_pipe = -1;        // MSW_MLP_PIPE        pipelined split edge MLP: -1 = F = 64
+  int mlp_pipe = 0;         // MSW_MLP_PIPE        pipelined split edge MLP (1)
   int eh_loop = 0;          // MSW_EH_LOOP         grid-stride fused edge hops at any size
   int hop_split = -1;       // MSW_HOP_SPLIT       feature-split middle hops: -1 = F = 64 rule
   int pool_wide = 1;        // MSW_POOL_WIDE       2F / 16 waves per pooling tile
@@ -999,10 +999,12 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     }
     case L_EDGE_MLP: {
-      // one wave per SIMD walking ~2 chunks, the next chunk's gathers in flight under the
-      // current chunk's MLP (k_edge_mlp_pipe; zenodo4_f64: 27.8 -> 27.0 us per launch,
-      // +0.4 %; MSW_MLP_PIPE=0: k_edge_mlp, two waves per SIMD, one chunk each)
-      L.eh.pipe = P->kn.mlp_pipe >= 0 ? P->kn.mlp_pipe != 0 : P->NT == 4;
+      // k_edge_mlp: two waves per SIMD, one chunk each.  (MSW_MLP_PIPE=1: k_edge_mlp_pipe, one
+      // wave per SIMD walking ~2 chunks, the next chunk's gathers in flight under the current
+      // chunk's MLP -- +0.4 % in round 3 while both read their operands through FLAT loads;
+      // with LDS-typed operands (round 4) it spills and the two-wave kernel is ahead:
+      // zenodo4_f64 27.76 / 27.91 -> 28.08 / 28.09 M, profiles/r04/ab_f64_lds_operands.txt)
+      L.eh.pipe = P->kn.mlp_pipe > 0;
       L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
     }
