@@ -814,3 +814,23 @@ def test_roofline_roles_match_kernel_kinds(tmp_path):
     assert roles["hop"]["kernel"].startswith("k_hop<") and roles["edge_hop"]["kernel"].startswith("k_edge_hop<2, 1, false")
     assert roles["hop_large"]["kernel"] == "k_hop_rows<2>" and abs(roles["hop_large"]["avg_duration_us"] - 144) < 1e-9
     assert roles["edge_hop_large"]["kernel"].startswith("k_edge_hop<2, 1, true")
+
+
+def test_step_breakdown_takes_the_rollout_period(tmp_path):
+    """tools/step_breakdown.py finds the rollout step as the most common distance between
+    encoder launches, not the rollout prologue's shorter one (round-4 fix: a 13-launch
+    prologue was reported as the step)."""
+    import subprocess
+    rows = ["k_encode<2,1,true>"] + [f"k_rowmlp<{i}>" for i in range(12)]  # prologue: 13 launches
+    step = ["k_encode<2,1,true>"] + [f"k_hop<{i}>" for i in range(29)]       # steps: 30 launches
+    seq = rows + step * 5 + ["k_encode<2,1,true>"]
+    path = tmp_path / "trace.csv"
+    with open(path, "w") as f:
+        f.write("Kernel_Name,Grid_Size_X,Workgroup_Size_X,Start_Timestamp,End_Timestamp\n")
+        t = 0
+        for n in seq:
+            f.write(f"\"void msw::{n}(msw::Args)\",256,64,{t},{t + 4000}\n")
+            t += 4500
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "step_breakdown.py"), str(path)],
+                         capture_output=True, text=True, check=True).stdout
+    assert out.splitlines()[0].endswith("steps of 30 launches"), out[:200]
