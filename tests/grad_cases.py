@@ -103,6 +103,30 @@ def training_step_case(dev, sname, R, engine="auto", dtype=torch.float32, model=
     return out, fx
 
 
+def f64_training_step_case(dev, R=4, engine="auto"):
+    """config.yaml's default width F = 64 (mlp_layers 3, K 4): the reference's training_step
+    on the two-graph batch from the seeded initialisation (seed 666), whose state dict must
+    match the reference's bit for bit (fixture digest) -> (loss, gradients)."""
+    import hashlib
+    fx = golden("fx_grad_train_F64")
+    names = manifest()["fx_grad_train_F64_sets"]["b2"]
+    m = build_msgnn(4, 64, 4)
+    h = hashlib.sha256()
+    for v in m.state_dict().values():
+        h.update(v.detach().float().contiguous().numpy().tobytes())
+    assert np.frombuffer(h.digest(), dtype=np.uint8).tolist() == fx["sd_digest"].tolist(), \
+        "seeded F = 64 init differs from the reference's"
+    m = m.to(dev).train()
+    m.engine = engine
+    m.zero_grad(set_to_none=True)
+    temp = training_batch("b2__", names, 5, fx, dev)
+    loss = loss_ref.training_step(m, temp, R)
+    loss.backward()
+    out = {"loss": loss.detach()}
+    out.update({"g__" + n: p.grad for n, p in m.named_parameters() if p.grad is not None})
+    return out, fx
+
+
 def gnn_training_step_case(dev, R, engine="auto"):
     """training_step of the 1-scale GNN (config 1 model) on a batch of two graphs."""
     fx = golden("fx_grad_train_gnn")

@@ -319,6 +319,24 @@ def test_hip_training_step_vs_reference_fixture(cuda, sname, R):
           f"fp64 rule for {rule64}")
 
 
+def test_hip_f64_training_step_vs_reference_fixture(cuda):
+    """config.yaml's default width F = 64 (mlp_layers 3, K 4) on the HIP training kernels: the
+    reference's training_step over 4 rollout steps on the two-graph batch from its seeded
+    initialisation -- loss and every parameter gradient against the reference's (the same bar
+    as the F = 32 cases, grad_cases.check, the drop-in's torch path on this GPU as the extra
+    fp32 yardstick)."""
+    import grad_cases as gc
+    from mswegnn import autograd as ag
+    calls = ag.MLP_CALLS[0], ag.SWEGNN_CALLS[0], ag.POOL_CALLS[0]
+    ours, fx = gc.f64_training_step_case(cuda)
+    assert ag.MLP_CALLS[0] > calls[0] and ag.SWEGNN_CALLS[0] > calls[1] and ag.POOL_CALLS[0] > calls[2]
+    yard, _ = gc.f64_training_step_case(cuda, engine="torch")
+    pre = "b2_R4__"
+    worst, rule64 = gc.check(ours, fx, pre, TOL, "b2_R4_fp64__", yard=yard)
+    print(f"HIP F=64 training_step R=4: loss {float(ours['loss']):.7e} (reference {float(fx[pre + 'loss']):.7e}), "
+          f"worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; rules past 1e-4: {rule64}")
+
+
 @pytest.mark.parametrize("R", [1, 2])
 def test_hip_gnn_training_step_vs_reference_fixture(cuda, R):
     import grad_cases as gc

@@ -63,6 +63,18 @@ def test_torch_path_trains_under_autocast():
         assert g <= bound, (dt, g)
 
 
+def test_f64_training_step_gradients_vs_reference():
+    """config.yaml's default width F = 64: the reference's training_step over 4 rollout steps
+    on the two-graph batch from its seeded initialisation (the drop-in's seeded init is the same
+    state dict bit for bit): loss and every parameter gradient."""
+    ours, fx = gc.f64_training_step_case(CPU)
+    pre = "b2_R4__"
+    assert abs(float(ours["loss"]) - float(fx[pre + "loss"])) <= 1e-6 * abs(float(fx[pre + "loss"]))
+    worst, rule64 = gc.check(ours, fx, pre, TOL, "b2_R4_fp64__")
+    print(f"F=64 training_step R=4: worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; "
+          f"rules past 1e-5: {rule64}")
+
+
 @pytest.mark.parametrize("R", [1, 2])
 def test_gnn_training_step_gradients_vs_reference(R):
     ours, fx = gc.gnn_training_step_case(CPU, R)
