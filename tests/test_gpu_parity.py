@@ -51,6 +51,25 @@ def test_single_step_vs_reference(cuda, ck, K, F):
     assert rel_err(y.cpu(), fx["y"]) <= REL_TOL, rel_err(y.cpu(), fx["y"])
 
 
+def test_f64_default_width_vs_reference(cuda):
+    """config.yaml's default width F = 64 on the HIP engine against the REFERENCE's own outputs
+    (oracle/gen_golden_f64.py: seeded init, no shipped F = 64 checkpoint): single step on the
+    wet tiny mesh, the 48-step dry-start rollout and the 8-step wet-start rollout of the small
+    mesh, 1e-4 relative per step."""
+    m = _hip(build_msgnn(4, 64, 4), cuda)
+    fx = golden("fx_tiny_F64_step")
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=48), seed=1).to(cuda)
+    with torch.no_grad():
+        y = m(g)
+    assert rel_err(y.cpu(), fx["y"]) <= REL_TOL, rel_err(y.cpu(), fx["y"])
+    for name, g in (("fx_small_F64_rollout48", make_multiscale_mesh(**mesh_config("small"), T=48)),
+                    ("fx_small_F64_wet_rollout8", wet_state(make_multiscale_mesh(**mesh_config("small"), T=8), seed=4))):
+        r = m.rollout(g.to(cuda)).cpu()
+        err = per_step_rel(r, torch.from_numpy(golden(name)["rollout"]))
+        print(f"{name}: per-step rel {err:.2e}")
+        assert err <= REL_TOL, (name, err)
+
+
 def test_single_step_msgnn3_and_gnn(cuda):
     fx = golden("fx_small3_msgnn3_wet")
     g = wet_state(make_multiscale_mesh(**mesh_config("small3"), T=6), seed=3).to(cuda)

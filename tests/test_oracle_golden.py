@@ -77,6 +77,29 @@ def test_oracle_rollout48(ck):
     assert_pinned(r, torch.from_numpy(fx["rollout"]))
 
 
+def test_oracle_f64_default_width():
+    """config.yaml's default width F = 64 (mlp_layers 3, K 4; no shipped checkpoint: the
+    reference's seeded initialisation, which the drop-in's seeded init reproduces): the oracle
+    against the reference's single step, 48-step dry-start rollout and 8-step wet-start rollout
+    (oracle/gen_golden_f64.py)."""
+    from conftest import build_msgnn, state_dict_of
+    cfg = manifest()["fx_F64_cfg"]
+    cfg = {k: v for k, v in cfg.items() if k != "weights"}
+    P = state_dict_of(build_msgnn(4, 64, 4))
+    fx = golden("fx_tiny_F64_step")
+    g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=48), seed=1)
+    assert np.array_equal(_digest(g), fx["digest"])
+    assert_pinned(orc.forward(P, cfg, g), torch.from_numpy(fx["y"]))
+    fx = golden("fx_small_F64_rollout48")
+    g = make_multiscale_mesh(**mesh_config("small"), T=48)
+    assert np.array_equal(_digest(g), fx["digest"])
+    assert_pinned(orc.rollout(P, cfg, g), torch.from_numpy(fx["rollout"]))
+    fx = golden("fx_small_F64_wet_rollout8")
+    g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=8), seed=4)
+    assert np.array_equal(_digest(g), fx["digest"])
+    assert_pinned(orc.rollout(P, cfg, g), torch.from_numpy(fx["rollout"]))
+
+
 def test_oracle_msgnn3_wet():
     fx = golden("fx_small3_msgnn3_wet")
     cfg = manifest()["weights_msgnn3_F32_seed666_cfg"]
