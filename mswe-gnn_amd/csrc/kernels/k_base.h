@@ -203,6 +203,9 @@ __device__ __forceinline__ void side_proj(const f32x4 (&in)[TIN], int h1t, const
 // with the tile's gathers at kernel start instead of after the hop (one latency less on the
 // chain): x_s rows for the projections, the decoder's dynamic state columns, the step.
 constexpr int kMaxDyn = 16;
+#ifndef MSW_BC_HOIST
+#define MSW_BC_HOIST 0
+#endif
 template <int NT>
 struct EpiPre {
   f32x4 xs[NT];
