@@ -63,7 +63,7 @@ def build(force=False, verbose=True, variant=""):
              "e0w12": ["-DMSW_EDGE_WAVES0=12"], "hw4": ["-DMSW_HOP_WAVES=4"],
              "hw10": ["-DMSW_HOP_WAVES=10"], "hw16": ["-DMSW_HOP_WAVES=16"],
              "rdc2": ["-DMSW_ROW_DC=2"], "rdc4": ["-DMSW_ROW_DC=4"],
-             "flatw": ["-DMSW_FLAT_W=1"], "bchoist": ["-DMSW_BC_HOIST=1"]}.get(variant, [])
+             "flatw": ["-DMSW_FLAT_W=1"], "nobchoist": ["-DMSW_BC_HOIST=0"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     out = lib_path(variant)

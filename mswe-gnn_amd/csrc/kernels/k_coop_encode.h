@@ -87,12 +87,12 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
     dyn[q] = f < a.c.dyn ? xr[nstat + f] : 0.f;
   }
   wlv = xr[nstat - 1] + xr[a.c.nnf - 2];
-#if MSW_BC_HOIST
-  if (DEC && dstep >= 0) {  // variant bchoist (see k_encode)
-    pre.step = dstep;
-    bc_prefetch<NT>(pre, a.dec, c);
+  if constexpr (kBcHoist<NT>) {  // see k_base.h kBcHoist
+    if (DEC && dstep >= 0) {
+      pre.step = dstep;
+      bc_prefetch<NT>(pre, a.dec, c);
+    }
   }
-#endif
   MSW_MARK(c, 1);
   if constexpr (kStaged<NT>) {
     stage_glds<WV>(smem, a.c.W, a.sreg[s], 0, a.sreg[s].len);
@@ -103,10 +103,10 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
   int xc = 0;
   if (DEC && dstep >= 0) {
 #pragma clang fp contract(off)
-#if !MSW_BC_HOIST
-    pre.step = dstep;
-    bc_prefetch<NT>(pre, a.dec, c);
-#endif
+    if constexpr (!kBcHoist<NT>) {
+      pre.step = dstep;
+      bc_prefetch<NT>(pre, a.dec, c);
+    }
     float nd[kMaxDyn];
     {
       f32x4 x0[NT], o[1];

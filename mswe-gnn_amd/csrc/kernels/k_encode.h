@@ -57,13 +57,12 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
       dyn[r] = f < a.c.dyn ? xr[nstat + f] : 0.f;
     }
     wlv = xr[nstat - 1] + xr[a.c.nnf - 2];  // water level = bed elevation + depth
-#if MSW_BC_HOIST
-    // variant bchoist: the next step's BC values issued before the weight staging
-    if (DEC && dstep >= 0) {
-      pre.step = dstep;
-      bc_prefetch<NT>(pre, a.dec, c);
+    if constexpr (kBcHoist<NT>) {  // the next step's BC values before the weight staging
+      if (DEC && dstep >= 0) {
+        pre.step = dstep;
+        bc_prefetch<NT>(pre, a.dec, c);
+      }
     }
-#endif
     MSW_MARK(c, 1);
     if constexpr (kStaged<NT>) {
       if (s != staged) {  // uniform across the workgroup: every wave walks the same chunks
@@ -77,10 +76,10 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     // prove to be LDS across the loop: it emitted flat loads, which wait on vmcnt too)
     const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
     if (DEC && dstep >= 0) {  // decode the previous step; the encoders read the updated state
-#if !MSW_BC_HOIST
-      pre.step = dstep;
-      bc_prefetch<NT>(pre, a.dec, c);
-#endif
+      if constexpr (!kBcHoist<NT>) {
+        pre.step = dstep;
+        bc_prefetch<NT>(pre, a.dec, c);
+      }
       float nd[kMaxDyn];
       decode_state<NT, ACT>(xu, a.dec, c, Wl, pre, n, valid, lane, g, nd);
 #pragma unroll
