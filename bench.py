@@ -496,6 +496,26 @@ def _built_from_sources():
         return None
 
 
+def self_launch(n, backend):
+    """`bench.py --gpus N` run without a launcher: N ranks under torch.distributed.run on this
+    node (127.0.0.1, a free port), the same arguments; rank 0 prints the line.  With RCCL the
+    node must have N GPUs (counted without initialising one); gloo rehearsals may share them."""
+    import socket
+    import subprocess
+    ngpu = torch.cuda.device_count()
+    if backend == "nccl" and ngpu < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs for one RCCL rank each; this node has {ngpu}",
+              file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -529,13 +549,25 @@ def main():
                          "a section that does not fit is recorded as skipped")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
     # one rank per GPU; MSW_DIST_BACKEND=gloo + more ranks than GPUs rehearses the N > 1 path
     # on a one-GPU box (ranks share the device; RCCL refuses two ranks on one device)
     backend = os.environ.get("MSW_DIST_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start the N ranks ourselves, before anything
+        # here touches a GPU (no exec: the ranks are children, their exit code is ours)
+        sys.exit(self_launch(args.gpus, backend))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if not torch.cuda.is_available():
+        print(f"bench.py rank {rank}/{world}: no GPU visible (the HIP engine needs an MI355X)",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+    dist = None
     gpu = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     cpu_group = None
     if world > 1:

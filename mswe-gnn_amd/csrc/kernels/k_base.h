@@ -206,13 +206,9 @@ constexpr int kMaxDyn = 16;
 // Rollout-mode encoder: the next step's BC values issued before the weight staging (their
 // round trip then overlaps the staging instead of the decoder MLP; zenodo4 +0.65 %,
 // profiles/r04/ab_bc_hoist.txt) where there is a staging to overlap (F <= 32); F = 64 reads
-// its operands from the blob and measured neutral.  MSW_BC_HOIST=0 / 1 forces it off / on
-// (build variants, bit-identical).
-#ifndef MSW_BC_HOIST
-#define MSW_BC_HOIST -1
-#endif
+// its operands from the blob and measured neutral.
 template <int NT>
-constexpr bool kBcHoist = MSW_BC_HOIST < 0 ? NT <= 2 : MSW_BC_HOIST != 0;
+constexpr bool kBcHoist = NT <= 2;
 template <int NT>
 struct EpiPre {
   f32x4 xs[NT];

@@ -675,7 +675,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   };
   // (four ranks per tile only: the two-rank kernels' register count grew past two workgroups
   // per CU with it, 176 -> 256 VGPRs, and the finest unpooling lost its one-round grid)
-  if constexpr (kLdsW && P == 4) {
+  if constexpr (P == 4) {
     if (a.reg.len > 0 && !a.wdirect)
       rest((const float*)smem);
     else

@@ -3,14 +3,6 @@
 // comment for the register layout and conventions.
 #pragma once
 
-// F = 64 MLP operands in LDS read through a pointer the compiler can prove to be LDS
-// (ds_read); MSW_FLAT_W=1 builds the round-3 form, one pointer that is LDS or the blob at run
-// time (FLAT loads, which also wait on vmcnt) -- the A/B build variant
-#ifndef MSW_FLAT_W
-#define MSW_FLAT_W 0
-#endif
-constexpr bool kLdsW = !MSW_FLAT_W;
-
 // ---------------------------------------------------------------------------- message passing
 // One wave = one edge tile (whole destination neighbourhoods, <= 16 edges, <= 16 nodes).
 // Lane j is edge slot j in the edge phase and destination j in the node phase; per-node
@@ -319,7 +311,7 @@ void k_edge_hop(EdgeHopArgs a) {
     f32x4 res[NT];
     // F = 64: the MLP operands through a pointer the compiler can prove to be LDS (the run-time
     // LDS-or-blob choice made every weight read a FLAT load, which also waits on vmcnt)
-    if (kLdsW && !kStaged<NT> && a.reg.len > 0) {
+    if (!kStaged<NT> && a.reg.len > 0) {
       if (live) edge_hop_core<NT, ACT, XS>(r, a, c, (const float*)smem, wf, &slab[w][0][0], j, lane, g, res);
     } else if (live) {
       edge_hop_core<NT, ACT, XS>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
@@ -348,7 +340,7 @@ void k_edge_hop(EdgeHopArgs a) {
         edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
       }
     };
-    if (kLdsW && !kStaged<NT> && a.reg.len > 0)
+    if (!kStaged<NT> && a.reg.len > 0)
       walk((const float*)smem);  // F = 64: provably LDS (see above)
     else
       walk(Wm);
@@ -429,14 +421,10 @@ void k_edge_mlp(EdgeHopArgs a) {
     stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
   }
-  if constexpr (kLdsW) {
-    if (a.reg.len > 0)
-      run(smem);
-    else
-      run(a.c.W);
-  } else {
-    run(a.reg.len > 0 ? (const float*)smem : a.c.W);
-  }
+  if (a.reg.len > 0)
+    run(smem);
+  else
+    run(a.c.W);
 }
 
 // k_edge_mlp software-pipelined (F = 64, MSW_MLP_PIPE): one wave per SIMD, each wave walks
@@ -524,12 +512,8 @@ void k_edge_mlp_pipe(EdgeHopArgs a) {
     stage_glds<kMlpPipeWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
   }
-  if constexpr (kLdsW) {
-    if (a.reg.len > 0)
-      run(smem);
-    else
-      run(a.c.W);
-  } else {
-    run(a.reg.len > 0 ? (const float*)smem : a.c.W);
-  }
+  if (a.reg.len > 0)
+    run(smem);
+  else
+    run(a.c.W);
 }
