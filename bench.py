@@ -869,6 +869,7 @@ def main():
             "all_node_steps_per_s": value * desc.get("batch_nodes", desc["all_nodes"]) / fine_rank,
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "engine": {"kernels_per_step": st["kernels_per_step"], "graph_captured": st["graph_captured"],
+                       "dma_edge_hops": st["dma_edge_hops"],
                        "device_bytes": st["device_bytes"],
                        "device_bytes_note": "plan-owned: graph tables, weights, per-node buffers and the "
                                             "edge-encoder inputs / outputs kept for the per-rollout "

@@ -142,6 +142,8 @@ typedef struct {
   int64_t rollout_steps;     /* rollout steps executed through the HIP path so far */
   int64_t device_bytes;      /* device memory owned by the plan */
   int32_t graph_captured;    /* a hipGraph of one rollout step is instantiated */
+  int32_t dma_edge_hops;     /* launches of a rollout step on the LDS-DMA pipelined grid-stride
+                                edge MLP + hop (k_edge_hop_dma, MSW_EH_DMA) */
 } msw_plan_stats;
 
 /* Halo exchange of one rank of a single mesh split over several ranks (SURVEY §8 f2,

@@ -192,6 +192,9 @@ struct EdgeHopArgs {
                                    // &RolloutIO::step, advanced once (workgroup 0, lane 0)
   const EdgeChunk* chunks; int nchunks;  // k_edge_mlp: dense 16-edge chunks [nchunks][16]
   PoolFuse pool;                   // mean pooling + projection fused in (k_edge_coop only)
+  int dma;                         // grid-stride variant with the next tile's rows LDS-DMA'd
+                                   // during the current tile's MLP (k_edge_hop_dma)
+  int dma_off;                     // k_edge_hop_dma: floats of LDS before the per-wave regions
 };
 
 // Hops 2..K over the same edge tiles as the fused first hop.
@@ -254,6 +257,16 @@ struct EpiArgs {
   const float* xs;
   float* out;              // the layer's output rows (may be `in`, or null)
   Epilogue epi;
+};
+
+// Forward mode (msw_forward), decoder deferred out of the last hops: one row-local launch
+// after the schedule decodes every node from the stored last-layer rows (gnn.py:335-348,
+// models.py:50-91), as the rollout's encoder does for the previous step.
+struct DecodeArgs {
+  Common c;                // c.W: the blob (the decoder operands stay blob offsets)
+  int Npad;                // rows [0, Npad), 16 per wave; padding rows (perm -1) skipped
+  const float* in;         // [Npad][F] the last layer's output rows (x_up / the GNN's last layer)
+  DecDesc dec;             // forward variant: X = the forward input (graph rows), y = output
 };
 
 struct InitArgs {
@@ -321,5 +334,6 @@ template <int NT> hipError_t launch_hop(const HopArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_pool(const PoolArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_epi(const EpiArgs& a, hipStream_t st);
 template <int NT> hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st);
+template <int NT> hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 
 }  // namespace msw

@@ -120,3 +120,29 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
   }
   MSW_MARK(c, 9);
 }
+
+// ---------------------------------------------------------------------------- forward decode
+// Forward mode with the deferred decoder (plan.hip sched_step): decode_rows -- the last hops'
+// forward-mode epilogue, operation for operation -- on 16 stored last-layer rows per wave,
+// after the whole schedule instead of inside four latency-bound last hops.  The decoder
+// operands are read from the blob (a few KB, L2-resident): no staging barrier.
+template <int NT, int ACT>
+__global__ __launch_bounds__(kBlock) void k_decode_fwd(DecodeArgs a) {
+  constexpr int F = 16 * NT;
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int n = wave_row0() + j;
+  if (wave_row0() >= a.Npad) return;  // whole wave past the rows
+  const bool valid = n < a.Npad;
+  const int nn = valid ? n : 0;
+  EpiPre<NT> pre;
+  f32x4 xu[NT];
+  load_row<NT>(xu, a.in + (size_t)nn * F, g);
+  const Common& c = a.c;
+  pre.ext = valid ? c.perm[nn] : -1;
+  pre.step = 0;
+  pre.bc = -1;
+  const float* xr = a.dec.X + (size_t)(pre.ext > 0 ? pre.ext : 0) * c.nnf + (c.nnf - c.dyn);
+#pragma unroll
+  for (int k = 0; k < kMaxDyn; ++k) pre.xd[k] = k < c.dyn ? xr[k] : 0.f;
+  decode_rows<NT, ACT>(xu, a.dec, c, pre, nn, valid, lane, g);
+}

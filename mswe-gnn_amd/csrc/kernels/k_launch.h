@@ -37,6 +37,12 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
+  if constexpr (kStaged<NT>) {  // DMA-pipelined grid-stride edge hop: all of its LDS is dynamic
+    for (const void* f : {(const void*)k_edge_hop_dma<NT, 1>, (const void*)k_edge_hop_dma<NT, -1>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
+  }
   for (const void* f : {(const void*)k_edge_mlp<NT, 1>, (const void*)k_edge_mlp<NT, -1>}) {  // no slab
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
@@ -212,6 +218,15 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   }
   if (a.pool.slots || a.pool.parent) return hipErrorInvalidValue;  // fused into k_edge_coop only
   const bool loop = tile_loop(a);
+  if constexpr (kStaged<NT>) {
+    if (a.dma && loop && !a.last) {  // plan.hip set_grid_cap: the conditions k_edge_hop_dma assumes
+      EdgeHopArgs b = a;
+      b.c.xcd = 0;
+      void* args[] = {&b};
+      const void* f = a.c.prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>;
+      return hipLaunchKernel(f, dim3(a.max_blocks), dim3(64 * kDmaWaves), args, dma_lds_bytes<NT>(a.reg_nf), st);
+    }
+  }
   EdgeHopArgs b = a;
   const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
   if (loop) b.c.xcd = 0;
@@ -330,6 +345,17 @@ hipError_t launch_rowmlp(const RowMlpArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int NT>
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
+  if (a.Npad <= 0) return hipSuccess;
+  const dim3 grid(cdiv(a.Npad, kRowsPerBlock)), block(kBlock);
+  if (a.c.prelu)
+    hipLaunchKernelGGL((k_decode_fwd<NT, 1>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((k_decode_fwd<NT, -1>), grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
 // Workgroups of one launch resident on the whole chip (grid cap of the grid-stride kernels).
 template <int NT, bool LOOP>
 static const void* kernel_of(int kind, int prelu, int last) {
@@ -352,6 +378,9 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
     case 14: return (const void*)k_hop_rows<NT>;
     case 15: return prelu ? (const void*)k_edge_mlp_pipe<NT, 1> : (const void*)k_edge_mlp_pipe<NT, -1>;
+    case 17:
+      if constexpr (kStaged<NT>) return prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>;
+      return nullptr;
     default: return nullptr;
   }
 }
@@ -360,9 +389,12 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
-  const size_t dyn = (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
+  const size_t dyn = kind == 17 ? dma_lds_bytes<NT>((int)(dyn_bytes / 4))
+                     : (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
-  const int block = kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
+  if (dyn > 160 * 1024) return 0;
+  const int block = kind == 17 ? 64 * kDmaWaves
+                    : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
                     : kind == 15 ? 64 * kMlpPipeWaves
                     : kind == 13 ? 64 * 2 * NT
@@ -385,4 +417,5 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   template hipError_t launch_hop<NT>(const HopArgs&, hipStream_t);                \
   template hipError_t launch_pool<NT>(const PoolArgs&, hipStream_t);              \
   template hipError_t launch_epi<NT>(const EpiArgs&, hipStream_t);                \
-  template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);
+  template hipError_t launch_rowmlp<NT>(const RowMlpArgs&, hipStream_t);           \
+  template hipError_t launch_decode<NT>(const DecodeArgs&, hipStream_t);

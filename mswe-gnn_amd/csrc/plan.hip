@@ -221,7 +221,7 @@ static RcclApi& rccl() {
 
 // One kernel launch of a step, arguments fixed at plan time (forward mode patches the
 // input / output pointers per call).
-enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP };
+enum LaunchKind { L_ENCODE, L_EDGE_HOP, L_HOP, L_POOL, L_EXCHANGE, L_EPI, L_EDGE_MLP, L_DECODE };
 
 // Halo exchange before a gathering launch (partitioned meshes, msw_plan_create_part):
 // refresh the halo rows of up to two of the plan's buffers on one scale.
@@ -243,6 +243,7 @@ struct Launch {
     PoolArgs pool;
     ExchangeArgs xch;
     EpiArgs ep;
+    DecodeArgs dec;
   };
   Launch() { memset((void*)this, 0, sizeof(*this)); }
   Common& common() {
@@ -253,6 +254,7 @@ struct Launch {
       case L_HOP: return hop.c;
       case L_EXCHANGE: return xch.c;
       case L_EPI: return ep.c;
+      case L_DECODE: return dec.c;
       default: return pool.c;
     }
   }
@@ -280,6 +282,7 @@ struct Knobs {
   int xcd_max = 1;          // MSW_XCD_MAX         XCD packing of small grids (0 = all eight XCDs)
   int coop_waves = -1;      // MSW_COOP_WAVES      cooperative kernels while P x tiles <= this (-1 default)
   int epi_split_tiles = -1; // MSW_EPI_SPLIT_TILES row-epilogue threshold in edge tiles (-1 default)
+  int eh_dma = 0;           // MSW_EH_DMA          grid-stride edge hops with LDS-DMA prefetch (k_edge_hop_dma)
   int trace_encode = 0;     // MSW_TRACE_ENCODE    diagnostic builds (-DMSW_TRACE): encoder marks only
 };
 inline Knobs knobs_from_env() {
@@ -291,10 +294,10 @@ inline Knobs knobs_from_env() {
       {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_EH_LOOP", &k.eh_loop},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
       {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
-      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
+      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode},
+      {"MSW_EH_DMA", &k.eh_dma}};
   for (const auto& t : tab)
     if (const char* e = getenv(t.name)) *t.v = atoi(e);
-  if (getenv("MSW_TRACE_ENCODE")) k.trace_encode = 1;
   return k;
 }
 
@@ -699,11 +702,14 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
   // meshes whose finest scale has >= kDeferMaxTiles edge tiles the decoder stays in the last
   // hops' row epilogue (config 5: -1.2 % deferred; profiles/r02_v3/ab_defer_decode.txt).
   // MSW_DEFER_DECODE=0/1 overrides.
+  // Forward mode (msw_forward, the reference's own step loop): the decoder leaves the last
+  // hops for one row-local launch after the schedule (k_decode_fwd), by the same size rule.
   constexpr int kDeferMaxTiles = 65536;
-  bool defer = rollout && P->sc[0].ntiles < kDeferMaxTiles;
-  if (P->kn.defer_decode >= 0) defer = rollout && P->kn.defer_decode != 0;
+  bool defer = P->sc[0].ntiles < kDeferMaxTiles;
+  if (P->kn.defer_decode >= 0) defer = P->kn.defer_decode != 0;
+  if (!rollout && !P->xch.empty()) defer = false;  // parts of a split mesh: decoded in their last hops
   ea.dec = dd;
-  ea.dec.on = defer ? 1 : 0;
+  ea.dec.on = defer && rollout ? 1 : 0;
   ea.dec_in = P->model_type == 0 ? P->xup : P->xgnn;
   ea.decode_only = 0;
   q.push_back(LE);
@@ -786,7 +792,20 @@ void sched_step(msw_plan* P, std::vector<Launch>& q, bool rollout) {
       sched_proc(P, q, P->procs[j], P->xgnn, e);
     }
   }
-  if (defer)  // the step counter the next step's encoder reads advances here
+  if (defer && !rollout) {  // forward mode: the deferred decoder, after everything else
+    Launch LD;
+    LD.kind = L_DECODE;
+    LD.scale = 0;
+    DecodeArgs& da = LD.dec;
+    da.c = c;
+    da.c.xcd_max = 0;
+    da.Npad = P->Npad;
+    da.in = ea.dec_in;
+    da.dec = dd;
+    da.dec.on = 1;
+    q.push_back(LD);
+  }
+  if (defer && rollout)  // the step counter the next step's encoder reads advances here
     for (Launch& L : q)
       if (L.kind == L_EDGE_HOP || L.kind == L_EDGE_MLP) {
         L.eh.step_inc = &P->io_d->step;
@@ -929,8 +948,8 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
       a.filt_l = R.put(a.filt_a, P->NT * P->NT * 256);
       a.reg = R.done(split);
       reg = &a.reg;
-    } else if (L.kind == L_EXCHANGE) {
-      continue;  // no LDS weight region
+    } else if (L.kind == L_EXCHANGE || L.kind == L_DECODE) {
+      continue;  // no LDS weight region (the forward decode reads its operands from the blob)
     } else if (L.kind == L_EPI) {
       EpiArgs& a = L.ep;
       RegionBuilder R(P->blob, 0);
@@ -1049,6 +1068,20 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         }
       }
       if ((a.pool.slots || a.pool.parent) && !a.coop) a.coop = 2;  // F = 64 fused: two waves per tile, any grid
+      // grid-stride first hops of K > 1 layers (F <= 32): the next tile's rows LDS-DMA'd during
+      // the current tile's MLP (k_edge_hop_dma) -- its layout assumes an edge term, a 2F-wide
+      // first layer, stored s and out rows, no skip, no epilogue, no fused (un)pooling
+      a.dma = 0;
+      a.dma_off = 0;
+      if (P->kn.eh_dma > 0 && P->NT <= 2 && loop && !a.coop && !a.last && a.Pe && a.h1t == 2 * P->NT &&
+          !a.own_zero && a.s && a.out && !a.skip && !a.pool.slots && !a.pool.parent) {
+        const int nb = resident_of(P->NT, 17, a.c.prelu, 0, (size_t)a.reg_nf * 4, 1);
+        if (nb > 0) {
+          a.dma = 1;
+          a.dma_off = (a.reg_nf + kChunk - 1) / kChunk * kChunk;
+          a.max_blocks = nb;
+        }
+      }
       break;
     }
     case L_HOP:
@@ -1086,6 +1119,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       }
       break;
     case L_EXCHANGE: break;
+    case L_DECODE: break;
     case L_EPI:
       caps(P, L.ep, 6, L.ep.c.prelu, 1, L.ep.reg.len);
       break;
@@ -1136,6 +1170,7 @@ hipError_t launch_one(const Launch& L, hipStream_t st) {
     case L_HOP: return launch_hop<NT>(L.hop, st);
     case L_POOL: return launch_pool<NT>(L.pool, st);
     case L_EPI: return launch_epi<NT>(L.ep, st);
+    case L_DECODE: return launch_decode<NT>(L.dec, st);
     default: return hipErrorInvalidValue;  // exchanges are run by run_schedule / the group driver
   }
 }
@@ -1218,6 +1253,10 @@ int final_decode(msw_plan* P, hipStream_t st) {
 void patch_forward(std::vector<Launch>& q, const float* x, float* y) {
   for (Launch& L : q) {
     if (L.kind == L_ENCODE) L.enc.x = x;
+    if (L.kind == L_DECODE) {
+      L.dec.dec.X = x;
+      L.dec.dec.y = y;
+    }
     Epilogue* e = L.kind == L_EDGE_HOP ? &L.eh.epi : L.kind == L_HOP ? &L.hop.epi
                  : L.kind == L_EPI ? &L.ep.epi : nullptr;
     if (e && e->dec.on) {
@@ -1898,6 +1937,13 @@ int msw_plan_get_stats(const msw_plan* P, msw_plan_stats* s) {
   s->rollout_steps = P->rollout_steps;
   s->device_bytes = P->dev_bytes;
   s->graph_captured = P->step_exec != nullptr || P->multi_exec != nullptr || P->fwd_exec != nullptr;
+  s->dma_edge_hops = 0;
+  for (const Launch& L : P->sched_roll) {
+    const EdgeHopArgs& a = L.eh;
+    if (L.kind == L_EDGE_HOP && a.dma && !a.last && a.fit_blocks > 0 && a.max_blocks > 0 &&
+        (a.ntiles + kWaves - 1) / kWaves > a.fit_blocks)
+      ++s->dma_edge_hops;
+  }
   return MSW_OK;
 }
 

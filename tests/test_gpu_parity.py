@@ -497,6 +497,33 @@ def test_deferred_decoder_matches_fused_decoder(cuda, model, monkeypatch):
     assert torch.equal(outs["0"], outs["1"])
 
 
+@pytest.mark.parametrize("model", ["msgnn_K4_F32", "gnn"])
+def test_forward_deferred_decoder_matches_fused_decoder(cuda, model, monkeypatch):
+    """Forward mode (msw_forward: the reference's own step loop, gnn.py:335-348 per call) runs
+    the decoder as one row-local launch after the schedule (k_decode_fwd) on latency-bound
+    meshes instead of in the four last hops' epilogues (MSW_DEFER_DECODE=0): the same output
+    bit for bit, and the reference's single-step output."""
+    from mswegnn.engine import EnginePlan
+    outs, launches = {}, {}
+    for dv in ("0", "1"):
+        monkeypatch.setenv("MSW_DEFER_DECODE", dv)
+        if model == "gnn":
+            fx = golden("fx_gnn_small_rollout10")
+            g = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=10), seed=2).to(cuda)
+            m = build_gnn(state=weights("gnn_F32_seed42")).to(cuda)
+        else:
+            fx = golden("fx_tiny_K4_F32_step")
+            g = wet_state(make_multiscale_mesh(**mesh_config("tiny"), T=48), seed=1).to(cuda)
+            m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+        plan = EnginePlan(m, g, cuda)
+        outs[dv] = plan.forward(g.x).clone().cpu()
+        outs[dv + "_again"] = plan.forward(g.x).clone().cpu()  # the captured forward graph replayed
+        plan.close()
+        assert rel_err(outs[dv], torch.from_numpy(fx["y"])) <= REL_TOL
+    assert torch.equal(outs["0"], outs["1"])
+    assert torch.equal(outs["1"], outs["1_again"])
+
+
 @pytest.mark.parametrize("act", ["relu", "leakyrelu", "elu", "swish", "sigmoid", "tanh"])
 def test_mlp_activations_vs_oracle(cuda, act):
     """Every make_mlp activation of activation_functions (models/models.py:149-169) other
@@ -718,6 +745,34 @@ def test_grid_stride_edge_hops_match_one_tile_per_wave(cuda, monkeypatch, S, F, 
         plan = EnginePlan(m, g, cuda)
         outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
         plan.close()
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", ["forced_small", "medium_natural"])
+def test_dma_edge_hops_match_grid_stride(cuda, monkeypatch, case):
+    """The LDS-DMA pipelined grid-stride fused edge MLP + hop (k_edge_hop_dma, MSW_EH_DMA=1:
+    the next tile's U / V / Pe and out rows gathered into the wave's LDS region during the
+    current tile's MLP, waits counted by hand) == the grid-stride k_edge_hop bit for bit over a
+    wet rollout: on the small 4-scale mesh with the grid-stride path forced (MSW_EH_LOOP=1, one
+    or two tiles per wave), and on a 115 k-node 3-scale mesh whose finest scale takes the
+    grid-stride path by size (~11 tiles per wave: the prefetch pipeline runs in steady state)."""
+    from mswegnn.engine import EnginePlan
+    T = 3
+    if case == "forced_small":
+        g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=4).to(cuda)
+        m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+        monkeypatch.setenv("MSW_EH_LOOP", "1")
+    else:
+        g = wet_state(make_multiscale_mesh(n_coarse=60, num_scales=3, T=T), seed=5, all_wet=True).to(cuda)
+        m = build_msgnn(3, 32, 4).to(cuda)
+    outs, dma = [], []
+    for v in ("0", "1"):
+        monkeypatch.setenv("MSW_EH_DMA", v)
+        plan = EnginePlan(m, g, cuda)
+        outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
+        dma.append(plan.stats()["dma_edge_hops"])
+        plan.close()
+    assert dma[0] == 0 and dma[1] >= 1, dma
     assert torch.equal(outs[0], outs[1])
 
 

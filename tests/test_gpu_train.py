@@ -211,7 +211,7 @@ def test_batched_training_step_gradients(cuda):
     gradient tensor of ours must be within 1e-4 of it, or -- where the fp32 torch path itself
     is not (cancellation-heavy sums such as a bias-free encoder's weight gradient on a partly
     dry batch) -- within 3x torch fp32's own error; over 2 steps the same rule on the global
-    relative L2 norm (float64 yardstick)."""
+    relative L2 norm (CHANGELOG.md round 3: float64 yardstick)."""
     import copy
     from mswegnn.batch import collate
     from mswegnn.rollout import adapt_batch_training, apply_boundary_condition, use_prediction

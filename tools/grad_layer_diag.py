@@ -29,6 +29,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--R", type=int, default=1)
     ap.add_argument("--all", action="store_true", help="every tensor (default: those where HIP > 1e-5)")
+    ap.add_argument("--hip-calls", default="all",
+                    help="SWEGNN calls (by order in the forward) on the HIP kernels in the recorded run, "
+                         "the others and every make_mlp / pooling on the torch path; 'all' = the HIP path")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     from models.gnn import SWEGNN
@@ -36,8 +39,16 @@ def main():
     calls = []
     orig_fwd = SWEGNN.forward
 
+    hip_calls = None if a.hip_calls == "all" else {int(c) for c in a.hip_calls.split(",") if c}
+
     def recording(self, x_s, x_d, edge_index, edge_attr=None):
-        y = orig_fwd(self, x_s, x_d, edge_index, edge_attr)
+        old = self.train_engine
+        if hip_calls is not None:
+            self.train_engine = "auto" if len(calls) in hip_calls else "torch"
+        try:
+            y = orig_fwd(self, x_s, x_d, edge_index, edge_attr)
+        finally:
+            self.train_engine = old
         rec = {"layer": self, "args": [t.detach().clone() if t is not None else None
                                        for t in (x_s, x_d, edge_index, edge_attr)]}
         calls.append(rec)
@@ -56,11 +67,16 @@ def main():
             y.register_hook(lambda g, rec=rec: rec.__setitem__("dout", g.detach().clone()))
         return y
     mg._mlp_call = mlp_recording
+    from models.gnn import MSGNN
+    orig_te = MSGNN.train_engine
+    if hip_calls is not None:
+        MSGNN.train_engine = "torch"
     try:
         gc.zenodo4_training_step_case(dev, a.R)
     finally:
         SWEGNN.forward = orig_fwd
         mg._mlp_call = orig_mlp
+        MSGNN.train_engine = orig_te
 
     def run(layer, args, dout, engine, dtype, mlp=False):
         lay = copy.deepcopy(layer).to(dtype)
