@@ -41,6 +41,43 @@ _CSR_KEEP = 32
 MLP_CALLS = [0]  # mlp_apply / pool_apply / swegnn_apply calls (tests check that the HIP path ran)
 POOL_CALLS = [0]
 SWEGNN_CALLS = [0]
+# Diagnostics (tests/: the branch-following float64 yardstick).  A list here receives, per HIP
+# training-forward call in call order, the discrete decisions the kernels took: the side of
+# every activation kink (pre-activation > 0) of each MLP layer and, for SWEGNN, the hop
+# predicate out.sum(1) != 0 of every hop (gnn.py:408) -- read back from the saved buffer.
+RECORD = None
+
+
+def _al(n):
+    return (n + 63) // 64 * 64  # csrc/train.hip layout_of / mlp_layout_of: 64-float aligned slots
+
+
+def _swegnn_decisions(d, saved):
+    """The saved buffer of msw_swegnn_train_forward (csrc/train.hip layout_of): X0, pre[l],
+    post[l], s, nrm, outk, agg, nz -> {pre: [E x w(l+1) bool], nz: [K x N bool]}."""
+    E, N, F, K, nl = d.num_edges, d.num_nodes, d.F, d.K, d.n_layers
+    w = [d.width[i] for i in range(nl + 1)]
+    o = _al(E * w[0])
+    pre = []
+    for l in range(nl):
+        pre.append(saved[o:o + E * w[l + 1]].view(E, w[l + 1]) > 0)
+        o += _al(E * w[l + 1])
+    for l in range(nl):
+        o += _al(E * w[l + 1])
+    o += _al(E * F) + _al(E) + _al((K + 1) * N * F) + _al(K * N * F)
+    nz = saved[o:o + K * N].view(torch.int32).view(K, N) != 0
+    return {"kind": "swegnn", "pre": pre, "nz": [nz[k] for k in range(K)]}
+
+
+def _mlp_decisions(d, saved):
+    """The saved buffer of msw_mlp_train_forward (mlp_layout_of): pre[l], post[l]."""
+    R, nl = d.rows, d.n_layers
+    o, pre = 0, []
+    for l in range(nl):
+        w = d.width[l + 1]
+        pre.append(saved[o:o + R * w].view(R, w) > 0)
+        o += _al(R * w)
+    return {"kind": "mlp", "pre": pre}
 
 
 class GraphCSR:
@@ -247,6 +284,8 @@ class _SwegnnFunction(torch.autograd.Function):
                                                      ea.data_ptr() if ea is not None else None,
                                                      saved.data_ptr(), out.data_ptr(),
                                                      C.c_void_p(_raw_stream(dev.index or 0))))
+        if RECORD is not None:
+            RECORD.append(_swegnn_decisions(d, saved))
         ctx.meta = meta
         ctx.has_ea = edge_attr is not None
         ctx.save_for_backward(x_s, x_d, ea if ea is not None else torch.empty(0, device=dev), saved, *params)
@@ -365,6 +404,8 @@ class _MlpFunction(torch.autograd.Function):
         with torch.cuda.device(dev):  # the kernels launch on the current device
             L.check(L.lib().msw_mlp_train_forward(C.byref(d), x.data_ptr(), saved.data_ptr(), out.data_ptr(),
                                                   C.c_void_p(_raw_stream(dev.index or 0))))
+        if RECORD is not None:
+            RECORD.append(_mlp_decisions(d, saved))
         ctx.meta = meta
         ctx.save_for_backward(x, saved, *params)
         return out

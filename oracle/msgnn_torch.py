@@ -32,6 +32,70 @@ from torch.linalg import vector_norm
 
 NUM_WATER_VARS = 2
 
+# ------------------------------------------------------------------ branch following
+# Off by default (then every function below is the op-for-op restatement).  Set through
+# `following(tape)`: a list of the discrete decisions a fp32 run took, in call order --
+# {"kind": "mlp", "pre": [bool per layer]} per make_mlp call, {"kind": "swegnn", "pre": [...],
+# "nz": [bool per hop]} per SWEGNN call (mswegnn.autograd.RECORD reads them back from the HIP
+# kernels), {"kind": "out", "x": relu'd output} per forward.  The restatement then takes those
+# sides of every discontinuity the reference's arithmetic has (activation kinks, the hop
+# predicate out.sum(1) != 0, the ReLU and _mask_small_WD of the output) and exact arithmetic
+# everywhere else: run in float64 it is the yardstick of that fp32 run's ROUNDING, separated from
+# its branch decisions (tests/test_gpu_train.py).
+_TAPE = None
+
+
+class following:
+    """Context manager: the restatement follows `tape` (see above); `.flips` collects, per
+    decision, where the yardstick's own arithmetic would have taken the other side.
+    `following(None)` RECORDS instead: the run's own decisions are appended to `.tape` (the
+    tape of a restatement run, e.g. the reference's arithmetic in fp32)."""
+
+    def __init__(self, tape):
+        self.recording = tape is None
+        self.tape, self.pos, self.flips = ([] if tape is None else list(tape)), 0, []
+
+    def next(self, kind):
+        rec = self.tape[self.pos]
+        assert rec["kind"] == kind, (self.pos, rec["kind"], kind)
+        self.pos += 1
+        return rec
+
+    def __enter__(self):
+        global _TAPE
+        _TAPE = self
+        return self
+
+    def __exit__(self, *exc):
+        global _TAPE
+        _TAPE = None
+
+
+def _mlp_sides(P, prefix, x, n_layers, act, dropout=False):
+    """The kink sides (pre-activation > 0) of every layer of a natural make_mlp pass."""
+    per = 1 + (1 if dropout else 0) + (1 if act is not None else 0)
+    sides = []
+    for i in range(n_layers):
+        li = i * per
+        x = Fn.linear(x, P[f"{prefix}.{li}.weight"], P.get(f"{prefix}.{li}.bias"))
+        sides.append((x > 0).detach())
+        if act is not None:
+            x = activation(act, x, P.get(f"{prefix}.{li + per - 1}.weight"))
+    return sides
+
+
+def _forced(name, x, w, side, where):
+    """activation(name, x, w) taking the recorded side of the kink (side: x > 0 in the run
+    followed); `where` labels the decision for the flip log."""
+    if name not in ("prelu", "relu", "leakyrelu"):
+        return activation(name, x, w)
+    side = side.to(x.device)
+    flip = side != (x > 0)
+    if bool(flip.any()):  # (decision, how many, largest distance of the own value to the kink)
+        _TAPE.flips.append((where, int(flip.sum()), float(x.detach()[flip].abs().max())))
+    neg = w * x if name == "prelu" else (0.1 * x if name == "leakyrelu" else torch.zeros_like(x))
+    return torch.where(side, x, neg)
+
 
 # ------------------------------------------------------------------ PyG scatter (2.4.0)
 def scatter(src, index, dim_size, reduce="sum"):
@@ -71,9 +135,16 @@ def activation(name, x, w=None):
     raise AttributeError(name)
 
 
-def mlp(P, prefix, x, n_layers, act, dropout=False):
+def mlp(P, prefix, x, n_layers, act, dropout=False, sides=None):
     """make_mlp Sequential (models/models.py:121-146): Linear -> [Dropout] -> act after
-    EVERY layer (also the last).  Module indices follow the Sequential layout."""
+    EVERY layer (also the last).  Module indices follow the Sequential layout.  `sides`
+    (branch following only): the recorded kink sides per layer."""
+    if _TAPE is not None and _TAPE.recording:
+        if sides is None:  # a make_mlp call of its own (not a SWEGNN's edge MLP)
+            _TAPE.tape.append({"kind": "mlp", "pre": _mlp_sides(P, prefix, x, n_layers, act, dropout)})
+        sides = None
+    elif _TAPE is not None and sides is None:
+        sides = _TAPE.next("mlp")["pre"]
     per = 1 + (1 if dropout else 0) + (1 if act is not None else 0)
     for i in range(n_layers):
         li = i * per
@@ -82,7 +153,10 @@ def mlp(P, prefix, x, n_layers, act, dropout=False):
         x = Fn.linear(x, W, b)
         if act is not None:
             ai = li + per - 1
-            x = activation(act, x, P.get(f"{prefix}.{ai}.weight"))
+            if sides is not None:
+                x = _forced(act, x, P.get(f"{prefix}.{ai}.weight"), sides[i], f"{prefix}.{li}")
+            else:
+                x = activation(act, x, P.get(f"{prefix}.{ai}.weight"))
     return x
 
 
@@ -94,12 +168,25 @@ def swegnn(P, prefix, x_s, x_d, edge_index, edge_attr, K, n_layers, act,
     row = edge_index[0]
     col = edge_index[1]
     num_nodes = x_d.size(0)
+    rec = _TAPE.next("swegnn") if _TAPE is not None and not _TAPE.recording else None
+    if _TAPE is not None and _TAPE.recording:  # every edge's MLP sides + each hop's predicate
+        e_all = torch.cat([x_s[row], x_s[col], x_d[row], x_d[col]] + ([edge_attr] if edge_features > 0 else []), 1)
+        rec_out = {"kind": "swegnn", "pre": _mlp_sides(P, f"{prefix}.edge_mlp", e_all, n_layers, act), "nz": []}
+        _TAPE.tape.append(rec_out)
     if with_filter_matrix:
         out = Fn.linear(x_d.clone(), P[f"{prefix}.filter_matrix.0.weight"])      # :402
     else:
         out = x_d.clone()                                                          # :404
     for k in range(K):
         mask = out.sum(1) != 0                                                     # :408
+        if _TAPE is not None and _TAPE.recording:
+            rec_out["nz"].append(mask.detach())
+        if rec is not None:
+            side = rec["nz"][k].to(mask.device)
+            if bool((side != mask).any()):
+                _TAPE.flips.append((f"{prefix}.hop{k}", int((side != mask).sum()),
+                                    float(out.detach().sum(1)[side != mask].abs().max())))
+            mask = side
         mask_row = mask[row]
         mask_col = mask[col]
         edge_index_mask = mask_row + mask_col                                      # :411
@@ -107,7 +194,10 @@ def swegnn(P, prefix, x_s, x_d, edge_index, edge_attr, K, n_layers, act,
                           x_d[row][edge_index_mask], x_d[col][edge_index_mask]], 1)  # :414
         if edge_features > 0:
             e_ij = torch.cat([e_ij, edge_attr[edge_index_mask]], 1)                # :420
-        s_ij = mlp(P, f"{prefix}.edge_mlp", e_ij, n_layers, act)                   # :422
+        sides = [p[edge_index_mask.to(p.device)] for p in rec["pre"]] if rec is not None else None
+        if _TAPE is not None and _TAPE.recording:
+            sides = []  # the edge MLP's sides were recorded above, over every edge
+        s_ij = mlp(P, f"{prefix}.edge_mlp", e_ij, n_layers, act, sides=sides)     # :422
         if normalize:
             s_ij = s_ij / vector_norm(s_ij, dim=1, keepdim=True)                   # :425
             s_ij.masked_fill_(torch.isnan(s_ij), 0)                                # :426
@@ -149,6 +239,31 @@ def mask_small_wd(x, epsilon=0.0001):
     wd = x[:, 0::NUM_WATER_VARS] * (x[:, 0::NUM_WATER_VARS].abs() > epsilon)
     v = x[:, 1::NUM_WATER_VARS] * (x[:, 0::NUM_WATER_VARS] != 0)
     return torch.cat((wd, v), dim=-1)
+
+
+def relu_mask(x, epsilon=0.0001):
+    """torch.relu then mask_small_wd (gnn.py:345-348) -- or, following a tape, the recorded
+    sides of the ReLU and of both masks (the run's relu'd output x_run: x_run > 0, |h| > eps,
+    h != 0)."""
+    if _TAPE is None or _TAPE.recording:
+        y = torch.relu(x)
+        if _TAPE is not None:
+            _TAPE.tape.append({"kind": "out", "x": y.detach()})
+        return mask_small_wd(y, epsilon)
+    xr = _TAPE.next("out")["x"].to(x.device)
+    pos = xr > 0
+    flip = pos != (x > 0)
+    if bool(flip.any()):
+        _TAPE.flips.append(("relu", int(flip.sum()), float(x.detach()[flip].abs().max())))
+    x = torch.where(pos, x, torch.zeros_like(x))
+    h = x[:, 0::NUM_WATER_VARS]
+    hr = xr[:, 0::NUM_WATER_VARS]
+    keep, wet = hr.abs() > epsilon, hr != 0
+    for name, a, b, dist in (("depth_mask", keep, h.abs() > epsilon, (h.abs() - epsilon).abs()),
+                             ("velocity_mask", wet, h != 0, h.abs())):
+        if bool((a != b).any()):
+            _TAPE.flips.append((name, int((a != b).sum()), float(dist.detach()[a != b].max())))
+    return torch.cat((h * keep, x[:, 1::NUM_WATER_VARS] * wet), dim=-1)
 
 
 def create_scale_mask(num_nodes, num_scales, node_ptr):
@@ -217,8 +332,7 @@ def msgnn_forward(P, cfg, graph):
     x = activation(cfg["gnn_activation"], x, P.get("gnn_activation.weight"))
     x = mlp(P, "node_decoder", x, L, act)
     x = x + residual(P, cfg, x0)
-    x = torch.relu(x)
-    return mask_small_wd(x, 0.0001)
+    return relu_mask(x, 0.0001)
 
 
 def gnn_forward(P, cfg, graph):
@@ -250,8 +364,7 @@ def gnn_forward(P, cfg, graph):
         x_d = x
     x = mlp(P, "node_decoder", x, L, act, dropout=bool(cfg.get("dropout", 0)))
     x = x + residual(P, cfg, x0)
-    x = torch.relu(x)
-    return mask_small_wd(x, 0.0001)
+    return relu_mask(x, 0.0001)
 
 
 def forward(P, cfg, graph):

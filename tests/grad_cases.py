@@ -135,33 +135,48 @@ def zenodo4_graph(T=5):
     return make_multiscale_mesh(**kw, T=T)
 
 
-def zenodo4_training_step_case(dev, R, engine="auto", dtype=torch.float32, premask=None):
-    """BASELINE config 2 at the bench's size: the reference's training_step on the zenodo4 mesh
-    (K4_F32, one-graph batch, R rollout steps) -> (loss, gradients).  `premask`, a list, receives
-    the fine-scale decoder output entering _mask_small_WD at every rollout step (the quantity
-    whose side of the 1e-4 threshold decides a fork)."""
+def zenodo4_batch(dev, dtype=torch.float32):
+    """The fixture's one-graph batch, adapted as training_step does (train.py:127)."""
     from mswegnn.batch import collate
     from mswegnn.rollout import adapt_batch_training
     fx = golden("fx_grad_train_zenodo4")
     g = zenodo4_graph()
     assert np.array_equal(graph_digest(g), fx["digest"])
     g.y = torch.from_numpy(fx["y"])
-    n0 = int(g.node_ptr[1])
-    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(dev).to(dtype).train()
-    m.engine = engine
-    if premask is not None:
-        orig = type(m)._mask_small_WD
-
-        def recording(self, x, epsilon=0.001):
-            premask.append(x.detach()[:n0].clone())
-            return orig(self, x, epsilon)
-        m._mask_small_WD = recording.__get__(m)
-    m.zero_grad(set_to_none=True)
     b = collate([g])
     for k in ("x", "edge_attr", "BC", "y"):
         setattr(b, k, getattr(b, k).to(dtype))
-    temp = adapt_batch_training(b.to(dev))
-    loss = loss_ref.training_step(m, temp, R)
+    return adapt_batch_training(b.to(dev)), int(g.node_ptr[1]), fx
+
+
+def zenodo4_training_step_case(dev, R, engine="auto", dtype=torch.float32, premask=None, record=None):
+    """BASELINE config 2 at the bench's size: the reference's training_step on the zenodo4 mesh
+    (K4_F32, one-graph batch, R rollout steps) -> (loss, gradients).  `premask`, a list, receives
+    the fine-scale decoder output entering _mask_small_WD at every rollout step (the quantity
+    whose side of the 1e-4 threshold decides a fork).  `record`, a list, receives the tape of
+    every discrete decision the run took, in call order (mswegnn.autograd.RECORD for the HIP
+    training kernels, plus the relu'd output of each forward): what msgnn_torch.following
+    replays in float64 (oracle_zenodo4_step(tape=...))."""
+    from mswegnn import autograd as ag
+    temp, n0, fx = zenodo4_batch(dev, dtype)
+    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(dev).to(dtype).train()
+    m.engine = engine
+    if premask is not None or record is not None:
+        orig = type(m)._mask_small_WD
+
+        def recording(self, x, epsilon=0.001):
+            if premask is not None:
+                premask.append(x.detach()[:n0].clone())
+            if record is not None:
+                record.append({"kind": "out", "x": x.detach().clone()})
+            return orig(self, x, epsilon)
+        m._mask_small_WD = recording.__get__(m)
+    m.zero_grad(set_to_none=True)
+    ag.RECORD = record
+    try:
+        loss = loss_ref.training_step(m, temp, R)
+    finally:
+        ag.RECORD = None
     loss.backward()
     out = {"loss": loss.detach()}
     out.update({"g__" + n: p.grad for n, p in m.named_parameters() if p.grad is not None})
@@ -225,7 +240,7 @@ def global_rel(ours, fx, prefix):
     return (num / den) ** 0.5
 
 
-def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0, floor=1e-2, floor_rel=1e-2):
+def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0, floor=1e-2, floor_rel=1e-2, noise=None):
     """The gradient bar, per parameter tensor (max-abs relative: max|ours - ref| / max|ref|):
     1. within `tol` of the reference's fp32 result; or
     2. (`floor`) an absolute error within tol x floor x the largest gradient entry of the
@@ -237,7 +252,9 @@ def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0, floor=1e-2, floor_
        a small tensor that is zero, or of the wrong sign, does not pass here; or
     3. (the fp64 rule) no further from the reference's float64 result than `slack` x the
        reference's OWN fp32 run is (a rollout the fp32 reference cannot resolve: a mask flip of
-       _mask_small_WD forks it).  Nothing of ours is a yardstick.
+       _mask_small_WD forks it) -- or (`noise`, reference_fp32_noise) than `slack` x the
+       farthest of an ensemble of the reference's arithmetic in fp32 on one-ulp-perturbed
+       inputs.  Nothing of ours is a yardstick.
     Returns (worst error vs fp32, {tensor: how it passed past rule 1}); asserts.  The tensors
     passed by rule 2 or 3 are printed."""
     errs = compare(ours, fx, prefix)
@@ -261,6 +278,8 @@ def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0, floor=1e-2, floor_
         ref64 = torch.from_numpy(fx[fp64_prefix + k])
         e_o = rel_err(ours.get(k, ours.get(prefix + k)), ref64)
         e_r = rel_err(torch.from_numpy(ref), ref64)
+        if noise is not None and k in noise:
+            e_r = max(e_r, noise[k])
         rule64[k] = ("fp64", e_o, e_r)
         if not e_o <= max(tol, slack * e_r):
             bad[k] = (e, e_o, e_r)
@@ -268,3 +287,65 @@ def check(ours, fx, prefix, tol, fp64_prefix=None, slack=3.0, floor=1e-2, floor_
         print(f"{prefix}: past rule 1 -> {rule64}")
     assert not bad, (prefix, bad)
     return worst, rule64
+
+
+def oracle_training_step(temp, P, cfg, R, tape=None, record=False):
+    """The reference's training_step through the oracle restatement (oracle/msgnn_torch.py,
+    loss_ref.py) on an adapted batch `temp`, weights P {state-dict name: tensor} in the dtype of
+    the run -- following `tape` or recording its own decisions (record=True; see
+    msgnn_torch.following) -> (loss, gradients, the following context)."""
+    import msgnn_torch as orc
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
+
+    class Model:  # loss_ref.training_step's view of a model
+        previous_t = 3
+        NUM_WATER_VARS = 2
+
+        def __call__(self, graph):
+            return orc.msgnn_forward(P, cfg, graph)
+    with orc.following(None if record else tape) as fl:
+        loss = loss_ref.training_step(Model(), temp, R)
+    loss.backward()
+    return loss.detach(), {"g__" + k: p.grad.float() for k, p in P.items() if p.grad is not None}, fl
+
+
+def oracle_zenodo4_step(R, dtype, tape=None, record=False):
+    """oracle_training_step on the zenodo4 fixture's batch (CPU, `dtype`)."""
+    import msgnn_torch as orc
+    temp, _, _ = zenodo4_batch(torch.device("cpu"), dtype)
+    P = {k: v.to(dtype) for k, v in weights("K4_F32").items()}
+    return oracle_training_step(temp, P, orc.msgnn_config(num_scales=4, hid_features=32, K=4), R, tape, record)
+
+
+def reference_fp32_noise(make_batch, P, cfg, R, fx, p64, n=6, seed=0):
+    """How far the REFERENCE's arithmetic in fp32 lands from its float64 result per gradient
+    tensor, over an ensemble: the oracle restatement (bit-identical to the reference on CPU) run
+    n times in fp32 on the batch's float inputs perturbed by one ulp at random (x, edge_attr,
+    BC) -- each run another equally valid fp32 rounding of the same problem.  One run (the
+    fixture's) is one sample of that noise; a tensor whose sum cancels heavily (a PReLU slope
+    sums every element of its layer) spreads over a range no fp32 implementation can be held
+    below.  -> {tensor: max over the ensemble of max|run - fp64| / max|fp64|}."""
+    gen = torch.Generator().manual_seed(seed)
+    worst = {}
+    for _ in range(n):
+        temp = make_batch()
+        for k in ("x", "edge_attr", "BC"):
+            v = getattr(temp, k)
+            bump = torch.randint(0, 3, v.shape, generator=gen).to(v.device) - 1  # -1 / 0 / +1 ulp
+            setattr(temp, k, torch.where(bump > 0, torch.nextafter(v, v.new_tensor(float("inf"))),
+                                         torch.where(bump < 0, torch.nextafter(v, v.new_tensor(float("-inf"))), v)))
+        _, g, _ = oracle_training_step(temp, {k: v.float() for k, v in P.items()}, cfg, R)
+        for k, v in g.items():
+            if p64 + k in fx:
+                worst[k] = max(worst.get(k, 0.0), rel_err(v, torch.from_numpy(fx[p64 + k])))
+    return worst
+
+
+def as_fixture(grads, prefix="X__"):
+    """{g__name: tensor} -> {prefix + g__name: ndarray} (compare / global_rel against it)."""
+    return {prefix + k: v.detach().cpu().numpy() for k, v in grads.items()}
+
+
+# a decision whose float64 value lies this close to its threshold is "within rounding" of it:
+# the values are O(1) (pre-activations, depths), fp32 dot products of 64 terms round at ~1e-6
+FLIP_DIST = 1e-5

