@@ -171,9 +171,11 @@ int msw_plan_destroy(msw_plan* plan);
 
 /* msw_plan_create for one rank of a partitioned mesh: `xch` describes its halo exchange
  * (hop pairs are not used: their halo is two rings deep).  The exchange itself runs either
- * over RCCL (msw_plan_set_comm, one process per GPU, inside msw_rollout; eager launches
- * unless MSW_PART_GRAPH=1 asks for graph capture) or between plans of one process
- * (msw_group_rollout, validation on one GPU). */
+ * over RCCL (msw_plan_set_comm, one process per GPU, inside msw_rollout; launched eagerly:
+ * a partitioned plan is created with graph capture off, and msw_set_graph_capture(plan, 1) is
+ * the only way to capture the RCCL exchanges too) or between plans of one process
+ * (msw_group_rollout, validation on one GPU: the group's steps are captured as hipGraphs held
+ * by plans[0] -- msw_set_graph_capture(plans[0], 0) steps it eagerly). */
 int msw_plan_create_part(const msw_graph_desc* graph, const msw_model_desc* model, int device,
                          const msw_exchange_desc* xch, int32_t rank, msw_plan** out_plan);
 

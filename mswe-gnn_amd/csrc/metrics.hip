@@ -14,6 +14,8 @@
 // integer confusion counts use integer atomics: exact in any order.)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../../include/mswegnn.h"
 #include "engine.h"
 
@@ -46,39 +48,63 @@ struct MetricArgs {
   unsigned long long* counts;   // this simulation's [T][nthr][4]
 };
 
+// Grid-stride over 256-row blocks (at most kMaxParts workgroups per simulation, so the partials
+// do not grow with the mesh): each thread adds its rows' terms in row-block order, then the
+// workgroup's waves are combined in a fixed order -- deterministic for a given grid.
+constexpr int kMaxParts = 512;
 __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
-  const int i = blockIdx.x * kThreads + threadIdx.x;
-  const bool valid = i < a.nrows;
-  const size_t n = (size_t)a.row0 + (valid ? i : 0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __shared__ double wsum[kThreads / 64][kSums];
   const int t0 = blockIdx.y * kTChunk;
-  const double ar = valid && a.area ? (double)a.area[n] : 0.0;
   for (int t = t0; t < t0 + kTChunk && t < a.T; ++t) {
-    float dh = 0.f, dv = 0.f, ph = 0.f, rh = 0.f;
-    if (valid) {
-      ph = a.pred[(n * 2 + 0) * a.T + t];
-      rh = a.real[(n * 2 + 0) * a.T + t];
-      dh = ph - rh;
-      dv = a.pred[(n * 2 + 1) * a.T + t] - a.real[(n * 2 + 1) * a.T + t];
-    }
-    const bool wet = valid && (dh != 0.f || dv != 0.f);
-    double v[kSums];
-    v[0] = fabs((double)dh);
-    v[1] = fabs((double)dv);
-    v[2] = (double)dh * dh;
-    v[3] = (double)dv * dv;
-    v[4] = wet ? v[0] : 0.0;
-    v[5] = wet ? v[1] : 0.0;
-    v[6] = wet ? v[2] : 0.0;
-    v[7] = wet ? v[3] : 0.0;
-    v[8] = wet ? 1.0 : 0.0;
-    v[9] = ar * (double)ph;
+    double acc[kSums];
 #pragma unroll
-    for (int k = 0; k < kSums; ++k) v[k] = wave_sum(v[k]);
+    for (int k = 0; k < kSums; ++k) acc[k] = 0.0;
+    for (int rb = blockIdx.x; rb * kThreads < a.nrows; rb += gridDim.x) {  // uniform per workgroup
+      const int i = rb * kThreads + threadIdx.x;
+      const bool valid = i < a.nrows;
+      const size_t n = (size_t)a.row0 + (valid ? i : 0);
+      float dh = 0.f, dv = 0.f, ph = 0.f, rh = 0.f;
+      if (valid) {
+        ph = a.pred[(n * 2 + 0) * a.T + t];
+        rh = a.real[(n * 2 + 0) * a.T + t];
+        dh = ph - rh;
+        dv = a.pred[(n * 2 + 1) * a.T + t] - a.real[(n * 2 + 1) * a.T + t];
+      }
+      const double ar = valid && a.area ? (double)a.area[n] : 0.0;
+      const bool wet = valid && (dh != 0.f || dv != 0.f);
+      const double ah = fabs((double)dh), av = fabs((double)dv);
+      const double qh = (double)dh * dh, qv = (double)dv * dv;
+      acc[0] += ah;
+      acc[1] += av;
+      acc[2] += qh;
+      acc[3] += qv;
+      acc[4] += wet ? ah : 0.0;
+      acc[5] += wet ? av : 0.0;
+      acc[6] += wet ? qh : 0.0;
+      acc[7] += wet ? qv : 0.0;
+      acc[8] += wet ? 1.0 : 0.0;
+      acc[9] += ar * (double)ph;
+      for (int k = 0; k < a.nthr; ++k) {
+        const bool p = ph > a.thr[k], r = rh > a.thr[k];
+        const unsigned long long tp = __popcll(__ballot(valid && p && r));
+        const unsigned long long tn = __popcll(__ballot(valid && !p && !r));
+        const unsigned long long fp = __popcll(__ballot(valid && p && !r));
+        const unsigned long long fn = __popcll(__ballot(valid && !p && r));
+        if (lane == 0) {
+          unsigned long long* c = a.counts + ((size_t)t * a.nthr + k) * 4;
+          atomicAdd(c + 0, tp);
+          atomicAdd(c + 1, tn);
+          atomicAdd(c + 2, fp);
+          atomicAdd(c + 3, fn);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSums; ++k) acc[k] = wave_sum(acc[k]);
     if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < kSums; ++k) wsum[w][k] = v[k];
+      for (int k = 0; k < kSums; ++k) wsum[w][k] = acc[k];
     }
     __syncthreads();
     if (threadIdx.x < kSums) {  // the waves' sums in a fixed order
@@ -88,20 +114,6 @@ __global__ __launch_bounds__(kThreads) void k_metrics(MetricArgs a) {
       a.part[((size_t)blockIdx.x * a.T + t) * kSums + threadIdx.x] = b;
     }
     __syncthreads();
-    for (int k = 0; k < a.nthr; ++k) {
-      const bool p = ph > a.thr[k], r = rh > a.thr[k];
-      const unsigned long long tp = __popcll(__ballot(valid && p && r));
-      const unsigned long long tn = __popcll(__ballot(valid && !p && !r));
-      const unsigned long long fp = __popcll(__ballot(valid && p && !r));
-      const unsigned long long fn = __popcll(__ballot(valid && !p && r));
-      if (lane == 0) {
-        unsigned long long* c = a.counts + ((size_t)t * a.nthr + k) * 4;
-        atomicAdd(c + 0, tp);
-        atomicAdd(c + 1, tn);
-        atomicAdd(c + 2, fp);
-        atomicAdd(c + 3, fn);
-      }
-    }
   }
 }
 
@@ -127,7 +139,22 @@ extern "C" int msw_rollout_metrics(const float* pred, const float* real, int32_t
     return msw::set_error(MSW_ERR_INVALID, "T, num_sims or n_thr out of range (n_thr <= 4)");
   if (T == 0) return MSW_OK;
   hipStream_t st = (hipStream_t)stream;
+  // one stream-ordered scratch for every simulation's workgroup partials, sized for the largest
+  // (kMaxParts workgroups at most: bounded whatever the mesh)
+  const long count = (long)T * kSums;
+  int nb_max = 0;
   for (int g = 0; g < num_sims; ++g) {
+    const long nr = fine_ranges[2 * g + 1] - fine_ranges[2 * g];
+    if (nr < 0) return msw::set_error(MSW_ERR_INVALID, "fine range end < start");
+    nb_max = std::max(nb_max, (int)std::min<long>(kMaxParts, (nr + kThreads - 1) / kThreads));
+  }
+  double* part = nullptr;
+  if (nb_max > 0) {
+    const hipError_t e = hipMallocAsync((void**)&part, (size_t)nb_max * count * sizeof(double), st);
+    if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
+  }
+  hipError_t e = hipSuccess;
+  for (int g = 0; g < num_sims && e == hipSuccess; ++g) {
     MetricArgs a{};
     a.pred = pred;
     a.real = real;
@@ -135,29 +162,23 @@ extern "C" int msw_rollout_metrics(const float* pred, const float* real, int32_t
     a.T = T;
     a.row0 = (int)fine_ranges[2 * g];
     a.nrows = (int)(fine_ranges[2 * g + 1] - fine_ranges[2 * g]);
-    if (a.nrows < 0) return msw::set_error(MSW_ERR_INVALID, "fine range end < start");
     a.nthr = n_thr;
     for (int k = 0; k < n_thr; ++k) a.thr[k] = thresholds[k];
     double* out = sums + (size_t)g * T * kSums;
     a.counts = reinterpret_cast<unsigned long long*>(counts) + (size_t)g * T * (n_thr > 0 ? n_thr : 1) * 4;
-    const long count = (long)T * kSums;
     if (a.nrows == 0) {  // no fine rows: zero sums (the caller zeroes the counts)
-      if (hipMemsetAsync(out, 0, (size_t)count * sizeof(double), st) != hipSuccess)
-        return msw::set_error(MSW_ERR_HIP, "hipMemsetAsync");
+      e = hipMemsetAsync(out, 0, (size_t)count * sizeof(double), st);
       continue;
     }
-    const int nb = (a.nrows + kThreads - 1) / kThreads;
-    double* part = nullptr;  // stream-ordered scratch for the workgroup partials
-    hipError_t e = hipMallocAsync((void**)&part, (size_t)nb * count * sizeof(double), st);
-    if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
+    const int nb = (int)std::min<long>(kMaxParts, ((long)a.nrows + kThreads - 1) / kThreads);
     a.part = part;
     hipLaunchKernelGGL(k_metrics, dim3(nb, (T + kTChunk - 1) / kTChunk), dim3(kThreads), 0, st, a);
     hipLaunchKernelGGL(k_metrics_reduce, dim3((unsigned)((count + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
                        (const double*)part, nb, count, out);
     e = hipGetLastError();
-    const hipError_t f = hipFreeAsync(part, st);
-    if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
-    if (f != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(f));
   }
+  const hipError_t f = part ? hipFreeAsync(part, st) : hipSuccess;
+  if (e != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(e));
+  if (f != hipSuccess) return msw::set_error(MSW_ERR_HIP, hipGetErrorString(f));
   return MSW_OK;
 }

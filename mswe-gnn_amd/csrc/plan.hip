@@ -7,6 +7,7 @@
 //   MSGNN.forward  models/gnn.py:267-350     GNN.forward  models/gnn.py:102-152
 //   SWEGNN.forward models/gnn.py:387-445     rollout_test training/train.py:67-95
 //   update_batch_multiscale training/train.py:31-65 (batched node_ptr layout)
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <dlfcn.h>
@@ -381,11 +382,27 @@ struct msw_plan {
   // (edge_coop_lds_cap): the schedule is rebuilt with the pooling / unpooling launches
   int no_fuse = 0;
   std::vector<void*> owned;
+  // In-process group of partitioned plans (msw_group_rollout): the group's steps captured as
+  // graphs too (every part's launches and the halo copies between their buffers), held by the
+  // group's plan 0 and keyed by the members' identities and graph generations
+  uint64_t uid = 0;              // unique per plan created in this process
+  int graph_gen = 0;             // advanced whenever this plan's captured arguments go stale
+  int group_graph = 1;           // msw_set_graph_capture(plans[0], 0): the group steps eagerly
+  hipGraphExec_t group_one = nullptr, group_multi = nullptr;
+  std::vector<uint64_t> group_key;
+  void drop_group_graphs() {
+    if (group_one) (void)hipGraphExecDestroy(group_one);
+    if (group_multi) (void)hipGraphExecDestroy(group_multi);
+    group_one = group_multi = nullptr;
+    group_key.clear();
+  }
   void drop_graphs() {
     if (step_exec) (void)hipGraphExecDestroy(step_exec);
     if (multi_exec) (void)hipGraphExecDestroy(multi_exec);
     if (fwd_exec) (void)hipGraphExecDestroy(fwd_exec);
     step_exec = multi_exec = fwd_exec = nullptr;
+    drop_group_graphs();
+    ++graph_gen;
   }
   ~msw_plan() {
     drop_graphs();
@@ -991,8 +1008,6 @@ void caps(msw_plan* P, A& a, int kind, int prelu, int last, int floats) {
   a.max_blocks = resident_of(P->NT, kind, prelu, last, (size_t)floats * 4, 1);
   a.fit_blocks = resident_of(P->NT, kind, prelu, last, (size_t)floats * 4, 0);
 }
-// A/B measurements: MSW_NO_LOOP=eh,hop,epi,all keeps those launches one tile per wave at
-// any size (no grid-stride loop).
 constexpr int kHopLoopTiles = 65536;
 // middle hops of scales with at least this many edge tiles run in the row layout
 // (k_hop_rows; MSW_HOP_ROWS=0 keeps the edge tiles)
@@ -1086,8 +1101,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
     }
     case L_HOP:
       caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
-      // one tile per wave below kHopLoopTiles (MSW_HOP_LOOP=1: loop whenever the grid does
-      // not fit): the grid-stride variant measured 1.1-1.6 % slower on the batch of 8 and
+      // one tile per wave below kHopLoopTiles: the grid-stride variant measured 1.1-1.6 % slower on the batch of 8 and
       // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
       // (profiles/r01_v7/ab_edge_waves.txt)
       if (L.hop.ntiles < kHopLoopTiles) L.hop.max_blocks = 0;
@@ -1411,6 +1425,8 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
   if (m->learned_pooling) return fail(MSW_ERR_UNSUPPORTED, "learned_pooling=True is not implemented");
   HIP_TRY(hipSetDevice(device));
   std::unique_ptr<msw_plan> P(new msw_plan());
+  static std::atomic<uint64_t> next_uid{1};
+  P->uid = next_uid++;
   P->device = device;
   P->model_type = m->model_type;
   P->F = m->hid_features;
@@ -1790,11 +1806,43 @@ int msw_group_rollout(msw_plan* const* plans, int32_t num_plans, const float* co
     int rc = rollout_prologue(plans[k], x0[k], bc[k], bc_tstride[k], node_bc[k], n_bc[k], type_bc, T, out[k], st);
     if (rc) return rc;
   }
-  for (int t = 0; t < T; ++t) {
-    int rc = P0->NT == 1 ? group_step<1>(plans, num_plans, st)
-           : P0->NT == 2 ? group_step<2>(plans, num_plans, st)
-                         : group_step<4>(plans, num_plans, st);
-    if (rc) return rc;
+  auto step = [&](hipStream_t s) {
+    return P0->NT == 1 ? group_step<1>(plans, num_plans, s)
+         : P0->NT == 2 ? group_step<2>(plans, num_plans, s)
+                       : group_step<4>(plans, num_plans, s);
+  };
+  msw_plan* G0 = plans[0];
+  if (G0->group_graph) {
+    // every part's launches and the halo copies of `steps` consecutive steps in one graph,
+    // replayed as msw_rollout replays its own (the parts' device-side I/O records were written
+    // by their prologues; the kernels read the step counters from them)
+    std::vector<uint64_t> key;
+    for (int k = 0; k < num_plans; ++k) {
+      key.push_back(plans[k]->uid);
+      key.push_back((uint64_t)plans[k]->graph_gen);
+    }
+    if (key != G0->group_key) {
+      G0->drop_group_graphs();
+      G0->group_key = key;
+    }
+    auto capture = [&](hipGraphExec_t* exec, int steps) -> int {
+      return capture_graph(G0, exec, [&](hipStream_t cs) {
+        int rc = MSW_OK;
+        for (int k = 0; k < steps && !rc; ++k) rc = step(cs);
+        return rc;
+      });
+    };
+    const int G = std::max(1, G0->graph_steps);
+    int rc;
+    if (G > 1 && T >= G && !G0->group_multi && (rc = capture(&G0->group_multi, G))) return rc;
+    if ((G == 1 || T % G) && !G0->group_one && (rc = capture(&G0->group_one, 1))) return rc;
+    int t = 0;
+    if (G > 1)
+      for (; t + G <= T; t += G) HIP_TRY(hipGraphLaunch(G0->group_multi, st));
+    for (; t < T; ++t) HIP_TRY(hipGraphLaunch(G0->group_one, st));
+  } else {
+    for (int t = 0; t < T; ++t)
+      if (int rc = step(st)) return rc;
   }
   for (int k = 0; k < num_plans; ++k)
     if (int rc = final_decode(plans[k], st)) return rc;
@@ -1845,6 +1893,8 @@ int msw_forward(msw_plan* P, const float* x, float* y, void* stream) {
 int msw_set_graph_capture(msw_plan* P, int enable) {
   if (!P) return fail(MSW_ERR_INVALID, "null plan");
   P->use_graph = enable ? 1 : 0;
+  P->group_graph = enable ? 1 : 0;
+  P->drop_group_graphs();
   return MSW_OK;
 }
 

@@ -103,11 +103,15 @@ class GraphCSR:
 
 
 def _drop_csr(key):
-    """Forget one cached GraphCSR and every descriptor template bound to it."""
+    """Forget one cached GraphCSR and every descriptor template bound to it; its owner's
+    finalizer is detached (one finalizer per live entry: a graph re-cached every epoch does not
+    pile them up, and a stale one can never drop a newer entry under the same key)."""
     ent = _CSR_CACHE.pop(key, None)
     if ent is not None:
-        for k in [k for k, m in _META_CACHE.items() if getattr(m, "csr", None) is ent[1]]:
-            del _META_CACHE[k]
+        ent[2].detach()
+        # a snapshot: a finalizer fired by the cyclic GC may call back into here
+        for k in [k for k, m in list(_META_CACHE.items()) if getattr(m, "csr", None) is ent[1]]:
+            _META_CACHE.pop(k, None)
 
 
 def graph_csr(edge_index, num_nodes):
@@ -125,8 +129,7 @@ def graph_csr(edge_index, num_nodes):
         return hit[1]
     _drop_csr(key)
     g = GraphCSR(edge_index, num_nodes)
-    _CSR_CACHE[key] = (weakref.ref(owner), g)
-    weakref.finalize(owner, _drop_csr, key)
+    _CSR_CACHE[key] = (weakref.ref(owner), g, weakref.finalize(owner, _drop_csr, key))
     while len(_CSR_CACHE) > _CSR_KEEP:
         _drop_csr(next(iter(_CSR_CACHE)))
     return g
@@ -134,6 +137,8 @@ def graph_csr(edge_index, num_nodes):
 
 def clear_caches():
     """Drop every cached CSR and descriptor template (their GPU arrays are freed)."""
+    for ent in list(_CSR_CACHE.values()):
+        ent[2].detach()
     _CSR_CACHE.clear()
     _META_CACHE.clear()
 

@@ -426,6 +426,28 @@ def test_partitioned_rollout_matches_whole_mesh(cuda, parts):
     assert per_step_rel(rg, torch.from_numpy(golden("fx_gnn_small_rollout10")["rollout"])) <= REL_TOL
 
 
+@pytest.mark.parametrize("parts", [2, 4])
+def test_group_rollout_graph_matches_eager(cuda, parts):
+    """msw_group_rollout replays its steps as hipGraphs (every part's launches + the halo copies
+    between the parts' buffers, 16 steps per graph, held by plans[0]): the same rollout bit for
+    bit as the eager group (msw_set_graph_capture(plans[0], 0)) and as the undivided plan, on a
+    replay (a second call) too, over T = 40 (two 16-step graph launches + eight single steps)."""
+    from mswegnn import _lib as L
+    from mswegnn.partition import PartitionedRollout
+    T = 40
+    g = make_multiscale_mesh(**mesh_config("small"), T=T).to(cuda)
+    m = _hip(build_msgnn(4, 32, 4, state=weights("K4_F32")), cuda)
+    whole = m.rollout(g, T).cpu()
+    pr = PartitionedRollout(m, g, parts, cuda)
+    graphed = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
+    again = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
+    L.check(L.lib().msw_set_graph_capture(pr.plans[0]._h, 0))
+    eager = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
+    pr.close()
+    assert torch.equal(graphed, eager) and torch.equal(graphed, again)
+    assert torch.equal(graphed, whole)
+
+
 def test_plan_cache_same_shape_graphs_in_sequence(cuda):
     """Two meshes of the same shape but different topology / edge_attr, one after the other,
     each freshly moved to the GPU (the allocator may hand the second the first's freed

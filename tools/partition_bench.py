@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--T", type=int, default=24)
     ap.add_argument("--parts", type=int, nargs="+", default=[2, 4])
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--eager", action="store_true",
+                    help="step the group eagerly (msw_set_graph_capture(plans[0], 0)) instead of its captured graphs")
     a = ap.parse_args()
     import bench
     from mswegnn.partition import PartitionedRollout
@@ -48,17 +50,21 @@ def main():
     gd = g.to(dev)
     t_whole, r_whole = timed(lambda: m.rollout(gd, a.T), a.reps)
     res = {"workload": a.workload, "fine_nodes": desc["fine_nodes"], "all_nodes": desc["all_nodes"],
-           "T": a.T, "undivided_ms": t_whole * 1e3, "parts": {}}
+           "T": a.T, "undivided_ms": t_whole * 1e3, "group": "eager" if a.eager else "graph", "parts": {}}
     ref = r_whole.cpu()
     den = [max(ref[..., t].abs().max().item(), 1e-30) for t in range(a.T)]
     for W in a.parts:
         pr = PartitionedRollout(m, g, W, device=dev)
+        if a.eager:
+            from mswegnn import _lib as L
+            L.check(L.lib().msw_set_graph_capture(pr.plans[0]._h, 0))
         t_p, r_p = timed(lambda: pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, a.T), a.reps)
         r_p = r_p.cpu()
         err = max((r_p[..., t] - ref[..., t]).abs().max().item() / den[t] for t in range(a.T))
         halo = sum(int(lp.graph.x.shape[0]) for lp in pr.parts) - desc["all_nodes"]
         res["parts"][W] = {"ms_all_parts_one_gpu": t_p * 1e3, "vs_undivided": t_p / t_whole,
-                           "halo_rows": halo, "max_rel_err_vs_undivided": err}
+                           "halo_rows": halo, "max_rel_err_vs_undivided": err,
+                           "bit_identical": bool(torch.equal(r_p, ref))}
         pr.close()
     print(json.dumps(res))
 
