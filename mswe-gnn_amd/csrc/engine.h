@@ -193,7 +193,8 @@ struct EdgeHopArgs {
   const EdgeChunk* chunks; int nchunks;  // k_edge_mlp: dense 16-edge chunks [nchunks][16]
   PoolFuse pool;                   // mean pooling + projection fused in (k_edge_coop only)
   int dma;                         // grid-stride variant with the next tile's rows LDS-DMA'd
-                                   // during the current tile's MLP (k_edge_hop_dma)
+                                   // during the current tile's MLP (k_edge_hop_dma): 1 = eight
+                                   // waves per workgroup, 2 = four
   int dma_off;                     // k_edge_hop_dma: floats of LDS before the per-wave regions
 };
 

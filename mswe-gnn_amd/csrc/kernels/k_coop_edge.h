@@ -42,6 +42,72 @@ __device__ __forceinline__ void mfma_layer_sub(const f32x4 (&in)[TIN], f32x4 (&o
 #pragma unroll
   for (int to = 0; to < TS; ++to) out[to] = acc[to];
 }
+// One layer's operands for output tiles [to0, to0 + TS), loaded ahead of the layer (the
+// blob operands of F = 64 come from L2: issued one layer early, their round trip overlaps the
+// previous layer's MFMA chain and exchange instead of following it); ops_layer is
+// mfma_layer_sub's arithmetic in the same order (proj's k order, then the bias).
+template <int TIN, int TS>
+struct LayerOps {
+  f32x4 w[TIN][TS];
+  f32x4 b[TS];
+};
+template <int TIN, int TS>
+__device__ __forceinline__ void ops_load(LayerOps<TIN, TS>& o, const LayerDev& L, const float* __restrict__ W,
+                                         int to0, int lane, int g) {
+  const float* A = W + L.a_off + (size_t)to0 * TIN * 256;
+#pragma unroll
+  for (int ti = 0; ti < TIN; ++ti)
+#pragma unroll
+    for (int to = 0; to < TS; ++to) o.w[ti][to] = ld4(A + ((size_t)(to * TIN + ti) * 64 + lane) * 4);
+#pragma unroll
+  for (int to = 0; to < TS; ++to) o.b[to] = ld4(W + L.b_off + 16 * (to0 + to) + 4 * g);  // zeros if bias=False
+}
+template <int TIN, int TS, int ACT>
+__device__ __forceinline__ void ops_layer(const f32x4 (&in)[TIN], f32x4 (&out)[TS], const LayerOps<TIN, TS>& o,
+                                          const LayerDev& L) {
+  f32x4 acc[TS];
+#pragma unroll
+  for (int to = 0; to < TS; ++to) acc[to] = zero4();
+#pragma unroll
+  for (int ti = 0; ti < TIN; ++ti)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int to = 0; to < TS; ++to) acc[to] = MSW_MFMA(o.w[ti][to][r], in[ti][r], acc[to]);
+#pragma unroll
+  for (int to = 0; to < TS; ++to) acc[to] = acc[to] + o.b[to];
+  act_tiles<ACT, TS>(acc, L.act, L.slope);
+#pragma unroll
+  for (int to = 0; to < TS; ++to) out[to] = acc[to];
+}
+// proj with D k-tiles of operands in flight (D = TIN: all issued before the first MFMA); the
+// same MFMA chain in the same k order as proj
+template <int TIN, int TOUT, int D>
+__device__ __forceinline__ void proj_ahead(const f32x4 (&in)[TIN], f32x4 (&acc)[TOUT], const float* __restrict__ A,
+                                           int lane) {
+  static_assert(D >= 1 && D <= TIN, "prefetch depth");
+  f32x4 w[D][TOUT];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int to = 0; to < TOUT; ++to) w[d][to] = ld4(A + ((size_t)(to * TIN + d) * 64 + lane) * 4);
+#pragma unroll
+  for (int to = 0; to < TOUT; ++to) acc[to] = zero4();
+#pragma unroll
+  for (int ti = 0; ti < TIN; ++ti) {
+    f32x4 cur[TOUT];
+#pragma unroll
+    for (int to = 0; to < TOUT; ++to) cur[to] = w[ti % D][to];
+    if (ti + D < TIN) {
+#pragma unroll
+      for (int to = 0; to < TOUT; ++to) w[ti % D][to] = ld4(A + ((size_t)(to * TIN + ti + D) * 64 + lane) * 4);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int to = 0; to < TOUT; ++to) acc[to] = MSW_MFMA(cur[to][r], in[ti][r], acc[to]);
+  }
+}
 // run_mlp with each layer's output tiles split over the P ranks; buffers alternate per layer
 template <int IN0, int T, int TL, int ACT, int P>
 __device__ __forceinline__ void coop_run_mlp(const f32x4 (&in)[IN0], f32x4 (&out)[TL], const MlpDev& m,
@@ -68,18 +134,22 @@ __device__ __forceinline__ void coop_run_mlp(const f32x4 (&in)[IN0], f32x4 (&out
   mfma_layer_sub<T, TL / P, ACT>(h, o, m.l[m.n - 1], W, r * (TL / P), lane, g);
   coop_exchange<TL, P>(o, out, ((m.n - 1) & 1) ? buf1 : buf0, xw, r, j, g);
 }
-// np_project with the output tiles of U, V and O split over the ranks (each stores its part)
-template <int TIN, int TS>
+// np_project with the output tiles of U, V and O split over the ranks (each stores its part);
+// D > 0: D k-tiles of operands in flight (proj_ahead), D = 0: proj
+template <int TIN, int TS, int D = 0>
 __device__ __forceinline__ void proj_store_part(const f32x4 (&in)[TIN], const float* A, int r, float* dst, size_t n,
                                                 int ntl, bool valid, int lane, int g) {
   f32x4 acc[TS];
-  proj<TIN, TS>(in, acc, A + (size_t)r * TS * TIN * 256, lane);
+  if constexpr (D > 0)
+    proj_ahead<TIN, TS, (D < TIN ? D : TIN)>(in, acc, A + (size_t)r * TS * TIN * 256, lane);
+  else
+    proj<TIN, TS>(in, acc, A + (size_t)r * TS * TIN * 256, lane);
   if (valid) {
 #pragma unroll
     for (int t = 0; t < TS; ++t) st4(dst + n * (16 * ntl) + 16 * (r * TS + t) + 4 * g, acc[t]);
   }
 }
-template <int NT, int H1T, int P>
+template <int NT, int H1T, int P, int D = 0>
 __device__ __forceinline__ void np_project_coop(const f32x4 (&xs)[NT], const f32x4 (&xin)[NT], const NpDesc& d,
                                                 const float* W, size_t n, bool valid, int r, int lane, int g) {
   constexpr int T2 = 2 * NT;
@@ -89,12 +159,12 @@ __device__ __forceinline__ void np_project_coop(const f32x4 (&xs)[NT], const f32
     in[t] = xs[t];
     in[NT + t] = xin[t];
   }
-  if (d.a_u >= 0) proj_store_part<T2, H1T / P>(in, W + d.a_u, r, d.U, n, H1T, valid, lane, g);
-  if (d.a_v >= 0) proj_store_part<T2, H1T / P>(in, W + d.a_v, r, d.V, n, H1T, valid, lane, g);
+  if (d.a_u >= 0) proj_store_part<T2, H1T / P, D>(in, W + d.a_u, r, d.U, n, H1T, valid, lane, g);
+  if (d.a_v >= 0) proj_store_part<T2, H1T / P, D>(in, W + d.a_v, r, d.V, n, H1T, valid, lane, g);
   if constexpr (P <= NT) {
-    if (d.a_o >= 0) proj_store_part<NT, NT / P>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
+    if (d.a_o >= 0) proj_store_part<NT, NT / P, D>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
   } else {  // more ranks than O tiles: ranks 0..NT-1 take one O tile each
-    if (d.a_o >= 0 && r < NT) proj_store_part<NT, 1>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
+    if (d.a_o >= 0 && r < NT) proj_store_part<NT, 1, D>(xin, W + d.a_o, r, d.O, n, NT, valid, lane, g);
   }
 }
 

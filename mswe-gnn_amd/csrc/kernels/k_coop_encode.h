@@ -44,11 +44,74 @@ __device__ __forceinline__ void enc_coop_mlp(const f32x4 (&in)[IN0], f32x4 (&out
   }
   last(h);
 }
+// enc_coop_mlp with the operands issued ahead (F = 64 reads them from the blob, i.e. from L2:
+// one round trip per layer instead of one per k-tile pair + the bias): the first layer's
+// operands are loaded by the caller (load(), early -- at kernel start), layer 1's are in flight
+// during layer 0's MFMA chain and exchange, deeper layers load theirs at the layer.  PF: every
+// layer's rank slice has TS = T / P output tiles (all F = 64 and F = 32 encoder MLPs at P =
+// NT); otherwise (the decoder at MSW_ENC_COOP_P=2) it is enc_coop_mlp.  Same arithmetic.
+#ifndef MSW_ENC_PF
+#define MSW_ENC_PF 1
+#endif
+template <int IN0, int T, int TL, int ACT, int P, int XW>
+struct CoopMlp {
+  static constexpr int TS = T / P;
+  static constexpr bool XL = TL % P == 0;  // the last layer split over the ranks, else on every rank
+  static constexpr bool PF = MSW_ENC_PF && (XL ? TL / P : TL) == TS;
+  LayerOps<IN0, TS> first;
+  __device__ __forceinline__ void load(const MlpDev& m, const float* __restrict__ W, int r, int lane, int g) {
+    if constexpr (PF) ops_load<IN0, TS>(first, m.l[0], W, (m.n == 1 && !XL) ? 0 : r * TS, lane, g);
+  }
+  // hook(): called once, after layer 0's MFMA chain (loads for what follows this MLP)
+  template <class Hook>
+  __device__ __forceinline__ void run(const f32x4 (&in)[IN0], f32x4 (&out)[TL], const MlpDev& m,
+                                      const float* __restrict__ W, int lane, int g, int j, int r, float* buf,
+                                      int& xc, Hook&& hook) const {
+    if constexpr (!PF) {
+      hook();
+      enc_coop_mlp<IN0, T, TL, ACT, P, XW>(in, out, m, W, lane, g, j, r, buf, xc);
+    } else {
+      const int tl0 = XL ? r * TS : 0;
+      auto finish = [&](const f32x4 (&o)[TS]) {
+        if constexpr (XL) {
+          coop_exchange<TL, P>(o, out, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+        } else {
+#pragma unroll
+          for (int t = 0; t < TL; ++t) out[t] = o[t];
+        }
+      };
+      f32x4 o[TS];
+      if (m.n == 1) {
+        ops_layer<IN0, TS, ACT>(in, o, first, m.l[0]);
+        hook();
+        finish(o);
+        return;
+      }
+      LayerOps<T, TS> nx;
+      ops_load<T, TS>(nx, m.l[1], W, m.n == 2 ? tl0 : r * TS, lane, g);
+      ops_layer<IN0, TS, ACT>(in, o, first, m.l[0]);
+      hook();
+      f32x4 h[T];
+      coop_exchange<T, P>(o, h, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+      ops_layer<T, TS, ACT>(h, o, nx, m.l[1]);
+      for (int li = 2; li < m.n; ++li) {
+        coop_exchange<T, P>(o, h, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+        LayerOps<T, TS> cur;
+        ops_load<T, TS>(cur, m.l[li], W, li + 1 == m.n ? tl0 : r * TS, lane, g);
+        ops_layer<T, TS, ACT>(h, o, cur, m.l[li]);
+      }
+      finish(o);
+    }
+  }
+};
+// projections' operands: this many k-tiles in flight (0: proj)
+constexpr int kEncProjAhead = MSW_ENC_PF ? 4 : 0;
 // Workgroup: WV waves = WV / P row tiles (F = 32: eight waves, the four row tiles of k_encode's
 // workgroup, so the weight region is staged as often as there; F = 64 reads the blob).
 template <int NT> constexpr int enc_coop_waves() { return NT == 2 ? 8 : kWaves; }
+// at most 128 registers: four waves per SIMD keep the zenodo4 F = 64 grid (3,488 waves) in one round
 template <int NT, int ACT, bool DEC, int P, int WV = enc_coop_waves<NT>()>
-__global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(4))) void k_encode_coop(EncodeArgs a) {
   constexpr int F = 16 * NT, T2 = 2 * NT, G = WV / P;
   constexpr int XW = 16 * T2 + 4;
   __shared__ __attribute__((aligned(16))) float xbuf[G][2][kRowsPerWave][XW];
@@ -72,9 +135,13 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
   float raw[4], dyn[4];
   float wlv;
   EpiPre<NT> pre;
-  f32x4 xu[NT];
+  // the decoder's pre-activation is split over the ranks like its MFMA layers: rank r loads and
+  // activates input tiles [r DS, (r + 1) DS) only, the tiles are exchanged before layer 0
+  constexpr int DS = NT / P;
+  f32x4 xu[DS];
   if (DEC) {  // as k_encode: not behind the step counter
-    load_row<NT>(xu, a.dec_in + (size_t)n * F, g);
+#pragma unroll
+    for (int t = 0; t < DS; ++t) xu[t] = ld4(a.dec_in + (size_t)n * F + 16 * (r * DS + t) + 4 * g);
     pre.ext = ext;
     pre.bc = a.dec.bc_slot[n];
 #pragma unroll
@@ -101,8 +168,20 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
   const float* Wl = kStaged<NT> ? (const float*)smem : c.W;
   float* buf = &xbuf[grp][0][0][0];
   int xc = 0;
-  if (DEC && dstep >= 0) {
+  // first-layer operands of the encoder MLPs, in flight from here (F = 64: from L2)
+  // (rollout mode: issued inside the decoder, once its own first layer has run)
+  CoopMlp<1, NT, NT, ACT, P, XW> stat_mlp, dyn_mlp;
+  auto enc_loads = [&]() {
+    stat_mlp.load(a.stat, Wl, r, lane, g);
+    dyn_mlp.load(a.dynm, Wl, r, lane, g);  // unconditional (scale 0 only uses it): no branch
+  };
+  auto none = [&]() {};
+  const bool decode = DEC && dstep >= 0;
+  if (!decode) enc_loads();
+  if (decode) {
 #pragma clang fp contract(off)
+    CoopMlp<NT, NT, 1, ACT, P, XW> dec_mlp;
+    dec_mlp.load(a.dec.dec, Wl, r, lane, g);
     if constexpr (!kBcHoist<NT>) {
       pre.step = dstep;
       bc_prefetch<NT>(pre, a.dec, c);
@@ -110,10 +189,9 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
     float nd[kMaxDyn];
     {
       f32x4 x0[NT], o[1];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) x0[t] = xu[t];
-      act_tiles<-1, NT>(x0, a.dec.pre_act, a.dec.pre_slope);
-      enc_coop_mlp<NT, NT, 1, ACT, P, XW>(x0, o, a.dec.dec, Wl, lane, g, j, r, buf, xc);
+      act_tiles<-1, DS>(xu, a.dec.pre_act, a.dec.pre_slope);
+      coop_exchange<NT, P>(xu, x0, buf + (xc++ & 1) * kRowsPerWave * XW, XW, r, j, g);
+      dec_mlp.run(x0, o, a.dec.dec, Wl, lane, g, j, r, buf, xc, enc_loads);
       decode_state_tail<NT>(o, a.dec, c, Wl, pre, n, valid && r == 0, lane, g, nd);
     }
 #pragma unroll
@@ -137,27 +215,27 @@ __global__ __launch_bounds__(64 * WV) void k_encode_coop(EncodeArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = (c.with_wl && 4 * g + q == nstat) ? wlv : raw[q];
     const f32x4 in[1] = {v};
-    enc_coop_mlp<1, NT, NT, ACT, P, XW>(in, xs, a.stat, Wl, lane, g, j, r, buf, xc);
+    stat_mlp.run(in, xs, a.stat, Wl, lane, g, j, r, buf, xc, none);
     if (valid && r == 0) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
   }
   MSW_MARK(c, 5);
   if (s == 0) {
     f32x4 xd[NT];
     const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
-    enc_coop_mlp<1, NT, NT, ACT, P, XW>(in, xd, a.dynm, Wl, lane, g, j, r, buf, xc);
+    dyn_mlp.run(in, xd, a.dynm, Wl, lane, g, j, r, buf, xc, none);
     if (valid && r == P - 1 && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
     MSW_MARK(c, 6);
     if (a.np0.h1t == T2)
-      np_project_coop<NT, T2, P>(xs, xd, a.np0, Wl, n, valid, r, lane, g);
+      np_project_coop<NT, T2, P, kEncProjAhead>(xs, xd, a.np0, Wl, n, valid, r, lane, g);
     else
-      np_project_coop<NT, NT, P>(xs, xd, a.np0, Wl, n, valid, r, lane, g);
+      np_project_coop<NT, NT, P, kEncProjAhead>(xs, xd, a.np0, Wl, n, valid, r, lane, g);
   }
   MSW_MARK(c, 8);
   if (a.vu_a[s] >= 0) {
     if (a.vu_h1t == T2)
-      proj_store_part<NT, T2 / P>(xs, Wl + a.vu_a[s], r, a.Vu, n, T2, valid, lane, g);
+      proj_store_part<NT, T2 / P, kEncProjAhead>(xs, Wl + a.vu_a[s], r, a.Vu, n, T2, valid, lane, g);
     else
-      proj_store_part<NT, NT / P>(xs, Wl + a.vu_a[s], r, a.Vu, n, NT, valid, lane, g);
+      proj_store_part<NT, NT / P, kEncProjAhead>(xs, Wl + a.vu_a[s], r, a.Vu, n, NT, valid, lane, g);
   }
   MSW_MARK(c, 9);
 }

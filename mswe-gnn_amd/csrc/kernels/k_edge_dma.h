@@ -27,7 +27,9 @@
 // wait of its own there; the waits below are counted by hand (loads, stores and LDS-DMA retire
 // in issue order on the one vmcnt counter), each assuming the FEWEST operations that can be
 // younger -- a skipped store then only makes a wait stricter, never too weak.
-constexpr int kDmaWaves = 8;  // two waves per SIMD, one workgroup per CU (LDS-bound)
+// Workgroup: eight waves (two per SIMD, one workgroup per CU: LDS-bound; MSW_EH_DMA=1) or four
+// (one per SIMD, the MFMA chains of one wave per SIMD under the DMA; MSW_EH_DMA=2)
+constexpr int kDmaWaves = 8;
 template <int NT>
 struct DmaLayout {  // floats, per wave
   static constexpr int T2 = 2 * NT;
@@ -36,8 +38,8 @@ struct DmaLayout {  // floats, per wave
   static constexpr int WAVE = REC + 2 * 64;
 };
 template <int NT>
-constexpr size_t dma_lds_bytes(int reg_floats) {
-  return eh_lds_bytes(reg_floats) + (size_t)kDmaWaves * DmaLayout<NT>::WAVE * sizeof(float);
+constexpr size_t dma_lds_bytes(int reg_floats, int waves = kDmaWaves) {
+  return eh_lds_bytes(reg_floats) + (size_t)waves * DmaLayout<NT>::WAVE * sizeof(float);
 }
 
 __device__ __forceinline__ void glds16(const float* src, float* lds) {
@@ -123,22 +125,22 @@ __device__ __forceinline__ void gather_bpermute(f32x4 (&agg)[NT], const f32x4 (&
   }
 }
 
-template <int NT, int ACT>
-__global__ __launch_bounds__(64 * kDmaWaves) __attribute__((amdgpu_waves_per_eu(2)))
+template <int NT, int ACT, int WV = kDmaWaves>
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(WV / 4)))
 void k_edge_hop_dma(EdgeHopArgs a) {
 #pragma clang fp contract(off)
   using D = DmaLayout<NT>;
   constexpr int F = 16 * NT, T2 = 2 * NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];  // the ONLY LDS object (see above)
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  const int stride = gridDim.x * kDmaWaves;
+  const int stride = gridDim.x * WV;
   const int last_tile = a.ntiles - 1;
-  int tile = blockIdx.x * kDmaWaves + w;
+  int tile = blockIdx.x * WV + w;
   float* wl = smem + a.dma_off + w * D::WAVE;
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset; drained by the barrier below
-  stage_glds<kDmaWaves>(smem, a.c.W, a.reg, 0, a.reg_nf);  // without the trailing filter copy
+  stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg_nf);  // without the trailing filter copy
   const bool live = tile < a.ntiles;
   if (live) dma_rec<NT>(a, tile, wl, 0, lane);
   __syncthreads();  // vmcnt(0): weights, the filter, the first record

@@ -38,7 +38,8 @@ hipError_t prepare_kernels() {
     if (e != hipSuccess) return e;
   }
   if constexpr (kStaged<NT>) {  // DMA-pipelined grid-stride edge hop: all of its LDS is dynamic
-    for (const void* f : {(const void*)k_edge_hop_dma<NT, 1>, (const void*)k_edge_hop_dma<NT, -1>}) {
+    for (const void* f : {(const void*)k_edge_hop_dma<NT, 1>, (const void*)k_edge_hop_dma<NT, -1>,
+                          (const void*)k_edge_hop_dma<NT, 1, 4>, (const void*)k_edge_hop_dma<NT, -1, 4>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -223,8 +224,10 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
       EdgeHopArgs b = a;
       b.c.xcd = 0;
       void* args[] = {&b};
-      const void* f = a.c.prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>;
-      return hipLaunchKernel(f, dim3(a.max_blocks), dim3(64 * kDmaWaves), args, dma_lds_bytes<NT>(a.reg_nf), st);
+      const int wv = a.dma == 2 ? 4 : kDmaWaves;
+      const void* f = a.dma == 2 ? (a.c.prelu ? (const void*)k_edge_hop_dma<NT, 1, 4> : (const void*)k_edge_hop_dma<NT, -1, 4>)
+                                 : (a.c.prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>);
+      return hipLaunchKernel(f, dim3(a.max_blocks), dim3(64 * wv), args, dma_lds_bytes<NT>(a.reg_nf, wv), st);
     }
   }
   EdgeHopArgs b = a;
@@ -381,6 +384,9 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 17:
       if constexpr (kStaged<NT>) return prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>;
       return nullptr;
+    case 18:
+      if constexpr (kStaged<NT>) return prelu ? (const void*)k_edge_hop_dma<NT, 1, 4> : (const void*)k_edge_hop_dma<NT, -1, 4>;
+      return nullptr;
     default: return nullptr;
   }
 }
@@ -390,10 +396,12 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
   const size_t dyn = kind == 17 ? dma_lds_bytes<NT>((int)(dyn_bytes / 4))
+                     : kind == 18 ? dma_lds_bytes<NT>((int)(dyn_bytes / 4), 4)
                      : (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
                                                      : lds_bytes<NT>((int)(dyn_bytes / 4));
   if (dyn > 160 * 1024) return 0;
   const int block = kind == 17 ? 64 * kDmaWaves
+                    : kind == 18 ? 64 * 4
                     : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
                     : kind == 15 ? 64 * kMlpPipeWaves

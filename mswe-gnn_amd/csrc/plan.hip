@@ -1090,9 +1090,10 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       a.dma_off = 0;
       if (P->kn.eh_dma > 0 && P->NT <= 2 && loop && !a.coop && !a.last && a.Pe && a.h1t == 2 * P->NT &&
           !a.own_zero && a.s && a.out && !a.skip && !a.pool.slots && !a.pool.parent) {
-        const int nb = resident_of(P->NT, 17, a.c.prelu, 0, (size_t)a.reg_nf * 4, 1);
+        // MSW_EH_DMA=2: four waves per workgroup (one per SIMD) instead of eight
+        const int nb = resident_of(P->NT, P->kn.eh_dma == 2 ? 18 : 17, a.c.prelu, 0, (size_t)a.reg_nf * 4, 1);
         if (nb > 0) {
-          a.dma = 1;
+          a.dma = P->kn.eh_dma == 2 ? 2 : 1;
           a.dma_off = (a.reg_nf + kChunk - 1) / kChunk * kChunk;
           a.max_blocks = nb;
         }

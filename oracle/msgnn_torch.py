@@ -41,7 +41,7 @@ NUM_WATER_VARS = 2
 # sides of every discontinuity the reference's arithmetic has (activation kinks, the hop
 # predicate out.sum(1) != 0, the ReLU and _mask_small_WD of the output) and exact arithmetic
 # everywhere else: run in float64 it is the yardstick of that fp32 run's ROUNDING, separated from
-# its branch decisions (tests/test_gpu_train.py, DESIGN §10).
+# its branch decisions (tests/test_gpu_train.py, DESIGN §9).
 _TAPE = None
 
 

@@ -788,14 +788,15 @@ def test_dma_edge_hops_match_grid_stride(cuda, monkeypatch, case):
         g = wet_state(make_multiscale_mesh(n_coarse=60, num_scales=3, T=T), seed=5, all_wet=True).to(cuda)
         m = build_msgnn(3, 32, 4).to(cuda)
     outs, dma = [], []
-    for v in ("0", "1"):
+    for v in ("0", "1", "2"):  # 2: four waves per workgroup (one per SIMD) instead of eight
         monkeypatch.setenv("MSW_EH_DMA", v)
         plan = EnginePlan(m, g, cuda)
         outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
         dma.append(plan.stats()["dma_edge_hops"])
         plan.close()
-    assert dma[0] == 0 and dma[1] >= 1, dma
+    assert dma[0] == 0 and dma[1] >= 1 and dma[2] == dma[1], dma
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
 
 
 def _built_variants():
