@@ -23,6 +23,7 @@ def main():
     agg = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
     dur = defaultdict(dict)
+    seen = defaultdict(lambda: defaultdict(set))  # dispatches that reported each counter (one pass each)
     for d in sys.argv[1:]:
         for r in load(d):
             name = r["Kernel_Name"].replace("msw::", "").split("(")[0].replace("void ", "")
@@ -30,10 +31,11 @@ def main():
             did = (d, r["Dispatch_Id"])
             disp[key].add(did)
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            seen[key][r["Counter_Name"]].add(did)
             dur[key][did] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     for key in sorted(agg, key=lambda k: -sum(dur[k].values())):
         n = len(disp[key])
-        c = {k: v / n for k, v in agg[key].items()}
+        c = {k: v / max(len(seen[key][k]), 1) for k, v in agg[key].items()}
         us = sum(dur[key].values()) / max(len(dur[key]), 1)
         line = f"{key[0]:<32} grid={key[1]:>8} n={n:<5} dur={us:9.2f}us"
         for k in sorted(c):
