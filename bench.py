@@ -513,7 +513,14 @@ def self_launch(n, backend):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
     print(f"bench.py: launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
-    return subprocess.run(cmd).returncode
+    # stdout carries the ONE result line: the ranks' other output (the gloo library prints
+    # connection notes to stdout) goes to stderr
+    with subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1) as p:
+        for line in p.stdout:
+            out = sys.stdout if line.startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
+    return p.returncode
 
 
 def main():

@@ -6,6 +6,7 @@ The reference trains through this layer in training_step (training/train.py:125-
 bar: every parameter and input gradient within 1e-4 relative (max |ours - torch| / max |torch|)
 of torch's fp32 autograd on the same inputs.
 """
+import math
 import pytest
 import torch
 
@@ -449,8 +450,9 @@ def test_hip_training_step_under_autocast_fp16(cuda, sname, R):
     else:
         assert g_hip <= 0.1, (g_hip, g_amp, g_ref)
     # fp16 rounding compounds over the rollout (CPU fp16 autocast measures 1.9e-2 at R=1 and
-    # 9.9e-2 at R=4): a loose sanity bound on the reported torch-AMP figure
-    assert g_amp <= 0.2, g_amp
+    # 9.9e-2 at R=4; torch AMP on the GPU 9.3e-2 … 2.4e-1 run to run): torch's own figure is
+    # reported, not bounded -- it is not code of ours -- beyond being finite
+    assert math.isfinite(g_amp), g_amp
 
 
 def test_autograd_caches_follow_graph_lifetime_and_guards(cuda):
