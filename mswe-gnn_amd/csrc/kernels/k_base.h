@@ -35,9 +35,20 @@ __device__ __forceinline__ int logical_block(const Common& c) {
 __device__ __forceinline__ int wave_row0() { return (blockIdx.x * kWaves + wave_id()) * kRowsPerWave; }
 
 // activation_functions, models/models.py:149-169
+// ACT = 1 (the compile-time PReLU of kernels launched with Common::prelu): max(x, slope x),
+// two VALU ops instead of three (cmp, mul, select).  For slope <= 1, slope != 0 it equals
+// x > 0 ? x : slope x for every x -- infinities and NaN included -- except the sign of a zero
+// output when x = +0 and slope < 0 (+0 instead of -0), which no consumer can see: every PReLU
+// output feeds an MFMA chain or a sum that starts from +0, or a comparison with 0.  The host
+// checks the slopes per plan (plan.hip all_prelu); other slopes run the run-time switch, whose
+// PReLU is ACT = 8 (the reference's form).
+#ifndef MSW_PRELU_MAX
+#define MSW_PRELU_MAX 1  // 0: the reference's form for ACT = 1 too (A/B build variant)
+#endif
 template <int ACT>
 __device__ __forceinline__ float act_static(float x, float slope) {
-  if constexpr (ACT == 1) return x > 0.f ? x : slope * x;       // PReLU
+  if constexpr (ACT == 1) return MSW_PRELU_MAX ? fmaxf(x, slope * x) : (x > 0.f ? x : slope * x);  // PReLU
+  else if constexpr (ACT == 8) return x > 0.f ? x : slope * x;  // PReLU, any slope
   else if constexpr (ACT == 2) return x > 0.f ? x : 0.f;        // ReLU
   else if constexpr (ACT == 3) return x > 0.f ? x : 0.1f * x;   // LeakyReLU(0.1)
   else if constexpr (ACT == 4) return x > 0.f ? x : expm1f(x);  // ELU
@@ -61,7 +72,7 @@ __device__ __forceinline__ void act_tiles(f32x4 (&v)[N], int act, float slope) {
     act_tiles_static<ACT, N>(v, slope);
   } else {
     switch (act) {
-      case 1: act_tiles_static<1, N>(v, slope); break;
+      case 1: act_tiles_static<8, N>(v, slope); break;
       case 2: act_tiles_static<2, N>(v, slope); break;
       case 3: act_tiles_static<3, N>(v, slope); break;
       case 4: act_tiles_static<4, N>(v, slope); break;

@@ -152,37 +152,47 @@ struct EdgeHopRows {  // everything one tile reads from HBM
 };
 // LST = 0: the launch never runs an epilogue (compiled out: fewer live scalars, no SGPR
 // spills into VGPR lanes in the grid-stride loop); LST = 1: a.last decides.
-template <int NT, int LST>
+// FULL: the processors' common shape, known at compile time -- a 2F-wide first layer with an
+// edge term (h1t = 2NT, Pe), own rows read, no skip (edge_full) -- so the run-time flags
+// below cost no per-element selects (a wave-uniform flag in a select is still one VALU op per
+// element).  Same loads and arithmetic where both apply.
+#ifndef MSW_EDGE_FULL
+#define MSW_EDGE_FULL 1  // 0: no FULL specialisation (A/B build variant)
+#endif
+__device__ __forceinline__ bool edge_full(const EdgeHopArgs& a, int nt) {
+  return MSW_EDGE_FULL && a.h1t == 2 * nt && a.Pe && !a.own_zero && !a.skip;
+}
+template <int NT, int LST, bool FULL = false>
 __device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHopArgs& a, const LaneRec& rec,
                                                 int tile, int j, int g) {
   constexpr int F = 16 * NT, T2 = 2 * NT;
   r.L = lanes_of(rec, tile, j, a.n0);
   const Lanes& L = r.L;
-  const int hs = 16 * a.h1t;
+  const int hs = FULL ? 16 * T2 : 16 * a.h1t;
   const float* z = a.c.zrow;
   const float* Ub = a.U + L.sr * hs;
   const float* Vb = a.V + L.n * hs;
-  const float* Pb = a.Pe ? a.Pe + L.p * hs : z;
+  const float* Pb = FULL ? a.Pe + L.p * hs : a.Pe ? a.Pe + L.p * hs : z;
 #pragma unroll
   for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
     const int off = 16 * t + 4 * g;
-    const bool on = t < a.h1t;
+    const bool on = FULL || t < a.h1t;
     r.Us[t] = ld4((on ? Ub : z) + off);
     r.Vn[t] = ld4((on ? Vb : z) + off);
     r.Ps[t] = ld4((on ? Pb : z) + off);
   }
   load_row<NT>(r.os, a.in + L.sr * F, g);
-  load_row<NT>(r.inn, a.own_zero ? z : a.in + L.n * F, g);
-  load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
+  load_row<NT>(r.inn, !FULL && a.own_zero ? z : a.in + L.n * F, g);
+  if constexpr (!FULL) load_row<NT>(r.sk, a.skip ? a.skip + L.n * F : z, g);
   if (LST && a.last) epi_prefetch<NT>(r.pre, a.epi, a.c, a.xs, L.n, g);
 }
-template <int NT, int LST>
+template <int NT, int LST, bool FULL = false>
 __device__ __forceinline__ void edge_hop_load(EdgeHopRows<NT>& r, const EdgeHopArgs& a, int tile, int j, int g) {
-  edge_hop_gather<NT, LST>(r, a, load_rec(a.recs, tile, j), tile, j, g);
+  edge_hop_gather<NT, LST, FULL>(r, a, load_rec(a.recs, tile, j), tile, j, g);
 }
 // Wm: the MLP operands (b1, layers 2..L) -- the staged region; c.W: everything else (the
 // same region for F <= 32, the blob for F = 64, whose epilogue operands do not fit in LDS).
-template <int NT, int ACT, int XS, bool FREG = true>
+template <int NT, int ACT, int XS, bool FREG = true, bool FULL = false>
 __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const EdgeHopArgs& a, const Common& c,
                                               const float* Wm, const f32x4 (&wf)[NT][NT], float* slab, int j,
                                               int lane, int g, f32x4 (&res_out)[NT]) {
@@ -204,12 +214,16 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
   for (int t = 0; t < T2; ++t) {
     const int off = 16 * t + 4 * g;
     vr[t] = ld4(dr + off);
-    br[t] = ld4(Wm + b1 + off);
+    if constexpr (!FULL) br[t] = ld4(Wm + b1 + off);
   }
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
-    const f32x4 p = a.Pe ? r.Ps[t] : br[t];
-    H[t] = (t < a.h1t) ? (r.Us[t] + vr[t]) + p : zero4();
+    if constexpr (FULL) {
+      H[t] = (r.Us[t] + vr[t]) + r.Ps[t];
+    } else {
+      const f32x4 p = a.Pe ? r.Ps[t] : br[t];
+      H[t] = (t < a.h1t) ? (r.Us[t] + vr[t]) + p : zero4();
+    }
   }
   load_row<NT>(od, dr + 16 * T2, g);
   MSW_MARK(c, 4);
@@ -250,9 +264,11 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
   else  // filter operand in the staged LDS region (fewer live registers in the loop)
     apply_filter<NT>(res, agg, a.filt_l, c.W, lane);
   MSW_MARK(c, 8);
-  if (a.skip) {
+  if constexpr (!FULL) {
+    if (a.skip) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) res[t] = res[t] + r.sk[t];
+      for (int t = 0; t < NT; ++t) res[t] = res[t] + r.sk[t];
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) res_out[t] = res[t];
@@ -330,20 +346,29 @@ void k_edge_hop(EdgeHopArgs a) {
       __syncthreads();
       Wm = smem;
     }
-    auto walk = [&](const float* Wl) __attribute__((always_inline)) {
+    auto walk = [&](const float* Wl, auto full) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(full)::value;
       for (; tile < a.ntiles; tile += stride) {
         const int ln = opaque_lane(), gg = ln >> 4, jj = ln & 15;
         EdgeHopRows<NT> q;
-        edge_hop_load<NT, LST>(q, a, tile, jj, gg);
+        edge_hop_load<NT, LST, FULL>(q, a, tile, jj, gg);
         f32x4 res[NT];
-        edge_hop_core<NT, ACT, XS, !kStaged<NT>>(q, a, c, Wl, wf, &slab[w][0][0], jj, ln, gg, res);
+        edge_hop_core<NT, ACT, XS, !kStaged<NT>, FULL>(q, a, c, Wl, wf, &slab[w][0][0], jj, ln, gg, res);
         edge_hop_finish<NT, ACT, LST>(res, q, a, c, ln, gg);
       }
     };
-    if (!kStaged<NT> && a.reg.len > 0)
-      walk((const float*)smem);  // F = 64: provably LDS (see above)
-    else
-      walk(Wm);
+    // the processors' first hops (config 5's finest launches) take the FULL loop
+    const bool full = edge_full(a, NT);
+    if (!kStaged<NT> && a.reg.len > 0) {  // F = 64: provably LDS (see above)
+      if (full)
+        walk((const float*)smem, std::true_type{});
+      else
+        walk((const float*)smem, std::false_type{});
+    } else if (full) {
+      walk(Wm, std::true_type{});
+    } else {
+      walk(Wm, std::false_type{});
+    }
   }
   MSW_MARK(c, 9);
 }

@@ -18,6 +18,8 @@
 //    edge-MLP+hop-1, hops 2..K (the last with an epilogue: next projection / unpool
 //    projection / decoder + rollout update) -> pooling+projection / unpooling+projection.
 #pragma once
+#include <type_traits>
+
 #include "engine.h"
 
 namespace msw {

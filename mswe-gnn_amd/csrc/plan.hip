@@ -108,9 +108,13 @@ int pack_mlp(Blob& B, const msw_mlp& m, MlpDev& d) {
   return MSW_OK;
 }
 
+// every activation of the MLP is a PReLU with slope <= 1, slope != 0: the compile-time PReLU
+// kernels (kernels/k_base.h act_static<1>: max(x, slope x)); otherwise the run-time switch
 int all_prelu(const msw_mlp& m) {
-  for (int i = 0; i < m.n_layers; ++i)
-    if (m.layer[i].act != MSW_ACT_PRELU) return 0;
+  for (int i = 0; i < m.n_layers; ++i) {
+    const float s = m.layer[i].act_param;
+    if (m.layer[i].act != MSW_ACT_PRELU || !(s <= 1.f && s != 0.f)) return 0;
+  }
   return 1;
 }
 
