@@ -404,6 +404,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   constexpr int G = kWaves / P;                  // tile groups per workgroup
   __shared__ __attribute__((aligned(16))) float slab_all[kWaves][kRowsPerWave][XS];
   __shared__ __attribute__((aligned(16))) float xbuf[G][2][kRowsPerWave][XW];
+  __shared__ __attribute__((aligned(16))) float pbuf[FUSE ? G : 1][kRowsPerWave][XS];  // FUSE != 0
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
   const int grp = w / P, r = w % P;
@@ -415,135 +416,152 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
-  EdgeHopRows<NT> q;
-  [[maybe_unused]] PoolIn<NT> pin;
-  [[maybe_unused]] UnpoolIn<NT> uin;
-  if constexpr (FUSE == 1)
-    edge_pool_load<NT, LST>(q, pin, a, live ? tile : 0, j, g, r);
-  else if constexpr (FUSE == 2)
-    edge_unpool_load<NT, LST>(q, uin, a, live ? tile : 0, j, g, r);
-  else
-    edge_hop_load<NT, LST>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
-  const bool split = a.reg.split < a.reg_nf;
-  stage_glds<kWaves>(smem, a.c.W, a.reg, 0, a.reg.split);
-  __syncthreads();
-  c.W = smem;
-  if (split) stage_glds<kWaves>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
-  if constexpr (FUSE != 0) {
-    static_assert(P == 2, "fused pooling / unpooling: a source rank and a destination rank");
-    __shared__ __attribute__((aligned(16))) float pbuf[G][kRowsPerWave][XS];
-    f32x4 xp[NT];
+  // FULL (FUSE = 0 only): the processors' common shape, see k_edge.h edge_full
+  auto body = [&](auto full) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(full)::value;
+    EdgeHopRows<NT> q;
+    [[maybe_unused]] PoolIn<NT> pin;
+    [[maybe_unused]] UnpoolIn<NT> uin;
     if constexpr (FUSE == 1)
-      pool_mean<NT>(xp, pin, a, g);
+      edge_pool_load<NT, LST>(q, pin, a, live ? tile : 0, j, g, r);
+    else if constexpr (FUSE == 2)
+      edge_unpool_load<NT, LST>(q, uin, a, live ? tile : 0, j, g, r);
     else
-      unpool_row<NT>(xp, uin, a, c.W, lane, g);
-    side_project_exchange<NT, XS>(q, xp, FUSE == 1 ? pin.xs : uin.xs, a.pool.np, c.W, lane, g, j, r,
-                                  &pbuf[grp][0][0], &slab_all[grp * P][0][0], &slab_all[grp * P + 1][0][0]);
-  }
-  float* slab = &slab_all[w][0][0];
-  float* b0 = &xbuf[grp][0][0][0];
-  float* b1p = &xbuf[grp][1][0][0];
-  const Lanes& L = q.L;
-  // ---- as edge_hop_core up to the MLP (every rank)
-  float* my = slab + j * XS;
-  if constexpr (FUSE == 0) {  // fused (un)pooling: the destination rank stored them (barrier above)
-    store_row<T2>(my, q.Vn, T2, g);
-    store_row<NT>(my + 16 * T2, q.inn, NT, g);
-    wave_lds_sync();
-  }
-  const float* dr = slab + L.dl * XS;
-  f32x4 H[T2], od[NT];
-  const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
-  f32x4 vr[T2], br[T2];
-#pragma unroll
-  for (int t = 0; t < T2; ++t) {
-    const int off = 16 * t + 4 * g;
-    vr[t] = ld4(dr + off);
-    br[t] = ld4(c.W + b1 + off);
-  }
-#pragma unroll
-  for (int t = 0; t < T2; ++t) {
-    const f32x4 p = a.Pe ? q.Ps[t] : br[t];
-    H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
-  }
-  load_row<NT>(od, dr + 16 * T2, g);
-  act_tiles<ACT, T2>(H, a.act1, a.slope1);
-  f32x4 sv[NT];
-  if (a.rest.n > 0) {
-    coop_run_mlp<T2, T2, NT, ACT, P>(H, sv, a.rest, c.W, lane, g, j, r, b0, b1p, XW);
-  } else {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) sv[t] = H[t];
-  }
-  if (a.normalize) {
-    float ss = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-    const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      f32x4 v = sv[t] / nrm;
-      v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
-      v.y = (v.y == v.y) ? v.y : 0.f;
-      v.z = (v.z == v.z) ? v.z : 0.f;
-      v.w = (v.w == v.w) ? v.w : 0.f;
-      sv[t] = v;
+      edge_hop_load<NT, LST, FULL>(q, a, live ? tile : 0, j, g);  // dead groups compute tile 0, store nothing
+    const bool split = a.reg.split < a.reg_nf;
+    stage_glds<kWaves>(smem, a.c.W, a.reg, 0, a.reg.split);
+    __syncthreads();
+    c.W = smem;
+    if (split) stage_glds<kWaves>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
+    if constexpr (FUSE != 0) {
+      static_assert(P == 2, "fused pooling / unpooling: a source rank and a destination rank");
+      f32x4 xp[NT];
+      if constexpr (FUSE == 1)
+        pool_mean<NT>(xp, pin, a, g);
+      else
+        unpool_row<NT>(xp, uin, a, c.W, lane, g);
+      side_project_exchange<NT, XS>(q, xp, FUSE == 1 ? pin.xs : uin.xs, a.pool.np, c.W, lane, g, j, r,
+                                    &pbuf[grp][0][0], &slab_all[grp * P][0][0], &slab_all[grp * P + 1][0][0]);
     }
-  }
-  if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
-  put_message<NT>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
-  f32x4 agg[NT];
-  gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
-  // ---- filter on this rank's output tiles, + skip, exchanged into the full row
-  constexpr int TS = NT / P;
-  f32x4 rs[TS];
+    float* slab = &slab_all[w][0][0];
+    float* b0 = &xbuf[grp][0][0][0];
+    float* b1p = &xbuf[grp][1][0][0];
+    const Lanes& L = q.L;
+    // ---- as edge_hop_core up to the MLP (every rank)
+    float* my = slab + j * XS;
+    if constexpr (FUSE == 0) {  // fused (un)pooling: the destination rank stored them (barrier above)
+      store_row<T2>(my, q.Vn, T2, g);
+      store_row<NT>(my + 16 * T2, q.inn, NT, g);
+      wave_lds_sync();
+    }
+    const float* dr = slab + L.dl * XS;
+    f32x4 H[T2], od[NT];
+    const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+    f32x4 vr[T2], br[T2];
 #pragma unroll
-  for (int t = 0; t < TS; ++t) rs[t] = pick<NT, TS>(q.inn, r, t);
-  if (a.filt_a >= 0) {
-    f32x4 wr[TS][NT];  // this rank's filter rows, selected with compile-time indices
+    for (int t = 0; t < T2; ++t) {
+      const int off = 16 * t + 4 * g;
+      vr[t] = ld4(dr + off);
+      if constexpr (!FULL) br[t] = ld4(c.W + b1 + off);
+    }
 #pragma unroll
-    for (int to = 0; to < TS; ++to)
-#pragma unroll
-      for (int ti = 0; ti < NT; ++ti) {
-        f32x4 v = wf[to][ti];
-#pragma unroll
-        for (int k = 1; k < P; ++k) v = (r == k) ? wf[k * TS + to][ti] : v;
-        wr[to][ti] = v;
+    for (int t = 0; t < T2; ++t) {
+      if constexpr (FULL) {
+        H[t] = (q.Us[t] + vr[t]) + q.Ps[t];
+      } else {
+        const f32x4 p = a.Pe ? q.Ps[t] : br[t];
+        H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
       }
-    f32x4 acc[TS];
+    }
+    load_row<NT>(od, dr + 16 * T2, g);
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      coop_run_mlp<T2, T2, NT, ACT, P>(H, sv, a.rest, c.W, lane, g, j, r, b0, b1p, XW);
+    } else {
 #pragma unroll
-    for (int to = 0; to < TS; ++to) acc[to] = zero4();
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
 #pragma unroll
-    for (int ti = 0; ti < NT; ++ti)
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
+      for (int t = 0; t < NT; ++t) {
+        f32x4 v = sv[t] / nrm;
+        v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
+        v.y = (v.y == v.y) ? v.y : 0.f;
+        v.z = (v.z == v.z) ? v.z : 0.f;
+        v.w = (v.w == v.w) ? v.w : 0.f;
+        sv[t] = v;
+      }
+    }
+    if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
+    put_message<NT, FULL ? 1 : -1>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
+    f32x4 agg[NT];
+    gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
+    // ---- filter on this rank's output tiles, + skip, exchanged into the full row
+    constexpr int TS = NT / P;
+    f32x4 rs[TS];
 #pragma unroll
-        for (int to = 0; to < TS; ++to) acc[to] = MSW_MFMA(wr[to][ti][rr], agg[ti][rr], acc[to]);
+    for (int t = 0; t < TS; ++t) rs[t] = pick<NT, TS>(q.inn, r, t);
+    if (a.filt_a >= 0) {
+      f32x4 wr[TS][NT];  // this rank's filter rows, selected with compile-time indices
 #pragma unroll
-    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
-  } else {
+      for (int to = 0; to < TS; ++to)
 #pragma unroll
-    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + pick<NT, TS>(agg, r, t);
-  }
-  if (a.skip) {
+        for (int ti = 0; ti < NT; ++ti) {
+          f32x4 v = wf[to][ti];
 #pragma unroll
-    for (int t = 0; t < TS; ++t) rs[t] = rs[t] + pick<NT, TS>(q.sk, r, t);
-  }
-  f32x4 res[NT];
-  // the buffer the MLP's last exchange did not use (its readers may still be reading that one)
-  coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? b1p : b0, XW, r, j, g);
-  if (split) __syncthreads();  // every wave: the epilogue operands have landed
-  // ---- finish: store, or the epilogue (projections split over the ranks)
-  if (LST && a.last) {
-    const Epilogue& e = a.epi;
-    if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
-    if (live && r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
-    if (e.np.h1t == T2)
-      np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, live && L.nv, r, lane, g);
+          for (int k = 1; k < P; ++k) v = (r == k) ? wf[k * TS + to][ti] : v;
+          wr[to][ti] = v;
+        }
+      f32x4 acc[TS];
+#pragma unroll
+      for (int to = 0; to < TS; ++to) acc[to] = zero4();
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+          for (int to = 0; to < TS; ++to) acc[to] = MSW_MFMA(wr[to][ti][rr], agg[ti][rr], acc[to]);
+#pragma unroll
+      for (int t = 0; t < TS; ++t) rs[t] = rs[t] + acc[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < TS; ++t) rs[t] = rs[t] + pick<NT, TS>(agg, r, t);
+    }
+    if constexpr (!FULL) {
+      if (a.skip) {
+#pragma unroll
+        for (int t = 0; t < TS; ++t) rs[t] = rs[t] + pick<NT, TS>(q.sk, r, t);
+      }
+    }
+    f32x4 res[NT];
+    // the buffer the MLP's last exchange did not use (its readers may still be reading that one)
+    coop_exchange<NT, P>(rs, res, (a.rest.n & 1) ? b1p : b0, XW, r, j, g);
+    if (split) __syncthreads();  // every wave: the epilogue operands have landed
+    // ---- finish: store, or the epilogue (projections split over the ranks)
+    if (LST && a.last) {
+      const Epilogue& e = a.epi;
+      if (e.post_act) act_tiles<-1, NT>(res, e.post_act, e.post_slope);
+      if (live && r == 0 && a.out && L.nv) store_row<NT>(a.out + L.n * F, res, NT, g);
+      if (e.np.h1t == T2)
+        np_project_coop<NT, T2, P>(q.pre.xs, res, e.np, c.W, L.n, live && L.nv, r, lane, g);
+      else
+        np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, live && L.nv, r, lane, g);
+    } else if (live && r == 0 && L.nv && a.out) {
+      store_row<NT>(a.out + L.n * F, res, NT, g);
+    }
+  };
+  if constexpr (FUSE == 0) {
+    if (edge_full(a, NT))
+      body(std::true_type{});
     else
-      np_project_coop<NT, NT, P>(q.pre.xs, res, e.np, c.W, L.n, live && L.nv, r, lane, g);
-  } else if (live && r == 0 && L.nv && a.out) {
-    store_row<NT>(a.out + L.n * F, res, NT, g);
+      body(std::false_type{});
+  } else {
+    body(std::false_type{});
   }
 }
 
@@ -616,11 +634,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma unroll
       for (int ti = 0; ti < NT; ++ti) wr[t][ti] = ld4(c.W + fa + ((size_t)((r * TS + t) * NT + ti) * 64 + lane) * 4);
   }
+  // FULL (FUSE = 0 only): the processors' common shape, see k_edge.h edge_full
+  const bool full = FUSE == 0 && edge_full(a, NT);
   EdgeHopRows<NT> q;
   [[maybe_unused]] PoolIn<NT> pin;
   [[maybe_unused]] const int side = r >= P / 2;  // fused pooling: 0 source side, 1 destination side
   if constexpr (FUSE == 1)
     edge_pool_load<NT, LST>(q, pin, a, tile, j, g, side);
+  else if (full)
+    edge_hop_load<NT, LST, true>(q, a, tile, j, g);
   else
     edge_hop_load<NT, LST>(q, a, tile, j, g);
   const Lanes& L = q.L;
@@ -628,7 +650,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   if (a.reg.len > 0 && !a.wdirect) stage_glds<kWaves>(smem, c.W, a.reg, 0, a.reg.len);
   // the MLP operands through a pointer the compiler can prove to be LDS when staged (the
   // run-time LDS-or-blob choice made every weight read a FLAT load, which also waits on vmcnt)
-  auto rest = [&](const float* Wm) __attribute__((always_inline)) {
+  auto rest = [&](const float* Wm, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
     float* my = &slab[j][0];
     if constexpr (FUSE != 0) {
       // source side -> exchange rows (in xbuf, free until the MLP), destination side -> the
@@ -661,12 +684,16 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
     for (int t = 0; t < T2; ++t) {
       const int off = 16 * t + 4 * g;
       vr[t] = ld4(dr + off);
-      br[t] = ld4(Wm + b1 + off);
+      if constexpr (!FULL) br[t] = ld4(Wm + b1 + off);
     }
 #pragma unroll
     for (int t = 0; t < T2; ++t) {
-      const f32x4 p = a.Pe ? q.Ps[t] : br[t];
-      H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
+      if constexpr (FULL) {
+        H[t] = (q.Us[t] + vr[t]) + q.Ps[t];
+      } else {
+        const f32x4 p = a.Pe ? q.Ps[t] : br[t];
+        H[t] = (t < a.h1t) ? (q.Us[t] + vr[t]) + p : zero4();
+      }
     }
     load_row<NT>(od, dr + 16 * T2, g);
     act_tiles<ACT, T2>(H, a.act1, a.slope1);
@@ -696,7 +723,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
     // every rank has read the slab's node rows before the first MLP exchange barrier: rank 0
     // may overwrite them with the messages (a.rest.n == 0 has no barrier: add one)
     if (a.rest.n == 0) __syncthreads();
-    if (r == 0) put_message<NT>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
+    if (r == 0) put_message<NT, FULL ? 1 : -1>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
     __syncthreads();
     f32x4 agg[NT];
     gather_messages<NT, XS>(agg, &slab[0][0], L.q0, L.q1, g);
@@ -725,7 +752,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
         rs[t] = rs[t] + ag;
       }
     }
-    if (a.skip) {
+    if (!FULL && a.skip) {
 #pragma unroll
       for (int t = 0; t < TS; ++t) rs[t] = rs[t] + ld4(a.skip + L.n * F + 16 * (r * TS + t) + 4 * g);
     }
@@ -745,14 +772,20 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
   };
   // (four ranks per tile only: the two-rank kernels' register count grew past two workgroups
   // per CU with it, 176 -> 256 VGPRs, and the finest unpooling lost its one-round grid)
-  if constexpr (P == 4) {
-    if (a.reg.len > 0 && !a.wdirect)
-      rest((const float*)smem);
-    else
-      rest(a.reg.len > 0 ? c.W + a.reg.off : c.W);
-  } else {
-    rest(a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W);
-  }
+  auto run = [&](auto fullc) __attribute__((always_inline)) {
+    if constexpr (P == 4) {
+      if (a.reg.len > 0 && !a.wdirect)
+        rest((const float*)smem, fullc);
+      else
+        rest(a.reg.len > 0 ? c.W + a.reg.off : c.W, fullc);
+    } else {
+      rest(a.reg.len > 0 ? (a.wdirect ? c.W + a.reg.off : (const float*)smem) : c.W, fullc);
+    }
+  };
+  if (full)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 }
 
 template <int NT>

@@ -34,10 +34,13 @@ __device__ __forceinline__ LaneRec load_rec(const LaneRec* recs, int tile, int j
 }
 
 // msg_e = active(e) * (out[col] - out[row]) * s_e  (or s_e * out[row])   (gnn.py:406-435)
-template <int NT>
+// GM = 1: gradient messages without upwind known at compile time (the flags then cost no
+// per-element selects); GM = -1: the run-time flags
+template <int NT, int GM = -1>
 __device__ __forceinline__ void put_message(float* slab_row, const f32x4 (&os)[NT], const f32x4 (&od)[NT],
-                                            const f32x4 (&sv)[NT], bool ev, int grad, int upwind, int g) {
+                                            const f32x4 (&sv)[NT], bool ev, int grad_rt, int upwind_rt, int g) {
 #pragma clang fp contract(off)
+  const int grad = GM == 1 ? 1 : grad_rt, upwind = GM == 1 ? 0 : upwind_rt;
   float rs = 0.f, rd = 0.f;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -153,14 +156,14 @@ struct EdgeHopRows {  // everything one tile reads from HBM
 // LST = 0: the launch never runs an epilogue (compiled out: fewer live scalars, no SGPR
 // spills into VGPR lanes in the grid-stride loop); LST = 1: a.last decides.
 // FULL: the processors' common shape, known at compile time -- a 2F-wide first layer with an
-// edge term (h1t = 2NT, Pe), own rows read, no skip (edge_full) -- so the run-time flags
-// below cost no per-element selects (a wave-uniform flag in a select is still one VALU op per
-// element).  Same loads and arithmetic where both apply.
+// edge term (h1t = 2NT, Pe), own rows read, no skip, gradient messages without upwind
+// (edge_full) -- so the run-time flags below cost no per-element selects (a wave-uniform flag
+// in a select is still one VALU op per element).  Same loads and arithmetic where both apply.
 #ifndef MSW_EDGE_FULL
 #define MSW_EDGE_FULL 1  // 0: no FULL specialisation (A/B build variant)
 #endif
 __device__ __forceinline__ bool edge_full(const EdgeHopArgs& a, int nt) {
-  return MSW_EDGE_FULL && a.h1t == 2 * nt && a.Pe && !a.own_zero && !a.skip;
+  return MSW_EDGE_FULL && a.h1t == 2 * nt && a.Pe && !a.own_zero && !a.skip && a.grad && !a.upwind;
 }
 template <int NT, int LST, bool FULL = false>
 __device__ __forceinline__ void edge_hop_gather(EdgeHopRows<NT>& r, const EdgeHopArgs& a, const LaneRec& rec,
@@ -252,7 +255,7 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
     }
   }
   if (a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);  // padding slots too: never read
-  put_message<NT>(my, r.os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
+  put_message<NT, FULL ? 1 : -1>(my, r.os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
   MSW_MARK(c, 6);
   f32x4 agg[NT], res[NT];
   gather_messages<NT, XS>(agg, slab, L.q0, L.q1, g);
@@ -304,36 +307,44 @@ void k_edge_hop(EdgeHopArgs a) {
   if constexpr (!LOOP || !kStaged<NT>)
     load_filter<NT>(wf, a.c.W, a.filt_a, lane);  // blob offset (not part of the LDS region)
   if constexpr (!LOOP) {
-    const bool live = tile < a.ntiles;
-    EdgeHopRows<NT> r;
-    edge_hop_load<NT, LST>(r, a, live ? tile : 0, j, g);  // idle waves stay in bounds
-    MSW_MARK(c, 1);
-    // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
-    // stream into LDS behind the MLP and are waited for at the epilogue barrier
-    const bool split = kStaged<NT> && a.reg.split < a.reg_nf;
-    const float* Wm = c.W;
-    if constexpr (kStaged<NT>) {
-      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.split);
-      __syncthreads();
-      c.W = smem;
-      Wm = smem;
-      if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
-    } else if (a.reg.len > 0) {  // F = 64: the MLP region alone (plan.hip relocate)
-      stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
-      __syncthreads();
-      Wm = smem;
-    }
-    MSW_MARK(c, 2);
-    f32x4 res[NT];
-    // F = 64: the MLP operands through a pointer the compiler can prove to be LDS (the run-time
-    // LDS-or-blob choice made every weight read a FLAT load, which also waits on vmcnt)
-    if (!kStaged<NT> && a.reg.len > 0) {
-      if (live) edge_hop_core<NT, ACT, XS>(r, a, c, (const float*)smem, wf, &slab[w][0][0], j, lane, g, res);
-    } else if (live) {
-      edge_hop_core<NT, ACT, XS>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
-    }
-    if (split) __syncthreads();  // every wave: the epilogue operands have landed
-    if (live) edge_hop_finish<NT, ACT, LST>(res, r, a, c, lane, g);
+    // one tile per wave; FULL: see edge_full
+    auto body = [&](auto full) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(full)::value;
+      const bool live = tile < a.ntiles;
+      EdgeHopRows<NT> r;
+      edge_hop_load<NT, LST, FULL>(r, a, live ? tile : 0, j, g);  // idle waves stay in bounds
+      MSW_MARK(c, 1);
+      // weights the MLP needs now; the epilogue's operands (unpool / K = 1 projections)
+      // stream into LDS behind the MLP and are waited for at the epilogue barrier
+      const bool split = kStaged<NT> && a.reg.split < a.reg_nf;
+      const float* Wm = c.W;
+      if constexpr (kStaged<NT>) {
+        stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.split);
+        __syncthreads();
+        c.W = smem;
+        Wm = smem;
+        if (split) stage_glds<WV>(smem, a.c.W, a.reg, chunk_ceil(a.reg.split), a.reg_nf);
+      } else if (a.reg.len > 0) {  // F = 64: the MLP region alone (plan.hip relocate)
+        stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
+        __syncthreads();
+        Wm = smem;
+      }
+      MSW_MARK(c, 2);
+      f32x4 res[NT];
+      // F = 64: the MLP operands through a pointer the compiler can prove to be LDS (the run-time
+      // LDS-or-blob choice made every weight read a FLAT load, which also waits on vmcnt)
+      if (!kStaged<NT> && a.reg.len > 0) {
+        if (live) edge_hop_core<NT, ACT, XS, true, FULL>(r, a, c, (const float*)smem, wf, &slab[w][0][0], j, lane, g, res);
+      } else if (live) {
+        edge_hop_core<NT, ACT, XS, true, FULL>(r, a, c, Wm, wf, &slab[w][0][0], j, lane, g, res);
+      }
+      if (split) __syncthreads();  // every wave: the epilogue operands have landed
+      if (live) edge_hop_finish<NT, ACT, LST>(res, r, a, c, lane, g);
+    };
+    if (edge_full(a, NT))
+      body(std::true_type{});
+    else
+      body(std::false_type{});
   } else {
     const float* Wm = c.W;
     if constexpr (kStaged<NT>) {
@@ -394,8 +405,11 @@ void k_edge_mlp(EdgeHopArgs a) {
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   // the MLP operands through a pointer the compiler can prove to be LDS (a run-time choice
   // between LDS and the blob made every weight read a FLAT load, which also waits on vmcnt)
-  auto run = [&](const float* Wm) __attribute__((always_inline)) {
-    const int hs = 16 * a.h1t;
+  // FULL: a 2F-wide first layer with an edge term (k_edge_hop's edge_full): no per-element
+  // selects on the run-time shape flags
+  auto run = [&](const float* Wm, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    const int hs = FULL ? 16 * T2 : 16 * a.h1t;
     const float* z = a.c.zrow;
     const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
     for (int ch = blockIdx.x * kMlpWaves + w; ch < a.nchunks; ch += stride) {
@@ -404,17 +418,21 @@ void k_edge_mlp(EdgeHopArgs a) {
       const bool ev = e.z >= 0;
       const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
       const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
-      const float* Pb = a.Pe && ev ? a.Pe + (size_t)e.z * hs : z;
+      const float* Pb = (FULL || a.Pe) && ev ? a.Pe + (size_t)e.z * hs : z;
       f32x4 H[T2];
 #pragma unroll
       for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
         const int off = 16 * t + 4 * g;
-        const bool on = t < a.h1t;
-        const f32x4 u = ld4((on ? Ub : z) + off);
-        const f32x4 v = ld4((on ? Vb : z) + off);
-        const f32x4 pe = ld4((on ? Pb : z) + off);
-        const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
-        H[t] = on ? (u + v) + p : zero4();
+        if constexpr (FULL) {
+          H[t] = (ld4(Ub + off) + ld4(Vb + off)) + ld4(Pb + off);
+        } else {
+          const bool on = t < a.h1t;
+          const f32x4 u = ld4((on ? Ub : z) + off);
+          const f32x4 v = ld4((on ? Vb : z) + off);
+          const f32x4 pe = ld4((on ? Pb : z) + off);
+          const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
+          H[t] = on ? (u + v) + p : zero4();
+        }
       }
       act_tiles<ACT, T2>(H, a.act1, a.slope1);
       f32x4 sv[NT];
@@ -446,10 +464,17 @@ void k_edge_mlp(EdgeHopArgs a) {
     stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
   }
-  if (a.reg.len > 0)
-    run(smem);
-  else
-    run(a.c.W);
+  const bool full = MSW_EDGE_FULL && a.h1t == T2 && a.Pe;
+  if (a.reg.len > 0) {
+    if (full)
+      run(smem, std::true_type{});
+    else
+      run(smem, std::false_type{});
+  } else if (full) {
+    run(a.c.W, std::true_type{});
+  } else {
+    run(a.c.W, std::false_type{});
+  }
 }
 
 // k_edge_mlp software-pipelined (F = 64, MSW_MLP_PIPE): one wave per SIMD, each wave walks
