@@ -59,10 +59,19 @@ __device__ __forceinline__ float act_static(float x, float slope) {
 }
 template <int ACT, int N>
 __device__ __forceinline__ void act_tiles_static(f32x4 (&v)[N], float slope) {
+  if constexpr (ACT == 1 && MSW_PRELU_MAX) {  // the products as packed pairs (v_pk_mul_f32)
 #pragma unroll
-  for (int t = 0; t < N; ++t)
+    for (int t = 0; t < N; ++t) {
+      const f32x4 m = v[t] * slope;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[t][r] = act_static<ACT>(v[t][r], slope);
+      for (int r = 0; r < 4; ++r) v[t][r] = fmaxf(v[t][r], m[r]);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[t][r] = act_static<ACT>(v[t][r], slope);
+  }
 }
 // ACT >= 0: activation fixed at compile time (PReLU kernels of the shipped configs);
 // ACT < 0: one wave-uniform switch outside the element loops.
