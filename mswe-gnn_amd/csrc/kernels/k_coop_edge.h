@@ -416,7 +416,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
   f32x4 wf[NT][NT];
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
-  // FULL (FUSE = 0 only): the processors' common shape, see k_edge.h edge_full
+  // FULL: the processors' common shape, see k_edge.h edge_full (with fused (un)pooling: the
+  // processor's part -- the fused loads fill the same rows)
   auto body = [&](auto full) __attribute__((always_inline)) {
     constexpr bool FULL = decltype(full)::value;
     EdgeHopRows<NT> q;
@@ -555,14 +556,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
       store_row<NT>(a.out + L.n * F, res, NT, g);
     }
   };
-  if constexpr (FUSE == 0) {
-    if (edge_full(a, NT))
-      body(std::true_type{});
-    else
-      body(std::false_type{});
-  } else {
+  if (edge_full(a, NT))
+    body(std::true_type{});
+  else
     body(std::false_type{});
-  }
 }
 
 // Fused pooling on k_edge_coop4 (F = 64): ranks [0, P/2) form the source side, [P/2, P) the
@@ -634,8 +631,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma unroll
       for (int ti = 0; ti < NT; ++ti) wr[t][ti] = ld4(c.W + fa + ((size_t)((r * TS + t) * NT + ti) * 64 + lane) * 4);
   }
-  // FULL (FUSE = 0 only): the processors' common shape, see k_edge.h edge_full
-  const bool full = FUSE == 0 && edge_full(a, NT);
+  // FULL: the processors' common shape, see k_edge.h edge_full (with fused pooling: the
+  // processor's part -- the fused load fills the same rows)
+  const bool full = edge_full(a, NT);
   EdgeHopRows<NT> q;
   [[maybe_unused]] PoolIn<NT> pin;
   [[maybe_unused]] const int side = r >= P / 2;  // fused pooling: 0 source side, 1 destination side
