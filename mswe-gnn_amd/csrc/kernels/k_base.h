@@ -235,19 +235,34 @@ struct EpiPre {
   float xd[kMaxDyn];  // X[row, nstat : nnf] (lane group 0 uses it)
   int ext, step;
   int bc;             // the row's BC slot (rollout mode), -1 = none
-  float bcv[kMaxDyn / 2];  // deferred decoder: the row's BC values of step + 1 (bc_prefetch)
+  float bcv[kMaxDyn / 2];  // deferred decoder: the row's BC values of step + 1 (bc_prefetch) ...
+  float bck[kMaxDyn];      // ... or (BYCOL) the value for each state column it overwrites
 };
 // Deferred decoder (k_encode): the BC values the state update writes, loaded with the tile's
 // other inputs instead of after the decoder chain (a BC row's wave would otherwise wait for
 // one more global load on the launch's critical path).
-template <int NT>
+// BYCOL: one load per state column (bck) instead of one per BC value (bcv): the state update
+// then reads bck[k] at a compile-time index instead of selecting bcv[(k - c0) / 2] for every
+// column (kMaxDyn x kMaxDyn / 2 selects), at the cost of kMaxDyn / 2 more live registers (the
+// four-rank F = 64 encoder, at its 128-register cap, keeps bcv)
+template <int NT, bool BYCOL = false>
 __device__ __forceinline__ void bc_prefetch(EpiPre<NT>& p, const DecDesc& d, const Common& c) {
   const RolloutIO* io = d.io;
   const bool on = p.bc >= 0 && p.step + 1 < io->bc_tstride;
   const float* bp = on ? io->bc + (size_t)p.bc * c.p * io->bc_tstride + p.step + 1 : c.zrow;
   const int ts = on ? io->bc_tstride : 0;
+  if constexpr (BYCOL) {  // wave-uniform column -> BC index map; other columns load bp[0], unused
+    const int c0 = io->type_bc - 1;
 #pragma unroll
-  for (int u = 0; u < kMaxDyn / 2; ++u) p.bcv[u] = u < c.p ? bp[u * ts] : 0.f;
+    for (int k = 0; k < kMaxDyn; ++k) {
+      const int u = (k - c0) >> 1;
+      const bool col = k >= c0 && ((k - c0) & 1) == 0 && u < c.p;
+      p.bck[k] = bp[col ? u * ts : 0];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kMaxDyn / 2; ++u) p.bcv[u] = u < c.p ? bp[u * ts] : 0.f;
+  }
 }
 template <int NT>
 __device__ __forceinline__ void epi_prefetch(EpiPre<NT>& p, const Epilogue& e, const Common& c,
@@ -336,11 +351,11 @@ __device__ __forceinline__ void decode_tail(const f32x4 (&o)[1], const DecDesc& 
 // same operations in the same order) and state update.  Every lane of a row ends with the
 // row's new dynamic columns in nd (window shifted, prediction appended, BC of step t + 1);
 // lane group 0 writes the rollout output and the state row.  W: the decoder operands.
-template <int NT>
+template <int NT, bool BYCOL = false>
 __device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const DecDesc& d, const Common& c,
                                                   const float* W, const EpiPre<NT>& pre, int n, bool valid,
                                                   int lane, int g, float (&nd)[kMaxDyn]);
-template <int NT, int ACT>
+template <int NT, int ACT, bool BYCOL = false>
 __device__ __forceinline__ void decode_state(const f32x4 (&x)[NT], const DecDesc& d, const Common& c,
                                              const float* W, const EpiPre<NT>& pre, int n, bool valid,
                                              int lane, int g, float (&nd)[kMaxDyn]) {
@@ -350,9 +365,9 @@ __device__ __forceinline__ void decode_state(const f32x4 (&x)[NT], const DecDesc
   for (int t = 0; t < NT; ++t) x0[t] = x[t];
   act_tiles<-1, NT>(x0, d.pre_act, d.pre_slope);
   run_mlp<NT, NT, 1, ACT>(x0, o, d.dec, W, lane, g);
-  decode_state_tail<NT>(o, d, c, W, pre, n, valid, lane, g, nd);
+  decode_state_tail<NT, BYCOL>(o, d, c, W, pre, n, valid, lane, g, nd);
 }
-template <int NT>
+template <int NT, bool BYCOL>
 __device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const DecDesc& d, const Common& c,
                                                   const float* W, const EpiPre<NT>& pre, int n, bool valid,
                                                   int lane, int g, float (&nd)[kMaxDyn]) {
@@ -387,9 +402,14 @@ __device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const Dec
   for (int k = 0; k < kMaxDyn; ++k) {
     float val = k + 2 < c.dyn ? pre.xd[k + 2] : (k == c.dyn - 2 ? hm : (k == c.dyn - 1 ? vm : 0.f));
     const int tau = (k - c0) >> 1;
-    float bv = 0.f;  // pre.bcv[tau] by selects (a run-time register index would use scratch)
+    float bv;
+    if constexpr (BYCOL) {
+      bv = pre.bck[k];
+    } else {  // pre.bcv[tau] by selects (a run-time register index would use scratch)
+      bv = 0.f;
 #pragma unroll
-    for (int u = 0; u < kMaxDyn / 2; ++u) bv = u == tau ? pre.bcv[u] : bv;
+      for (int u = 0; u < kMaxDyn / 2; ++u) bv = u == tau ? pre.bcv[u] : bv;
+    }
     if (bc_on && k >= c0 && ((k - c0) & 1) == 0 && tau < c.p) val = bv;
     nd[k] = val;
   }
@@ -401,6 +421,15 @@ __device__ __forceinline__ void decode_state_tail(const f32x4 (&o)[1], const Dec
 #pragma unroll
   for (int k = 0; k < kMaxDyn; ++k)
     if (k < c.dyn) xw[k] = nd[k];
+}
+
+// The dynamic encoder's input of this lane, state column 4 g + q (0 past dyn), from the row's
+// new state nd (every lane of a row holds all of it): a 4-way select on the lane group instead of
+// one select per column.
+__device__ __forceinline__ float nd_column(const float (&nd)[kMaxDyn], int g, int q, int dyn) {
+  static_assert(kMaxDyn == 16, "four lane groups x four columns");
+  const float v = g == 0 ? nd[q] : g == 1 ? nd[4 + q] : g == 2 ? nd[8 + q] : nd[12 + q];
+  return 4 * g + q < dyn ? v : 0.f;
 }
 
 // What follows the last hop of a SWEGNN layer, on the layer's destination rows.

@@ -195,13 +195,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(4))) vo
       decode_state_tail<NT>(o, a.dec, c, Wl, pre, n, valid && r == 0, lane, g, nd);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = 4 * g + q;
-      float v = 0.f;
-#pragma unroll
-      for (int k = 0; k < kMaxDyn; ++k) v = (k == f && f < c.dyn) ? nd[k] : v;
-      dyn[q] = v;
-    }
+    for (int q = 0; q < 4; ++q) dyn[q] = nd_column(nd, g, q, c.dyn);
     float hn = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxDyn; ++k) hn = (k == c.dyn - 2) ? nd[k] : hn;

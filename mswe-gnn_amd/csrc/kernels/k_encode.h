@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     if constexpr (kBcHoist<NT>) {  // the next step's BC values before the weight staging
       if (DEC && dstep >= 0) {
         pre.step = dstep;
-        bc_prefetch<NT>(pre, a.dec, c);
+        bc_prefetch<NT, true>(pre, a.dec, c);
       }
     }
     MSW_MARK(c, 1);
@@ -78,18 +78,12 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
     if (DEC && dstep >= 0) {  // decode the previous step; the encoders read the updated state
       if constexpr (!kBcHoist<NT>) {
         pre.step = dstep;
-        bc_prefetch<NT>(pre, a.dec, c);
+        bc_prefetch<NT, true>(pre, a.dec, c);
       }
       float nd[kMaxDyn];
-      decode_state<NT, ACT>(xu, a.dec, c, Wl, pre, n, valid, lane, g, nd);
+      decode_state<NT, ACT, true>(xu, a.dec, c, Wl, pre, n, valid, lane, g, nd);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = 4 * g + r;
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < kMaxDyn; ++k) v = (k == f && f < c.dyn) ? nd[k] : v;
-        dyn[r] = v;
-      }
+      for (int r = 0; r < 4; ++r) dyn[r] = nd_column(nd, g, r, c.dyn);
       float hn = 0.f;
 #pragma unroll
       for (int k = 0; k < kMaxDyn; ++k) hn = (k == c.dyn - 2) ? nd[k] : hn;
