@@ -186,6 +186,7 @@ struct EdgeHopArgs {
   int coop;                        // waves per tile (k_edge_coop: MFMA output tiles split
                                    // across them), 0/1 = one wave per tile
   int pipe;                        // k_edge_mlp: software-pipelined variant (k_edge_mlp_pipe)
+  int stagger;                     // k_edge_mlp: waves 4..7 start this many x 2 k cycles late
   int wdirect;                     // k_edge_coop4: read the MLP region from its blob copy
                                    // (c.W + reg.off) instead of staging it in LDS
   int* step_inc;                   // rollout mode, first edge-MLP launch of a step:

@@ -464,6 +464,10 @@ void k_edge_mlp(EdgeHopArgs a) {
     stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
     __syncthreads();
   }
+  // stagger: the two waves of a SIMD (w, w + 4) otherwise run the same phase at the same time, so
+  // one's VALU work never overlaps the other's MFMA chain
+  if (w >= 4)
+    for (int k = 0; k < a.stagger; ++k) __builtin_amdgcn_s_sleep(32);
   const bool full = MSW_EDGE_FULL && a.h1t == T2 && a.Pe;
   if (a.reg.len > 0) {
     if (full)

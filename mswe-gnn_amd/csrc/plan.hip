@@ -280,6 +280,8 @@ struct Knobs {
   int enc_coop = -1;        // MSW_ENC_COOP        cooperative encoder: -1 size rule, 0 / 1 force
   int enc_coop_p = 0;       // MSW_ENC_COOP_P      F = 64 cooperative encoder on 2 waves per tile
   int mlp_pipe = 0;         // MSW_MLP_PIPE        pipelined split edge MLP (1)
+  int mlp_stagger = 2;      // MSW_MLP_STAGGER     split edge MLP: waves 4..7 start n x 2 k cycles late
+                            //                     (k_edge_mlp 22.0 -> 21.2 us, profiles/r05/ab_f64_mlp_stagger.txt)
   int eh_loop = 0;          // MSW_EH_LOOP         grid-stride fused edge hops at any size
   int hop_split = -1;       // MSW_HOP_SPLIT       feature-split middle hops: -1 = F = 64 rule
   int pool_wide = 1;        // MSW_POOL_WIDE       2F / 16 waves per pooling tile
@@ -296,7 +298,7 @@ inline Knobs knobs_from_env() {
       {"MSW_SPLIT_EDGE_MLP", &k.split_edge_mlp}, {"MSW_POOL_FUSE", &k.pool_fuse},
       {"MSW_UNPOOL_FUSE", &k.unpool_fuse}, {"MSW_DEFER_DECODE", &k.defer_decode}, {"MSW_HOP_ROWS", &k.hop_rows},
       {"MSW_COOP2_DIRECT", &k.coop2_direct}, {"MSW_COOP2_F64", &k.coop2_f64}, {"MSW_ENC_COOP", &k.enc_coop},
-      {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_EH_LOOP", &k.eh_loop},
+      {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_MLP_STAGGER", &k.mlp_stagger}, {"MSW_EH_LOOP", &k.eh_loop},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
       {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
       {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode},
@@ -1043,6 +1045,7 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       // with LDS-typed operands (round 4) it spills and the two-wave kernel is ahead:
       // zenodo4_f64 27.76 / 27.91 -> 28.08 / 28.09 M, profiles/r04/ab_f64_lds_operands.txt)
       L.eh.pipe = P->kn.mlp_pipe > 0;
+      L.eh.stagger = P->kn.mlp_stagger;
       L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
     }
