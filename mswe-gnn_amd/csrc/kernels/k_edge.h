@@ -394,6 +394,30 @@ void k_edge_hop(EdgeHopArgs a) {
 // fused waves = three rounds; 1,927 chunks on 2,048 waves = one).  The arithmetic is
 // edge_hop_core's, operation for operation: s is bit-identical.
 constexpr int kMlpWaves = 8;
+template <int NT>
+struct MlpFetch {
+  f32x4 u[2 * NT], v[2 * NT], p[2 * NT];
+  int4 e;
+};
+// FULL shape (2F-wide first layer with an edge term): one chunk's U / V / Pe rows, no selects;
+// ok = false reads the zero row instead (a launch of another shape)
+template <int NT>
+__device__ __forceinline__ void mlp_fetch_full(MlpFetch<NT>& f, const EdgeHopArgs& a, int ch, bool ok, int j, int g) {
+  constexpr int T2 = 2 * NT, hs = 16 * T2;
+  f.e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+  const bool ev = ok && f.e.z >= 0;
+  const float* z = a.c.zrow;
+  const float* Ub = ok ? a.U + (size_t)(ev ? f.e.x : a.n0) * hs : z;
+  const float* Vb = ok ? a.V + (size_t)(ev ? f.e.y : a.n0) * hs : z;
+  const float* Pb = ev ? a.Pe + (size_t)f.e.z * hs : z;
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int off = 16 * t + 4 * g;
+    f.u[t] = ld4(Ub + off);
+    f.v[t] = ld4(Vb + off);
+    f.p[t] = ld4(Pb + off);
+  }
+}
 template <int NT, int ACT>
 __global__ __launch_bounds__(64 * kMlpWaves) __attribute__((amdgpu_waves_per_eu(2)))
 void k_edge_mlp(EdgeHopArgs a) {
@@ -402,30 +426,76 @@ void k_edge_mlp(EdgeHopArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int w = wave_id();
   const int stride = gridDim.x * kMlpWaves;
+  const int ch0 = blockIdx.x * kMlpWaves + w;
   if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
+  // FULL: a 2F-wide first layer with an edge term (k_edge_hop's edge_full): no per-element
+  // selects on the run-time shape flags, and the first chunk's rows are gathered while the
+  // weight staging is in flight (issued after it: the in-order memory counter then waits for
+  // both at once; the first layer's sums H0 are all that stays live across the barrier)
+  const bool full = MSW_EDGE_FULL && a.h1t == T2 && a.Pe;
+  f32x4 H0[T2];
+  int4 e0;
   // the MLP operands through a pointer the compiler can prove to be LDS (a run-time choice
   // between LDS and the blob made every weight read a FLAT load, which also waits on vmcnt)
-  // FULL: a 2F-wide first layer with an edge term (k_edge_hop's edge_full): no per-element
-  // selects on the run-time shape flags
+  // one chunk: first layer's activation, layers 2..L, normalisation, s stored
+  auto chunk = [&](f32x4 (&H)[T2], const int4 e, const float* Wm, int ln, int g) __attribute__((always_inline)) {
+    const bool ev = e.z >= 0;
+    act_tiles<ACT, T2>(H, a.act1, a.slope1);
+    f32x4 sv[NT];
+    if (a.rest.n > 0) {
+      run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) sv[t] = H[t];
+    }
+    if (a.normalize) {
+      float ss = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
+      const float nrm = sqrtf(row_sum(ss));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 q = sv[t] / nrm;
+        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+        q.y = (q.y == q.y) ? q.y : 0.f;
+        q.z = (q.z == q.z) ? q.z : 0.f;
+        q.w = (q.w == q.w) ? q.w : 0.f;
+        sv[t] = q;
+      }
+    }
+    if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
+  };
   auto run = [&](const float* Wm, auto fullc) __attribute__((always_inline)) {
     constexpr bool FULL = decltype(fullc)::value;
-    const int hs = FULL ? 16 * T2 : 16 * a.h1t;
-    const float* z = a.c.zrow;
-    const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
-    for (int ch = blockIdx.x * kMlpWaves + w; ch < a.nchunks; ch += stride) {
-      const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
-      const int4 e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
-      const bool ev = e.z >= 0;
-      const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
-      const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
-      const float* Pb = (FULL || a.Pe) && ev ? a.Pe + (size_t)e.z * hs : z;
-      f32x4 H[T2];
+    if constexpr (FULL) {
+      if (ch0 < a.nchunks) {  // the first chunk, gathered during the staging
+        const int ln = opaque_lane(), g = ln >> 4;
+        chunk(H0, e0, Wm, ln, g);
+      }
+      for (int ch = ch0 + stride; ch < a.nchunks; ch += stride) {
+        const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+        MlpFetch<NT> f;
+        mlp_fetch_full<NT>(f, a, ch, true, j, g);
+        f32x4 H[T2];
 #pragma unroll
-      for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
-        const int off = 16 * t + 4 * g;
-        if constexpr (FULL) {
-          H[t] = (ld4(Ub + off) + ld4(Vb + off)) + ld4(Pb + off);
-        } else {
+        for (int t = 0; t < T2; ++t) H[t] = (f.u[t] + f.v[t]) + f.p[t];
+        chunk(H, f.e, Wm, ln, g);
+      }
+    } else {
+      const int hs = 16 * a.h1t;
+      const float* z = a.c.zrow;
+      const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
+      for (int ch = ch0; ch < a.nchunks; ch += stride) {
+        const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
+        const int4 e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
+        const bool ev = e.z >= 0;
+        const float* Ub = a.U + (size_t)(ev ? e.x : a.n0) * hs;
+        const float* Vb = a.V + (size_t)(ev ? e.y : a.n0) * hs;
+        const float* Pb = a.Pe && ev ? a.Pe + (size_t)e.z * hs : z;
+        f32x4 H[T2];
+#pragma unroll
+        for (int t = 0; t < T2; ++t) {  // unconditional loads, tiles past h1t read zeros
+          const int off = 16 * t + 4 * g;
           const bool on = t < a.h1t;
           const f32x4 u = ld4((on ? Ub : z) + off);
           const f32x4 v = ld4((on ? Vb : z) + off);
@@ -433,42 +503,24 @@ void k_edge_mlp(EdgeHopArgs a) {
           const f32x4 p = a.Pe ? pe : ld4(Wm + b1 + off);
           H[t] = on ? (u + v) + p : zero4();
         }
+        chunk(H, e, Wm, ln, g);
       }
-      act_tiles<ACT, T2>(H, a.act1, a.slope1);
-      f32x4 sv[NT];
-      if (a.rest.n > 0) {
-        run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
-      } else {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) sv[t] = H[t];
-      }
-      if (a.normalize) {
-        float ss = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-        const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          f32x4 q = sv[t] / nrm;
-          q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-          q.y = (q.y == q.y) ? q.y : 0.f;
-          q.z = (q.z == q.z) ? q.z : 0.f;
-          q.w = (q.w == q.w) ? q.w : 0.f;
-          sv[t] = q;
-        }
-      }
-      if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
     }
   };
-  if (a.reg.len > 0) {
-    stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
-    __syncthreads();
+  if (a.reg.len > 0) stage_glds<kMlpWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
+  {
+    const int lane = threadIdx.x & 63;
+    MlpFetch<NT> f0;
+    mlp_fetch_full<NT>(f0, a, ch0 < a.nchunks ? ch0 : 0, full && ch0 < a.nchunks, lane & 15, lane >> 4);
+    e0 = f0.e;
+#pragma unroll
+    for (int t = 0; t < T2; ++t) H0[t] = (f0.u[t] + f0.v[t]) + f0.p[t];
   }
+  if (a.reg.len > 0) __syncthreads();
   // stagger: the two waves of a SIMD (w, w + 4) otherwise run the same phase at the same time, so
   // one's VALU work never overlaps the other's MFMA chain
   if (w >= 4)
     for (int k = 0; k < a.stagger; ++k) __builtin_amdgcn_s_sleep(32);
-  const bool full = MSW_EDGE_FULL && a.h1t == T2 && a.Pe;
   if (a.reg.len > 0) {
     if (full)
       run(smem, std::true_type{});
@@ -487,11 +539,6 @@ void k_edge_mlp(EdgeHopArgs a) {
 // chunk n instead of every wave of the launch gathering, then multiplying, in lockstep.  Same
 // operations on the same operands as k_edge_mlp: s is bit-identical.
 constexpr int kMlpPipeWaves = 4;
-template <int NT>
-struct MlpFetch {
-  f32x4 u[2 * NT], v[2 * NT], p[2 * NT];
-  int4 e;
-};
 template <int NT>
 __device__ __forceinline__ void mlp_fetch(MlpFetch<NT>& f, const EdgeHopArgs& a, int ch, int j, int g) {
   constexpr int T2 = 2 * NT;
