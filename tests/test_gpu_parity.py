@@ -835,18 +835,20 @@ def test_build_variant_matches_default_bitwise(variant):
         assert res[0]["sha256"] == res[1]["sha256"], res
 
 
-@pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct"])
+@pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct", "mlp_stagger"])
 def test_f64_kernel_variants_match_default(cuda, monkeypatch, variant):
     """F = 64 kernel variants == the default bit for bit over a wet-start rollout (forced on the
     small mesh): k_edge_mlp_pipe (the split edge MLP with the next chunk's gathers in flight,
-    MSW_MLP_PIPE) against k_edge_mlp, and the two-wave cooperative edge hop reading its MLP
-    region from the blob (MSW_COOP2_DIRECT=2) against the LDS-staged one."""
+    MSW_MLP_PIPE) against k_edge_mlp, the two-wave cooperative edge hop reading its MLP region
+    from the blob (MSW_COOP2_DIRECT=2) against the LDS-staged one, and k_edge_mlp's start
+    stagger (MSW_MLP_STAGGER=0 against 2)."""
     from mswegnn.engine import EnginePlan
     T = 6
     g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=4).to(cuda)
     m = build_msgnn(4, 64, 4).to(cuda)
-    base = {"mlp_pipe": {"MSW_SPLIT_EDGE_MLP": "1"}, "coop2_direct": {"MSW_COOP2_F64": "2"}}[variant]
-    knob = {"mlp_pipe": "MSW_MLP_PIPE", "coop2_direct": "MSW_COOP2_DIRECT"}[variant]
+    base = {"mlp_pipe": {"MSW_SPLIT_EDGE_MLP": "1"}, "coop2_direct": {"MSW_COOP2_F64": "2"},
+            "mlp_stagger": {"MSW_SPLIT_EDGE_MLP": "1"}}[variant]
+    knob = {"mlp_pipe": "MSW_MLP_PIPE", "coop2_direct": "MSW_COOP2_DIRECT", "mlp_stagger": "MSW_MLP_STAGGER"}[variant]
     for k, v in base.items():
         monkeypatch.setenv(k, v)
     outs = []
