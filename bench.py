@@ -112,8 +112,9 @@ def build_workload(name, seed, T):
 def make_gatherer(dist, world, n0, T, device):
     """The end-of-rollout collective: ONE all-gather of every rank's fine-scale rollout
     [n0_r, 2, T].  Sizes are exchanged once here (meshes may differ per rank); payloads are
-    padded to the largest n0.  Returns gather(out_fine) -> list of [n0_r, 2, T] per rank."""
-    if world == 1:
+    padded to the largest n0.  Returns gather(out_fine) -> list of [n0_r, 2, T] per rank.
+    dist None (a single rank without a process group): no collective."""
+    if dist is None:
         return lambda out_fine: [out_fine]
     sz = torch.tensor([n0], dtype=torch.int64, device=device)
     sizes = [torch.zeros_like(sz) for _ in range(world)]
@@ -525,7 +526,8 @@ def self_launch(n, backend):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); default: the launcher's WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="zenodo4", choices=sorted(WORKLOADS))
@@ -559,6 +561,9 @@ def main():
     # one rank per GPU; MSW_DIST_BACKEND=gloo + more ranks than GPUs rehearses the N > 1 path
     # on a one-GPU box (ranks share the device; RCCL refuses two ranks on one device)
     backend = os.environ.get("MSW_DIST_BACKEND", "nccl")
+    gpus_given = args.gpus is not None
+    if not gpus_given:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `bench.py --gpus N` without a launcher: start the N ranks ourselves, before anything
         # here touches a GPU (no exec: the ranks are children, their exit code is ours)
@@ -566,7 +571,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    if gpus_given and world != args.gpus:  # an explicit --gpus that contradicts the launcher
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
               file=sys.stderr, flush=True)
         sys.exit(2)

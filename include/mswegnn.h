@@ -144,6 +144,9 @@ typedef struct {
   int32_t graph_captured;    /* a hipGraph of one rollout step is instantiated */
   int32_t dma_edge_hops;     /* launches of a rollout step on the LDS-DMA pipelined grid-stride
                                 edge MLP + hop (k_edge_hop_dma, MSW_EH_DMA) */
+  int64_t rccl_calls;        /* ncclSend / ncclRecv calls this plan issued (eagerly, or recorded
+                                into a captured rollout graph) */
+  int64_t rccl_steps;        /* rollout steps whose halo exchanges ran over RCCL (eager or replayed) */
 } msw_plan_stats;
 
 /* Halo exchange of one rank of a single mesh split over several ranks (SURVEY §8 f2,
@@ -152,7 +155,9 @@ typedef struct {
  * pair: the rows this rank receives from `peer` (its halo rows of that scale, local graph
  * numbering) and the rows it sends to `peer` (its owned rows the peer holds as halo, in the
  * peer's receive order).  Exchanged before every launch that gathers from other nodes:
- * U and out_0 before a layer's first hop, out_k before each further hop. */
+ * U and out_0 before a layer's first hop, out_k before each further hop.  An entry whose peer
+ * is the rank itself (equal receive and send counts) copies send row k to receive row k through
+ * the transport -- RCCL send / recv to self in a one-rank communicator. */
 typedef struct msw_exchange_desc {
   int32_t num_entries;
   const int32_t* peer;       /* [num_entries] peer rank */
@@ -175,7 +180,7 @@ int msw_plan_destroy(msw_plan* plan);
  * a partitioned plan is created with graph capture off, and msw_set_graph_capture(plan, 1) is
  * the only way to capture the RCCL exchanges too) or between plans of one process
  * (msw_group_rollout, validation on one GPU: the group's steps are captured as hipGraphs held
- * by plans[0] -- msw_set_graph_capture(plans[0], 0) steps it eagerly). */
+ * by plans[0] -- msw_set_group_graph(plans[0], 0) steps it eagerly). */
 int msw_plan_create_part(const msw_graph_desc* graph, const msw_model_desc* model, int device,
                          const msw_exchange_desc* xch, int32_t rank, msw_plan** out_plan);
 
@@ -216,9 +221,13 @@ int msw_rollout(msw_plan* plan, const float* x0, const float* bc, int32_t bc_tim
  * into dst (device, [N][F], graph numbering).  Debug / parity localisation only. */
 int msw_debug_buffer(msw_plan* plan, const char* name, float* dst, void* stream);
 
-/* Enable (1) / disable (0) graph capture of rollout steps and of msw_forward (default 1;
- * 0 = every launch enqueued eagerly). */
+/* Enable (1) / disable (0) graph capture of this plan's own rollout steps and msw_forward
+ * (default 1, partitioned plans 0; 0 = every launch enqueued eagerly).  With a communicator
+ * set, 1 captures the RCCL halo exchanges into the rollout graphs too. */
 int msw_set_graph_capture(msw_plan* plan, int enable);
+/* msw_group_rollout's own graphs (default 1): only the flag of the group's plans[0] is read,
+ * and it is independent of msw_set_graph_capture. */
+int msw_set_group_graph(msw_plan* plans0, int enable);
 
 int msw_plan_get_stats(const msw_plan* plan, msw_plan_stats* stats);
 

@@ -378,8 +378,14 @@ inline int build_host_exchange(const HostGraph& H, int part_rank, const msw_exch
       return MSW_ERR_INVALID;
     }
     XchPeer pe{d->peer[i], (int)X[s].recv_rows.size(), (int)(r1 - r0), (int)X[s].send_rows.size(), (int)(s1 - s0)};
-    if (pe.peer < 0 || pe.peer == part_rank) {
+    if (pe.peer < 0) {
       err = "exchange entry with a bad peer";
+      return MSW_ERR_INVALID;
+    }
+    // an entry with peer == part_rank exchanges rows with the rank itself (RCCL send / recv
+    // to self): one-rank communicators, and the transport check on a one-GPU box
+    if (pe.peer == part_rank && pe.rcount != pe.scount) {
+      err = "self exchange entry: receive and send counts differ";
       return MSW_ERR_INVALID;
     }
     auto conv = [&](const int32_t* rows, int64_t a, int64_t b, std::vector<int>& dst) -> int {

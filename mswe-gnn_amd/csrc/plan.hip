@@ -345,6 +345,9 @@ struct msw_plan {
   int h1t_max = 1;
   int64_t dev_bytes = 0;
   int64_t forward_calls = 0, rollout_steps = 0;
+  // RCCL transport: ncclSend / ncclRecv calls issued (eagerly or into a captured graph) and
+  // rollout steps whose halo exchanges ran over RCCL (eager steps and graph replays)
+  int64_t rccl_calls = 0, rccl_steps = 0;
   int kernels_per_step = 0;
   std::vector<Launch> sched_fwd, sched_roll;  // one forward step: forward / rollout mode
   int use_graph = 1;
@@ -1220,10 +1223,14 @@ int rccl_exchange(msw_plan* P, const ExchangeArgs& a, hipStream_t st) {
     HIP_TRY(launch_copy_rows(buf, X.send_rows, P->xsend, nullptr, X.nsend, w, st));
     ncclResult_t e = r.groupStart();
     for (const auto& pe : X.peers) {
-      if (e == ncclSuccess && pe.scount > 0)
-        e = r.send(P->xsend + (size_t)pe.soff * w, (size_t)pe.scount * w, ncclFloat32, pe.peer, P->comm, st);
-      if (e == ncclSuccess && pe.rcount > 0)
-        e = r.recv(P->xrecv + (size_t)pe.roff * w, (size_t)pe.rcount * w, ncclFloat32, pe.peer, P->comm, st);
+      if (e == ncclSuccess && pe.scount > 0 &&
+          (e = r.send(P->xsend + (size_t)pe.soff * w, (size_t)pe.scount * w, ncclFloat32, pe.peer, P->comm, st)) ==
+              ncclSuccess)
+        ++P->rccl_calls;
+      if (e == ncclSuccess && pe.rcount > 0 &&
+          (e = r.recv(P->xrecv + (size_t)pe.roff * w, (size_t)pe.rcount * w, ncclFloat32, pe.peer, P->comm, st)) ==
+              ncclSuccess)
+        ++P->rccl_calls;
     }
     const ncclResult_t e2 = r.groupEnd();
     if (e != ncclSuccess || e2 != ncclSuccess)
@@ -1716,9 +1723,17 @@ int loopback_exchange(msw_plan* const* plans, int k, const ExchangeArgs& a, hipS
     if (!back || back->scount != pe.rcount)
       return fail(MSW_ERR_INVALID, "exchange lists of plans " + std::to_string(k) + " and " +
                                        std::to_string(pe.peer) + " disagree");
-    for (int b = 0; b < a.nbuf; ++b)
-      HIP_TRY(launch_copy_rows(buf_of(Q, a.buf[b]), Y.send_rows + back->soff, buf_of(P, a.buf[b]),
-                               X.recv_rows + pe.roff, pe.rcount, a.width[b], st));
+    for (int b = 0; b < a.nbuf; ++b) {
+      if (Q == P) {  // self entry: staged, as the RCCL transport does (the row sets may overlap)
+        HIP_TRY(launch_copy_rows(buf_of(P, a.buf[b]), Y.send_rows + back->soff, P->xsend, nullptr, pe.rcount,
+                                 a.width[b], st));
+        HIP_TRY(launch_copy_rows(P->xsend, nullptr, buf_of(P, a.buf[b]), X.recv_rows + pe.roff, pe.rcount,
+                                 a.width[b], st));
+      } else {
+        HIP_TRY(launch_copy_rows(buf_of(Q, a.buf[b]), Y.send_rows + back->soff, buf_of(P, a.buf[b]),
+                                 X.recv_rows + pe.roff, pe.rcount, a.width[b], st));
+      }
+    }
   }
   return MSW_OK;
 }
@@ -1900,7 +1915,12 @@ int msw_forward(msw_plan* P, const float* x, float* y, void* stream) {
 
 int msw_set_graph_capture(msw_plan* P, int enable) {
   if (!P) return fail(MSW_ERR_INVALID, "null plan");
-  P->use_graph = enable ? 1 : 0;
+  P->use_graph = enable ? 1 : 0;  // the plan's own rollout / forward graphs only
+  return MSW_OK;
+}
+
+int msw_set_group_graph(msw_plan* P, int enable) {
+  if (!P) return fail(MSW_ERR_INVALID, "null plan");
   P->group_graph = enable ? 1 : 0;
   P->drop_group_graphs();
   return MSW_OK;
@@ -1941,6 +1961,12 @@ int msw_rollout(msw_plan* P, const float* x0, const float* bc, int32_t bc_tstrid
   if (int rc = final_decode(P, st)) return rc;
   P->rollout_steps += T;
   P->forward_calls += T;
+  if (P->comm)
+    for (const auto& X : P->xch)
+      if (!X.peers.empty()) {
+        P->rccl_steps += T;
+        break;
+      }
   return MSW_OK;
 }
 
@@ -1995,6 +2021,8 @@ int msw_plan_get_stats(const msw_plan* P, msw_plan_stats* s) {
   s->rollout_steps = P->rollout_steps;
   s->device_bytes = P->dev_bytes;
   s->graph_captured = P->step_exec != nullptr || P->multi_exec != nullptr || P->fwd_exec != nullptr;
+  s->rccl_calls = P->rccl_calls;
+  s->rccl_steps = P->rccl_steps;
   s->dma_edge_hops = 0;
   for (const Launch& L : P->sched_roll) {
     const EdgeHopArgs& a = L.eh;

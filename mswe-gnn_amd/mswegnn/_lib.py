@@ -69,7 +69,8 @@ class MswPlanStats(C.Structure):
                 ("hid_features", C.c_int32), ("padded_features", C.c_int32),
                 ("kernels_per_step", C.c_int32), ("forward_calls", C.c_int64),
                 ("rollout_steps", C.c_int64), ("device_bytes", C.c_int64),
-                ("graph_captured", C.c_int32), ("dma_edge_hops", C.c_int32)]
+                ("graph_captured", C.c_int32), ("dma_edge_hops", C.c_int32),
+                ("rccl_calls", C.c_int64), ("rccl_steps", C.c_int64)]
 
 
 class MswExchangeDesc(C.Structure):
@@ -121,6 +122,7 @@ SYMBOLS = [
                               C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     ("msw_debug_buffer", C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_void_p]),
     ("msw_set_graph_capture", C.c_int, [C.c_void_p, C.c_int]),
+    ("msw_set_group_graph", C.c_int, [C.c_void_p, C.c_int]),
     ("msw_plan_get_stats", C.c_int, [C.c_void_p, C.POINTER(MswPlanStats)]),
     ("msw_last_error", C.c_char_p, []),
     ("msw_abi_version", C.c_int, []),

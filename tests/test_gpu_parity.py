@@ -430,7 +430,7 @@ def test_partitioned_rollout_matches_whole_mesh(cuda, parts):
 def test_group_rollout_graph_matches_eager(cuda, parts):
     """msw_group_rollout replays its steps as hipGraphs (every part's launches + the halo copies
     between the parts' buffers, 16 steps per graph, held by plans[0]): the same rollout bit for
-    bit as the eager group (msw_set_graph_capture(plans[0], 0)) and as the undivided plan, on a
+    bit as the eager group (msw_set_group_graph(plans[0], 0)) and as the undivided plan, on a
     replay (a second call) too, over T = 40 (two 16-step graph launches + eight single steps)."""
     from mswegnn import _lib as L
     from mswegnn.partition import PartitionedRollout
@@ -441,7 +441,7 @@ def test_group_rollout_graph_matches_eager(cuda, parts):
     pr = PartitionedRollout(m, g, parts, cuda)
     graphed = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
     again = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
-    L.check(L.lib().msw_set_graph_capture(pr.plans[0]._h, 0))
+    L.check(L.lib().msw_set_group_graph(pr.plans[0]._h, 0))
     eager = pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).cpu()
     pr.close()
     assert torch.equal(graphed, eager) and torch.equal(graphed, again)

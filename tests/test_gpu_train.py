@@ -319,7 +319,7 @@ def test_hip_training_step_vs_reference_fixture(cuda, sname, R):
     names = gc.manifest()["fx_grad_train_K4_F32_sets"][sname]
     noise = gc.reference_fp32_noise(lambda: gc.training_batch(f"{sname}__", names, 5, fx, torch.device("cpu")),
                                     gc.weights("K4_F32"), orc.msgnn_config(num_scales=4, hid_features=32, K=4),
-                                    R, fx, f"{sname}_R{R}_fp64__")
+                                    R, fx, f"{sname}_R{R}_fp64__", p32=pre)
     worst, rule64 = gc.check(ours, fx, pre, TOL, f"{sname}_R{R}_fp64__", noise=noise)
     print(f"HIP training_step {sname} R={R}: loss {float(ours['loss']):.7e} (reference "
           f"{float(fx[pre + 'loss']):.7e}), worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; "
@@ -341,7 +341,8 @@ def test_hip_f64_training_step_vs_reference_fixture(cuda):
     names = gc.manifest()["fx_grad_train_F64_sets"]["b2"]
     P64 = {k: v.detach().cpu() for k, v in build_msgnn(4, 64, 4).state_dict().items()}
     noise = gc.reference_fp32_noise(lambda: gc.training_batch("b2__", names, 5, fx, torch.device("cpu")), P64,
-                                    orc.msgnn_config(num_scales=4, hid_features=64, K=4), 4, fx, "b2_R4_fp64__", n=4)
+                                    orc.msgnn_config(num_scales=4, hid_features=64, K=4), 4, fx, "b2_R4_fp64__", n=4,
+                                    p32=pre)
     worst, rule64 = gc.check(ours, fx, pre, TOL, "b2_R4_fp64__", noise=noise)
     print(f"HIP F=64 training_step R=4: loss {float(ours['loss']):.7e} (reference {float(fx[pre + 'loss']):.7e}), "
           f"worst {worst:.2e}, global {gc.global_rel(ours, fx, pre):.2e}; rules past 1e-4: {rule64}")
@@ -383,26 +384,33 @@ def test_hip_zenodo4_training_step_vs_reference_fixture(cuda, R):
     glob = gc.global_rel(ours, fx, pre)
     import msgnn_torch as orc
     noise = gc.reference_fp32_noise(lambda: gc.zenodo4_batch(torch.device("cpu"))[0], gc.weights("K4_F32"),
-                                    orc.msgnn_config(num_scales=4, hid_features=32, K=4), R, fx, f"R{R}_fp64__", n=4)
+                                    orc.msgnn_config(num_scales=4, hid_features=32, K=4), R, fx, f"R{R}_fp64__", n=4,
+                                    p32=pre)
     try:
         worst, rule64 = gc.check(ours, fx, pre, TOL, f"R{R}_fp64__", noise=noise)
+        ref_ok = True
         print(f"HIP zenodo4 training_step R={R}: worst {worst:.2e}, global {glob:.2e} vs the reference")
-        return
     except AssertionError as e:
-        print(f"HIP zenodo4 R={R}: global {glob:.2e} vs the reference, per tensor {e}; along the HIP branch:")
+        ref_ok = False
+        print(f"HIP zenodo4 R={R}: global {glob:.2e} vs the reference, per tensor {e}")
+    # always: the HIP gradients against the reference restated in float64 along the
+    # HIP run's own branch -- global within 2e-5, every flipped decision within rounding
     _, gb, fl = gc.oracle_zenodo4_step(R, torch.float64, tape=[
         {k: (v if k == "kind" else [t.cpu() for t in v] if isinstance(v, list) else v.cpu()) for k, v in r.items()}
         for r in tape])
     assert fl.pos == len(fl.tape), "the HIP run's decision tape does not match the restatement's calls"
     along = gc.as_fixture(gb)
+    # the along-branch reference IS float64: its fp32 spread is the fixture's (noise, capped)
     worst_b, rules_b = gc.check(ours, along, "X__", TOL, "X__", noise=noise)
     glob_b = gc.global_rel(ours, along, "X__")
     far = [f for f in fl.flips if f[2] > gc.FLIP_DIST]
     print(f"  vs float64 along the HIP branch: worst {worst_b:.2e}, global {glob_b:.2e}, per tensor {rules_b}; "
           f"flipped decisions (where, count, largest distance to the threshold): {fl.flips}")
     assert glob_b <= 2e-5, glob_b
-    assert fl.flips, "the HIP run leaves the reference without a flipped decision"
     assert not far, far
+    if not ref_ok or glob > TOL:
+        # a departure from the reference's own fp32 gradients must come from a flipped decision
+        assert fl.flips, f"the HIP run leaves the reference (global {glob:.2e}) without a flipped decision"
 
 
 @pytest.mark.parametrize("R", [1, 2])

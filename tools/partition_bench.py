@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--parts", type=int, nargs="+", default=[2, 4])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--eager", action="store_true",
-                    help="step the group eagerly (msw_set_graph_capture(plans[0], 0)) instead of its captured graphs")
+                    help="step the group eagerly (msw_set_group_graph(plans[0], 0)) instead of its captured graphs")
     a = ap.parse_args()
     import bench
     from mswegnn.partition import PartitionedRollout
@@ -57,7 +57,7 @@ def main():
         pr = PartitionedRollout(m, g, W, device=dev)
         if a.eager:
             from mswegnn import _lib as L
-            L.check(L.lib().msw_set_graph_capture(pr.plans[0]._h, 0))
+            L.check(L.lib().msw_set_group_graph(pr.plans[0]._h, 0))
         t_p, r_p = timed(lambda: pr.rollout(g.x, g.BC, g.node_BC, g.type_BC, a.T), a.reps)
         r_p = r_p.cpu()
         err = max((r_p[..., t] - ref[..., t]).abs().max().item() / den[t] for t in range(a.T))
