@@ -109,6 +109,58 @@ def build_workload(name, seed, T):
     return g, m, w, desc
 
 
+CPU_SHARE_NOTE = ("threads = the CPU share of one GPU on the GPU box, 16 (gpurun sets OMP_NUM_THREADS=16; "
+                  "os.cpu_count() there reports the whole machine, host_cores); more threads on the "
+                  "oracle's ATen CPU ops do not help: profiles/r06/cpu_threads.json (1 / 8 / 16 / 32 / 64 / "
+                  "all threads on one simulation)")
+
+
+def cpu_share():
+    """(host cores, threads the CPU baseline uses): OMP_NUM_THREADS (the GPU box's per-GPU share)
+    else the host's cores, at most 16."""
+    host = os.cpu_count() or 1
+    return host, min(int(os.environ.get("OMP_NUM_THREADS", "0")) or host, 16)
+
+
+def _cpu_sim_worker(job):
+    """One simulation of a workload through the oracle on the host (a spawned process of
+    cpu_batch_baseline): built, then every worker starts its timed rollout together."""
+    name, seed, T, Tc, threads, barrier = job
+    torch.set_num_threads(threads)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import msgnn_torch as orc  # test/baseline infrastructure only
+    g, m, w, desc = build_workload(name, seed, T)
+    P = {k: v.detach() for k, v in m.state_dict().items()}
+    cfg = orc.msgnn_config(num_scales=w["S"], hid_features=w["F"], K=w["K"])
+    barrier.wait(timeout=300)
+    c0 = time.time()
+    orc.rollout(P, cfg, g, Tc)
+    return desc["fine_nodes"], Tc, c0, time.time()
+
+
+def cpu_batch_baseline(name, ids, T, share, seconds, t1, t1_threads):
+    """The CPU analogue of the reference's batched evaluation: the simulations `ids` one per
+    process, all at once, over the `share` host threads (threads split evenly), each a
+    Tc-step rollout sized to ~`seconds` from the single-simulation step time t1 (measured on
+    t1_threads).  -> {value, unit, processes, threads_per_process, sample}."""
+    import multiprocessing as mp
+    ids = list(ids)[:share]
+    procs = len(ids)
+    tpp = max(1, share // procs)
+    Tc = int(min(T, max(1, seconds / max(t1 * t1_threads / tpp, 1e-6))))
+    ctx = mp.get_context("spawn")  # fresh interpreters: no GPU state, no fork of this process
+    with ctx.Manager() as man:
+        bar = man.Barrier(procs)
+        with ctx.Pool(procs) as pool:
+            res = pool.map(_cpu_sim_worker, [(name, i, T, Tc, tpp, bar) for i in ids], chunksize=1)
+    wall = max(r[3] for r in res) - min(r[2] for r in res)
+    work = sum(r[0] * r[1] for r in res)
+    return {"value": work / wall, "unit": "fine-node-steps/s", "processes": procs, "threads_per_process": tpp,
+            "cores": procs * tpp, "kind": "port",
+            "sample": f"{procs} simulations of the workload (ids {ids[0]}..{ids[-1]}), one {Tc}-step rollout each "
+                      f"in its own process, started together; wall {wall:.1f} s"}
+
+
 def make_gatherer(dist, world, n0, T, device):
     """The end-of-rollout collective: ONE all-gather of every rank's fine-scale rollout
     [n0_r, 2, T].  Sizes are exchanged once here (meshes may differ per rank); payloads are
@@ -825,8 +877,8 @@ def main():
             if world == 1 and not args.no_cpu_baseline:
                 sys.path.insert(0, os.path.join(ROOT, "oracle"))
                 import msgnn_torch as orc  # test/baseline infrastructure only
-                threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-                threads = min(threads, 16)
+                host_cores, share = cpu_share()
+                threads = share
                 torch.set_num_threads(threads)
                 P = {k: v.detach().cpu() for k, v in model_cpu.state_dict().items()}
                 cfg = orc.msgnn_config(num_scales=desc["num_scales"], hid_features=F, K=desc["K"])
@@ -850,7 +902,13 @@ def main():
                        "sample": f"{reps} x {Tc}-step rollout of one simulation of the workload "
                                  f"(N0={n0}), reference algorithm in oracle/msgnn_torch.py (same ATen "
                                  f"CPU ops, bit-identical to the reference), torch {torch.__version__}, "
-                                 f"{threads} threads, {t_cpu:.1f} s"}
+                                 f"{threads} threads, {t_cpu:.1f} s",
+                       "host_cores": host_cores,
+                       "threads_note": CPU_SHARE_NOTE}
+                if B > 1:
+                    # the reference evaluates batches of simulations (test_model.py:37): on the host
+                    # that is one simulation per process over the CPU share
+                    cpu["batch"] = cpu_batch_baseline(args.workload, ids, T, share, args.cpu_seconds, t1, threads)
                 r0 = r_gpu[:g_cpu.num_nodes, :, :Tc]  # simulation 0 = the batch's first graph
                 d = (r0 - r_cpu).abs()
                 parity["vs_cpu_reference"] = {
@@ -881,7 +939,6 @@ def main():
             "all_node_steps_per_s": value * desc.get("batch_nodes", desc["all_nodes"]) / fine_rank,
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "engine": {"kernels_per_step": st["kernels_per_step"], "graph_captured": st["graph_captured"],
-                       "dma_edge_hops": st["dma_edge_hops"],
                        "device_bytes": st["device_bytes"],
                        "device_bytes_note": "plan-owned: graph tables, weights, per-node buffers and the "
                                             "edge-encoder inputs / outputs kept for the per-rollout "

@@ -142,8 +142,6 @@ typedef struct {
   int64_t rollout_steps;     /* rollout steps executed through the HIP path so far */
   int64_t device_bytes;      /* device memory owned by the plan */
   int32_t graph_captured;    /* a hipGraph of one rollout step is instantiated */
-  int32_t dma_edge_hops;     /* launches of a rollout step on the LDS-DMA pipelined grid-stride
-                                edge MLP + hop (k_edge_hop_dma, MSW_EH_DMA) */
   int64_t rccl_calls;        /* ncclSend / ncclRecv calls this plan issued (eagerly, or recorded
                                 into a captured rollout graph) */
   int64_t rccl_steps;        /* rollout steps whose halo exchanges ran over RCCL (eager or replayed) */

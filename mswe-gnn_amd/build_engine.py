@@ -60,7 +60,11 @@ def build(force=False, verbose=True, variant=""):
     odir = os.path.join(HERE, "_obj" + (f"_{variant}" if variant else ""))
     # build variants: the -DMSW_TRACE diagnostic library, and the speed A/Bs of the current
     # round (each bit-identical to the default: test_build_variant_matches_default_bitwise)
-    extra = {"trace": ["-DMSW_TRACE"], "r05base": ["-DMSW_PRELU_MAX=0", "-DMSW_EDGE_FULL=0"]}.get(variant, [])
+    extra = {"trace": ["-DMSW_TRACE"],
+             # the VALU diets of rounds 5-6 all off (PReLU as max, FULL edge kernels, shared-reciprocal
+             # division): test_build_variant_matches_default_bitwise[valubase]
+             "valubase": ["-DMSW_PRELU_MAX=0", "-DMSW_EDGE_FULL=0", "-DMSW_FAST_DIV=0"],
+             "nofastdiv": ["-DMSW_FAST_DIV=0"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     out = lib_path(variant)

@@ -156,6 +156,7 @@ struct PoolFuse {
   int post_act; float post_slope;
 };
 
+constexpr int kMlpStagger = 2;  // k_edge_mlp start stagger (profiles/r05/ab_f64_mlp_stagger.txt)
 struct EdgeHopArgs {
   Common c;
   WReg reg;                        // [MLP | epilogue operands | filter W_1]
@@ -185,18 +186,14 @@ struct EdgeHopArgs {
   Epilogue epi;
   int coop;                        // waves per tile (k_edge_coop: MFMA output tiles split
                                    // across them), 0/1 = one wave per tile
-  int pipe;                        // k_edge_mlp: software-pipelined variant (k_edge_mlp_pipe)
   int stagger;                     // k_edge_mlp: waves 4..7 start this many x 2 k cycles late
+                                   // (kMlpStagger)
   int wdirect;                     // k_edge_coop4: read the MLP region from its blob copy
                                    // (c.W + reg.off) instead of staging it in LDS
   int* step_inc;                   // rollout mode, first edge-MLP launch of a step:
                                    // &RolloutIO::step, advanced once (workgroup 0, lane 0)
   const EdgeChunk* chunks; int nchunks;  // k_edge_mlp: dense 16-edge chunks [nchunks][16]
   PoolFuse pool;                   // mean pooling + projection fused in (k_edge_coop only)
-  int dma;                         // grid-stride variant with the next tile's rows LDS-DMA'd
-                                   // during the current tile's MLP (k_edge_hop_dma): 1 = eight
-                                   // waves per workgroup, 2 = four
-  int dma_off;                     // k_edge_hop_dma: floats of LDS before the per-wave regions
 };
 
 // Hops 2..K over the same edge tiles as the fused first hop.
@@ -223,7 +220,17 @@ struct HopArgs {
   int nrows;         // destinations of the scale (local rows [0, nrows) = internal n0 + k)
   const int* rptr;   // [nrows + 1] CSR offsets (local destination order)
   const int2* redge; // [E] {internal source row, tile-padded s slot}, reference edge order
+  // one-workgroup hop chain (k_hop_wg, small scales): wg_hops > 0 hops in this launch, from
+  // `in` (the first hop's input) to `out`, with filters wg_filt[] (blob offsets, -1 = none)
+  // copied to LDS at float offset wg_foff (after the staged epilogue region of a LAST chain)
+  int wg_hops, wg_foff;
+  int wg_filt[MSW_MAX_HOPS];
+  const int4* wg_edges;  // per local row: {source local row, tile-padded s slot} x kWgDeg as two
+                         // int4 (sources, slots; -1 = no edge), one load each, no CSR round trip
 };
+constexpr int kWgWaves = 16;   // k_hop_wg: one workgroup, one 16-row tile per wave
+constexpr int kWgRows = 16 * kWgWaves;
+constexpr int kWgDeg = 4;      // in-edges per destination held in registers
 
 // Mean pooling into the coarse rows + projection of the next processor.
 

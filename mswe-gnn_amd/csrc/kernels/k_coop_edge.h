@@ -352,21 +352,7 @@ __device__ __forceinline__ void unpool_row(f32x4 (&res)[NT], const UnpoolIn<NT>&
 #pragma unroll
     for (int t = 0; t < NT; ++t) sv[t] = H[t];
   }
-  if (d.normalize) {
-    float ss = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-    const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      f32x4 q = sv[t] / nrm;
-      q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-      q.y = (q.y == q.y) ? q.y : 0.f;
-      q.z = (q.z == q.z) ? q.z : 0.f;
-      q.w = (q.w == q.w) ? q.w : 0.f;
-      sv[t] = q;
-    }
-  }
+  if (d.normalize) normalize_s<NT>(sv);  // gnn.py:424-426
   // put_message with the destination's rows zero (own_zero), then its one-edge sum
   float rs = 0.f, rd = 0.f;
 #pragma unroll
@@ -483,21 +469,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop(EdgeHopArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) sv[t] = H[t];
     }
-    if (a.normalize) {
-      float ss = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-      const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 v = sv[t] / nrm;
-        v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
-        v.y = (v.y == v.y) ? v.y : 0.f;
-        v.z = (v.z == v.z) ? v.z : 0.f;
-        v.w = (v.w == v.w) ? v.w : 0.f;
-        sv[t] = v;
-      }
-    }
+    if (a.normalize) normalize_s<NT>(sv);  // gnn.py:424-426
     if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
     put_message<NT, FULL ? 1 : -1>(my, q.os, od, sv, L.ev, a.grad, a.upwind, g);
     f32x4 agg[NT];
@@ -702,21 +674,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_edge_coop4(EdgeHopArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) sv[t] = H[t];
     }
-    if (a.normalize) {
-      float ss = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-      const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 v = sv[t] / nrm;
-        v.x = (v.x == v.x) ? v.x : 0.f;  // masked_fill_(isnan, 0)
-        v.y = (v.y == v.y) ? v.y : 0.f;
-        v.z = (v.z == v.z) ? v.z : 0.f;
-        v.w = (v.w == v.w) ? v.w : 0.f;
-        sv[t] = v;
-      }
-    }
+    if (a.normalize) normalize_s<NT>(sv);  // gnn.py:424-426
     if (live && r == 0 && a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);
     // every rank has read the slab's node rows before the first MLP exchange barrier: rank 0
     // may overwrite them with the messages (a.rest.n == 0 has no barrier: add one)

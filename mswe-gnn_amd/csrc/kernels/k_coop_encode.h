@@ -49,7 +49,7 @@ __device__ __forceinline__ void enc_coop_mlp(const f32x4 (&in)[IN0], f32x4 (&out
 // operands are loaded by the caller (load(), early -- at kernel start), layer 1's are in flight
 // during layer 0's MFMA chain and exchange, deeper layers load theirs at the layer.  PF: every
 // layer's rank slice has TS = T / P output tiles (all F = 64 and F = 32 encoder MLPs at P =
-// NT); otherwise (the decoder at MSW_ENC_COOP_P=2) it is enc_coop_mlp.  Same arithmetic.
+// NT); otherwise it is enc_coop_mlp.  Same arithmetic.
 #ifndef MSW_ENC_PF
 #define MSW_ENC_PF 1
 #endif

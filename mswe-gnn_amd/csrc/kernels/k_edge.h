@@ -239,21 +239,7 @@ __device__ __forceinline__ void edge_hop_core(const EdgeHopRows<NT>& r, const Ed
     for (int t = 0; t < NT; ++t) sv[t] = H[t];
   }
   MSW_MARK(c, 5);
-  if (a.normalize) {
-    float ss = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-    const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      f32x4 q = sv[t] / nrm;
-      q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-      q.y = (q.y == q.y) ? q.y : 0.f;
-      q.z = (q.z == q.z) ? q.z : 0.f;
-      q.w = (q.w == q.w) ? q.w : 0.f;
-      sv[t] = q;
-    }
-  }
+  if (a.normalize) normalize_s<NT>(sv);  // gnn.py:424-426
   if (a.s) store_row<NT>(a.s + L.p * F, sv, NT, g);  // padding slots too: never read
   put_message<NT, FULL ? 1 : -1>(my, r.os, od, sv, L.ev, a.grad, a.upwind, g);  // the slab row is free again
   MSW_MARK(c, 6);
@@ -448,21 +434,7 @@ void k_edge_mlp(EdgeHopArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) sv[t] = H[t];
     }
-    if (a.normalize) {
-      float ss = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-      const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        f32x4 q = sv[t] / nrm;
-        q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-        q.y = (q.y == q.y) ? q.y : 0.f;
-        q.z = (q.z == q.z) ? q.z : 0.f;
-        q.w = (q.w == q.w) ? q.w : 0.f;
-        sv[t] = q;
-      }
-    }
+    if (a.normalize) normalize_s<NT>(sv);  // gnn.py:424-426
     if (ev) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
   };
   auto run = [&](const float* Wm, auto fullc) __attribute__((always_inline)) {
@@ -531,90 +503,4 @@ void k_edge_mlp(EdgeHopArgs a) {
   } else {
     run(a.c.W, std::false_type{});
   }
-}
-
-// k_edge_mlp software-pipelined (F = 64, MSW_MLP_PIPE): one wave per SIMD, each wave walks
-// ~2 chunks and issues the next chunk's U / V / Pe gathers (1.5 KB per edge) before the
-// current chunk's MLP (384 MFMAs), so the gathers of chunk n+1 run under the MFMA chain of
-// chunk n instead of every wave of the launch gathering, then multiplying, in lockstep.  Same
-// operations on the same operands as k_edge_mlp: s is bit-identical.
-constexpr int kMlpPipeWaves = 4;
-template <int NT>
-__device__ __forceinline__ void mlp_fetch(MlpFetch<NT>& f, const EdgeHopArgs& a, int ch, int j, int g) {
-  constexpr int T2 = 2 * NT;
-  const int hs = 16 * a.h1t;
-  const float* z = a.c.zrow;
-  f.e = reinterpret_cast<const int4*>(a.chunks)[(size_t)ch * kRowsPerWave + j];
-  const bool ev = f.e.z >= 0;
-  const float* Ub = a.U + (size_t)(ev ? f.e.x : a.n0) * hs;
-  const float* Vb = a.V + (size_t)(ev ? f.e.y : a.n0) * hs;
-  const float* Pb = a.Pe && ev ? a.Pe + (size_t)f.e.z * hs : z;
-#pragma unroll
-  for (int t = 0; t < T2; ++t) {
-    const int off = 16 * t + 4 * g;
-    const bool on = t < a.h1t;
-    f.u[t] = ld4((on ? Ub : z) + off);
-    f.v[t] = ld4((on ? Vb : z) + off);
-    f.p[t] = ld4((on ? Pb : z) + off);
-  }
-}
-template <int NT, int ACT>
-__global__ __launch_bounds__(64 * kMlpPipeWaves) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_edge_mlp_pipe(EdgeHopArgs a) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT, T2 = 2 * NT;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int w = wave_id();
-  const int stride = gridDim.x * kMlpPipeWaves;
-  if (a.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *a.step_inc += 1;
-  const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
-  int ch = blockIdx.x * kMlpPipeWaves + w;
-  MlpFetch<NT> f;
-  if (ch < a.nchunks) mlp_fetch<NT>(f, a, ch, j, g);  // in flight during the weight staging
-  // the MLP operands through a pointer the compiler can prove to be LDS (see k_edge_mlp)
-  auto run = [&](const float* Wm) __attribute__((always_inline)) {
-    const int b1 = a.b1_off >= 0 ? a.b1_off : 0;
-    for (; ch < a.nchunks; ch += stride) {
-      f32x4 H[T2];
-#pragma unroll
-      for (int t = 0; t < T2; ++t) {
-        const f32x4 p = a.Pe ? f.p[t] : ld4(Wm + b1 + 16 * t + 4 * g);
-        H[t] = t < a.h1t ? (f.u[t] + f.v[t]) + p : zero4();
-      }
-      const int4 e = f.e;
-      if (ch + stride < a.nchunks) mlp_fetch<NT>(f, a, ch + stride, j, g);
-      act_tiles<ACT, T2>(H, a.act1, a.slope1);
-      f32x4 sv[NT];
-      if (a.rest.n > 0) {
-        run_mlp<T2, T2, NT, ACT>(H, sv, a.rest, Wm, ln, g);
-      } else {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) sv[t] = H[t];
-      }
-      if (a.normalize) {
-        float ss = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
-        const float nrm = sqrtf(row_sum(ss));
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          f32x4 q = sv[t] / nrm;
-          q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-          q.y = (q.y == q.y) ? q.y : 0.f;
-          q.z = (q.z == q.z) ? q.z : 0.f;
-          q.w = (q.w == q.w) ? q.w : 0.f;
-          sv[t] = q;
-        }
-      }
-      if (e.z >= 0) store_row<NT>(a.s + (size_t)e.z * F, sv, NT, g);
-    }
-  };
-  if (a.reg.len > 0) {
-    stage_glds<kMlpPipeWaves>(smem, a.c.W, a.reg, 0, a.reg.len);
-    __syncthreads();
-  }
-  if (a.reg.len > 0)
-    run(smem);
-  else
-    run(a.c.W);
 }

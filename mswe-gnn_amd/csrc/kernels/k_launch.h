@@ -37,9 +37,9 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
-  if constexpr (kStaged<NT>) {  // DMA-pipelined grid-stride edge hop: all of its LDS is dynamic
-    for (const void* f : {(const void*)k_edge_hop_dma<NT, 1>, (const void*)k_edge_hop_dma<NT, -1>,
-                          (const void*)k_edge_hop_dma<NT, 1, 4>, (const void*)k_edge_hop_dma<NT, -1, 4>}) {
+  if constexpr (kStaged<NT>) {  // one-workgroup hop chains: all of their LDS is dynamic
+    for (const void* f : {(const void*)k_hop_wg<NT, 1, false>, (const void*)k_hop_wg<NT, 1, true>,
+                          (const void*)k_hop_wg<NT, -1, true>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -101,24 +101,6 @@ hipError_t prepare_kernels() {
 template <int NT>
 hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   if (a.Npad <= 0) return hipSuccess;
-  if constexpr (NT == 4) {
-    if (a.coop == 2) {  // F = 64 on two waves per row tile (MSW_ENC_COOP_P=2)
-      constexpr int P = 2, WV = enc_coop_waves<NT>();
-      const dim3 grid(a.Npad / ((WV / P) * kRowsPerWave)), block(64 * WV);
-      const size_t sh = lds_bytes<NT>(a.lds_floats);
-      if (a.dec.on) {
-        if (a.c.prelu)
-          hipLaunchKernelGGL((k_encode_coop<NT, 1, true, P>), grid, block, sh, st, a);
-        else
-          hipLaunchKernelGGL((k_encode_coop<NT, -1, true, P>), grid, block, sh, st, a);
-      } else if (a.c.prelu) {
-        hipLaunchKernelGGL((k_encode_coop<NT, 1, false, P>), grid, block, sh, st, a);
-      } else {
-        hipLaunchKernelGGL((k_encode_coop<NT, -1, false, P>), grid, block, sh, st, a);
-      }
-      return hipGetLastError();
-    }
-  }
   if constexpr (NT >= 2) {
     if (a.coop == NT) {  // P = NT waves per row tile (F = 32: 2, F = 64: 4)
       constexpr int P = NT, WV = enc_coop_waves<NT>();
@@ -188,15 +170,6 @@ static const void* edge_hop_kernel(int prelu, bool loop, int last) {
 template <int NT>
 hipError_t launch_edge_mlp(const EdgeHopArgs& a, hipStream_t st) {
   if (a.nchunks <= 0) return hipSuccess;
-  if (a.pipe) {
-    const int n = cdiv(a.nchunks, kMlpPipeWaves);
-    const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(64 * kMlpPipeWaves);
-    if (a.c.prelu)
-      hipLaunchKernelGGL((k_edge_mlp_pipe<NT, 1>), grid, block, eh_lds_bytes(a.reg.len), st, a);
-    else
-      hipLaunchKernelGGL((k_edge_mlp_pipe<NT, -1>), grid, block, eh_lds_bytes(a.reg.len), st, a);
-    return hipGetLastError();
-  }
   const int n = cdiv(a.nchunks, kMlpWaves);
   const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(64 * kMlpWaves);
   if (a.c.prelu)
@@ -219,17 +192,6 @@ hipError_t launch_edge_hop(const EdgeHopArgs& a, hipStream_t st) {
   }
   if (a.pool.slots || a.pool.parent) return hipErrorInvalidValue;  // fused into k_edge_coop only
   const bool loop = tile_loop(a);
-  if constexpr (kStaged<NT>) {
-    if (a.dma && loop && !a.last) {  // plan.hip set_grid_cap: the conditions k_edge_hop_dma assumes
-      EdgeHopArgs b = a;
-      b.c.xcd = 0;
-      void* args[] = {&b};
-      const int wv = a.dma == 2 ? 4 : kDmaWaves;
-      const void* f = a.dma == 2 ? (a.c.prelu ? (const void*)k_edge_hop_dma<NT, 1, 4> : (const void*)k_edge_hop_dma<NT, -1, 4>)
-                                 : (a.c.prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>);
-      return hipLaunchKernel(f, dim3(a.max_blocks), dim3(64 * wv), args, dma_lds_bytes<NT>(a.reg_nf, wv), st);
-    }
-  }
   EdgeHopArgs b = a;
   const dim3 grid = loop ? dim3(tile_grid(a)) : xcd_grid(b, tile_grid(a));
   if (loop) b.c.xcd = 0;
@@ -243,6 +205,19 @@ hipError_t launch_hop_kernel(const HopArgs& a, bool loop, dim3 grid, dim3 block,
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
+  if (a.wg_hops > 0) {  // one-workgroup hop chain (plan.hip merge_wg_chains: F <= 32 only)
+    if constexpr (kStaged<NT>) {
+      const size_t sh = ((size_t)a.wg_foff + (size_t)a.wg_hops * NT * NT * 256 + 2 * (size_t)kWgRows * (16 * NT + 4)) *
+                        sizeof(float);
+      if (sh > 160 * 1024 || a.nrows > kWgRows) return hipErrorInvalidValue;
+      const void* f = !a.last ? (const void*)k_hop_wg<NT, 1, false>
+                    : a.c.prelu ? (const void*)k_hop_wg<NT, 1, true> : (const void*)k_hop_wg<NT, -1, true>;
+      HopArgs b = a;
+      void* args[] = {&b};
+      return hipLaunchKernel(f, dim3(1), dim3(64 * (a.last ? wg_waves<true>() : wg_waves<false>())), args, sh, st);
+    }
+    return hipErrorInvalidValue;
+  }
   if (a.coop > 1 && a.last) {  // waves per tile = NT (2 for F = 32, 4 for F = 64)
     const void* f = hop_coop_kernel<NT>(a.c.prelu);
     if (!f) return hipErrorInvalidValue;
@@ -380,13 +355,6 @@ static const void* kernel_of(int kind, int prelu, int last) {
     case 9: return hop_coop_kernel<NT>(prelu);
     case 10: return prelu ? (const void*)k_edge_mlp<NT, 1> : (const void*)k_edge_mlp<NT, -1>;
     case 14: return (const void*)k_hop_rows<NT>;
-    case 15: return prelu ? (const void*)k_edge_mlp_pipe<NT, 1> : (const void*)k_edge_mlp_pipe<NT, -1>;
-    case 17:
-      if constexpr (kStaged<NT>) return prelu ? (const void*)k_edge_hop_dma<NT, 1> : (const void*)k_edge_hop_dma<NT, -1>;
-      return nullptr;
-    case 18:
-      if constexpr (kStaged<NT>) return prelu ? (const void*)k_edge_hop_dma<NT, 1, 4> : (const void*)k_edge_hop_dma<NT, -1, 4>;
-      return nullptr;
     default: return nullptr;
   }
 }
@@ -395,16 +363,11 @@ int resident_blocks(int kind, int prelu, int last, size_t dyn_bytes, int loop) {
   const void* f = loop ? kernel_of<NT, true>(kind, prelu, last) : kernel_of<NT, false>(kind, prelu, last);
   int per_cu = 0, dev = 0, cus = 0;
   if (!f) return 0;
-  const size_t dyn = kind == 17 ? dma_lds_bytes<NT>((int)(dyn_bytes / 4))
-                     : kind == 18 ? dma_lds_bytes<NT>((int)(dyn_bytes / 4), 4)
-                     : (kind == 1 || kind == 7 || kind == 10 || kind == 12 || kind == 15) ? eh_lds_bytes((int)(dyn_bytes / 4))
-                                                     : lds_bytes<NT>((int)(dyn_bytes / 4));
+  const size_t dyn = (kind == 1 || kind == 7 || kind == 10 || kind == 12) ? eh_lds_bytes((int)(dyn_bytes / 4))
+                                                                          : lds_bytes<NT>((int)(dyn_bytes / 4));
   if (dyn > 160 * 1024) return 0;
-  const int block = kind == 17 ? 64 * kDmaWaves
-                    : kind == 18 ? 64 * 4
-                    : kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
+  const int block = kind == 1 ? 64 * (loop ? (last ? edge_waves<NT, true, 1>() : edge_waves<NT, true, 0>()) : kWaves)
                     : kind == 10 ? 64 * kMlpWaves
-                    : kind == 15 ? 64 * kMlpPipeWaves
                     : kind == 13 ? 64 * 2 * NT
                     : kind == 14 ? 64 * kRowHopWaves
                     : kind == 2 ? 64 * (loop ? hop_waves<NT, true>() : kWaves)

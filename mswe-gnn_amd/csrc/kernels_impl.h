@@ -61,7 +61,6 @@ constexpr int edge_eu() { return LOOP && NT <= 2 ? edge_waves<NT, LOOP, LST>() /
 #include "kernels/k_base.h"
 #include "kernels/k_encode.h"
 #include "kernels/k_edge.h"
-#include "kernels/k_edge_dma.h"
 #include "kernels/k_coop_edge.h"
 #include "kernels/k_coop_encode.h"
 #include "kernels/k_hop.h"

@@ -152,8 +152,11 @@ struct ScaleCSR {
   int ntiles = 0;
   EdgeChunk* chunks = nullptr;  // [nchunks][16] dense edge chunks (k_edge_mlp)
   int nchunks = 0;
-  int* rptr = nullptr;          // row-layout middle hops (k_hop_rows, large scales): CSR by
-  int2* redge = nullptr;        // destination, {source row, s slot} per edge
+  int* rptr = nullptr;          // row-layout middle hops (k_hop_rows, large scales) and the
+  int2* redge = nullptr;        // one-workgroup chains (k_hop_wg, small scales): CSR by
+                                // destination, {source row, s slot} per edge
+  int maxdeg = 0;               // largest in-degree (with the CSR)
+  int4* wg_edges = nullptr;     // k_hop_wg: [ns][2] int4 {sources}, {s slots} (small scales)
 
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
   std::vector<LaneRec> hrecs;   // host copy of recs (fused pooling slots, PoolSlot)
@@ -278,18 +281,15 @@ struct Knobs {
   int coop2_direct = 1;     // MSW_COOP2_DIRECT    F = 64 two-wave edge hop, blob-read MLP: 0 / 1 / 2
   int coop2_f64 = 1;        // MSW_COOP2_F64       F = 64 two-wave edge hops: 0 off, 2 also for four
   int enc_coop = -1;        // MSW_ENC_COOP        cooperative encoder: -1 size rule, 0 / 1 force
-  int enc_coop_p = 0;       // MSW_ENC_COOP_P      F = 64 cooperative encoder on 2 waves per tile
-  int mlp_pipe = 0;         // MSW_MLP_PIPE        pipelined split edge MLP (1)
-  int mlp_stagger = 2;      // MSW_MLP_STAGGER     split edge MLP: waves 4..7 start n x 2 k cycles late
-                            //                     (k_edge_mlp 22.0 -> 21.2 us, profiles/r05/ab_f64_mlp_stagger.txt)
   int eh_loop = 0;          // MSW_EH_LOOP         grid-stride fused edge hops at any size
+  int hop_wg = 0;           // MSW_HOP_WG          one-workgroup hop chains on small scales (k_hop_wg):
+                            //                     0 off, 1 the middle hops, 2 + the last hop
   int hop_split = -1;       // MSW_HOP_SPLIT       feature-split middle hops: -1 = F = 64 rule
   int pool_wide = 1;        // MSW_POOL_WIDE       2F / 16 waves per pooling tile
   int tile_pack = 1;        // MSW_TILE_PACK       degree-aware destination order
   int xcd_max = 1;          // MSW_XCD_MAX         XCD packing of small grids (0 = all eight XCDs)
   int coop_waves = -1;      // MSW_COOP_WAVES      cooperative kernels while P x tiles <= this (-1 default)
   int epi_split_tiles = -1; // MSW_EPI_SPLIT_TILES row-epilogue threshold in edge tiles (-1 default)
-  int eh_dma = 0;           // MSW_EH_DMA          grid-stride edge hops with LDS-DMA prefetch (k_edge_hop_dma)
   int trace_encode = 0;     // MSW_TRACE_ENCODE    diagnostic builds (-DMSW_TRACE): encoder marks only
 };
 inline Knobs knobs_from_env() {
@@ -298,11 +298,10 @@ inline Knobs knobs_from_env() {
       {"MSW_SPLIT_EDGE_MLP", &k.split_edge_mlp}, {"MSW_POOL_FUSE", &k.pool_fuse},
       {"MSW_UNPOOL_FUSE", &k.unpool_fuse}, {"MSW_DEFER_DECODE", &k.defer_decode}, {"MSW_HOP_ROWS", &k.hop_rows},
       {"MSW_COOP2_DIRECT", &k.coop2_direct}, {"MSW_COOP2_F64", &k.coop2_f64}, {"MSW_ENC_COOP", &k.enc_coop},
-      {"MSW_ENC_COOP_P", &k.enc_coop_p}, {"MSW_MLP_PIPE", &k.mlp_pipe}, {"MSW_MLP_STAGGER", &k.mlp_stagger}, {"MSW_EH_LOOP", &k.eh_loop},
+      {"MSW_EH_LOOP", &k.eh_loop}, {"MSW_HOP_WG", &k.hop_wg},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
       {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
-      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode},
-      {"MSW_EH_DMA", &k.eh_dma}};
+      {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
   for (const auto& t : tab)
     if (const char* e = getenv(t.name)) *t.v = atoi(e);
   return k;
@@ -1003,6 +1002,58 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
   return MSW_OK;
 }
 
+// One-workgroup hop chains (k_hop_wg): on a scale of at most kWgRows rows whose in-degree is at
+// most kWgDeg (F <= 32, not on parts), consecutive hop launches of one layer become ONE launch
+// -- MSW_HOP_WG=1: the middle hops, =2 (default): the middle hops and the last hop with its
+// epilogue -- when the chain's LDS (epilogue region, filters, two row buffers) fits.  Runs
+// after relocate (the epilogue region's size) and before set_grid_cap.  Bit-identical to one
+// launch per hop (test_hop_chain_matches_launch_per_hop).
+size_t wg_lds_floats(const HopArgs& h, int NT) {
+  return (size_t)h.wg_foff + (size_t)h.wg_hops * NT * NT * 256 + 2 * (size_t)kWgRows * (16 * NT + 4);
+}
+void merge_wg_chains(msw_plan* P, std::vector<Launch>& q) {
+  if (P->kn.hop_wg <= 0 || P->part_rank >= 0 || P->NT > 2) return;
+  std::vector<Launch> out;
+  for (size_t i = 0; i < q.size();) {
+    const Launch& L0 = q[i];
+    const bool ok0 = L0.kind == L_HOP && !L0.hop.wg_hops && L0.scale >= 0 && L0.scale < P->S;
+    const ScaleCSR* g = ok0 ? &P->sc[L0.scale] : nullptr;
+    if (!ok0 || !g->wg_edges || g->ns > kWgRows || g->maxdeg > kWgDeg || g->ns <= 0) {
+      out.push_back(q[i++]);
+      continue;
+    }
+    // the run: hop launches of this scale, each reading what the previous one wrote
+    size_t j = i + 1;
+    while (j < q.size() && q[j].kind == L_HOP && q[j].scale == L0.scale && q[j].hop.in == q[j - 1].hop.out &&
+           !q[j - 1].hop.last)
+      ++j;
+    size_t end = j;  // [i, end): hops; drop the last hop unless mode 2
+    if (P->kn.hop_wg < 2 && q[end - 1].hop.last) --end;
+    const int n = (int)(end - i);
+    if (n < 2) {
+      for (size_t k = i; k < j; ++k) out.push_back(q[k]);
+      i = j;
+      continue;
+    }
+    Launch M = q[end - 1];  // the chain's last hop: its output, epilogue and staged region
+    HopArgs& h = M.hop;
+    h.in = q[i].hop.in;
+    h.wg_hops = n;
+    h.wg_foff = h.last ? (h.reg.len + kChunk - 1) / kChunk * kChunk : 0;
+    for (int k = 0; k < n; ++k) h.wg_filt[k] = q[i + k].hop.filt_a;
+    h.nrows = g->ns; h.rptr = g->rptr; h.redge = g->redge; h.wg_edges = g->wg_edges;
+    if (wg_lds_floats(h, P->NT) * sizeof(float) > 160 * 1024) {
+      for (size_t k = i; k < j; ++k) out.push_back(q[k]);
+      i = j;
+      continue;
+    }
+    out.push_back(M);
+    for (size_t k = end; k < j; ++k) out.push_back(q[k]);
+    i = j;
+  }
+  q.swap(out);
+}
+
 // Grid cap of a grid-stride launch: the workgroups the chip holds at once, so that each
 // stages its weight region once (large meshes) and none waits for a second wave of blocks.
 int resident_of(int NT, int kind, int prelu, int last, size_t bytes, int loop) {
@@ -1037,19 +1088,16 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       bool coop = P->NT == 4 && (long)(L.enc.Npad / kRowsPerWave) * P->NT <= kEncCoopWaves;
       if (P->kn.enc_coop >= 0) coop = P->NT >= 2 && P->kn.enc_coop != 0;
       L.enc.coop = coop ? P->NT : 0;
-      // MSW_ENC_COOP_P=2: F = 64 on two waves per row tile instead of four (bit-identity test)
-      if (coop && P->NT == 4 && P->kn.enc_coop_p == 2) L.enc.coop = 2;
       break;
     }
     case L_EDGE_MLP: {
-      // k_edge_mlp: two waves per SIMD, one chunk each.  (MSW_MLP_PIPE=1: k_edge_mlp_pipe, one
-      // wave per SIMD walking ~2 chunks, the next chunk's gathers in flight under the current
-      // chunk's MLP -- +0.4 % in round 3 while both read their operands through FLAT loads;
-      // with LDS-typed operands (round 4) it spills and the two-wave kernel is ahead:
-      // zenodo4_f64 27.76 / 27.91 -> 28.08 / 28.09 M, profiles/r04/ab_f64_lds_operands.txt)
-      L.eh.pipe = P->kn.mlp_pipe > 0;
-      L.eh.stagger = P->kn.mlp_stagger;
-      L.eh.max_blocks = resident_of(P->NT, L.eh.pipe ? 15 : 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
+      // k_edge_mlp: two waves per SIMD, one chunk each.  (A software-pipelined variant, one wave
+      // per SIMD walking ~2 chunks with the next chunk's gathers in flight, spilled once the
+      // operands were LDS-typed and lost: zenodo4_f64 27.76 / 27.91 vs 28.08 / 28.09 M,
+      // profiles/r04/ab_f64_lds_operands.txt; removed in round 6.)  Waves 4..7 start 2 x 2 k
+      // cycles late (k_edge_mlp 22.0 -> 21.2 us, profiles/r05/ab_f64_mlp_stagger.txt).
+      L.eh.stagger = kMlpStagger;
+      L.eh.max_blocks = resident_of(P->NT, 10, L.eh.c.prelu, 0, (size_t)L.eh.reg.len * 4, 1);
       break;
     }
     case L_EDGE_HOP: {
@@ -1093,24 +1141,15 @@ void set_grid_cap(msw_plan* P, Launch& L) {
         }
       }
       if ((a.pool.slots || a.pool.parent) && !a.coop) a.coop = 2;  // F = 64 fused: two waves per tile, any grid
-      // grid-stride first hops of K > 1 layers (F <= 32): the next tile's rows LDS-DMA'd during
-      // the current tile's MLP (k_edge_hop_dma) -- its layout assumes an edge term, a 2F-wide
-      // first layer, stored s and out rows, no skip, no epilogue, no fused (un)pooling
-      a.dma = 0;
-      a.dma_off = 0;
-      if (P->kn.eh_dma > 0 && P->NT <= 2 && loop && !a.coop && !a.last && a.Pe && a.h1t == 2 * P->NT &&
-          !a.own_zero && a.s && a.out && !a.skip && !a.pool.slots && !a.pool.parent) {
-        // MSW_EH_DMA=2: four waves per workgroup (one per SIMD) instead of eight
-        const int nb = resident_of(P->NT, P->kn.eh_dma == 2 ? 18 : 17, a.c.prelu, 0, (size_t)a.reg_nf * 4, 1);
-        if (nb > 0) {
-          a.dma = P->kn.eh_dma == 2 ? 2 : 1;
-          a.dma_off = (a.reg_nf + kChunk - 1) / kChunk * kChunk;
-          a.max_blocks = nb;
-        }
-      }
       break;
     }
     case L_HOP:
+      if (L.hop.wg_hops > 0) {  // one-workgroup chain (merge_wg_chains): one block, no variants
+        L.hop.max_blocks = L.hop.fit_blocks = 0;
+        L.hop.coop = L.hop.split = L.hop.rows = 0;
+        L.common().xcd_max = 0;
+        break;
+      }
       caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
       // one tile per wave below kHopLoopTiles: the grid-stride variant measured 1.1-1.6 % slower on the batch of 8 and
       // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
@@ -1301,7 +1340,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   HostGraph H;
   std::string err;
   int rc = build_host_graph(g, P->S, kRowsPerBlock, P->kn.tile_pack != 0,
-                            row_hops_forced(P) ? 0 : kRowHopMinTiles, H, err);
+                            row_hops_forced(P) ? 0 : kRowHopMinTiles, H, err, P->kn.hop_wg > 0 ? kWgRows : 0);
   if (rc) return fail(rc, err);
   P->N = H.N;
   P->E = H.E;
@@ -1313,10 +1352,19 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   for (int s = 0; s < S; ++s) {
     HostScale& h = H.sc[s];
     ScaleCSR& c = P->sc[s];
-    c.n0 = h.n0; c.ns = h.ns; c.E = h.E; c.ntiles = h.ntiles; c.nchunks = h.nchunks;
+    c.n0 = h.n0; c.ns = h.ns; c.E = h.E; c.ntiles = h.ntiles; c.nchunks = h.nchunks; c.maxdeg = h.maxdeg;
     if ((rc = pupload(P, &c.recs, h.recs))) return rc;
     if (c.nchunks > 0 && (rc = pupload(P, &c.chunks, h.chunks))) return rc;
     if (!h.rptr.empty() && ((rc = pupload(P, &c.rptr, h.rptr)) || (rc = pupload(P, &c.redge, h.redge)))) return rc;
+    if (!h.rptr.empty() && h.ns <= kWgRows && h.maxdeg <= kWgDeg) {  // k_hop_wg's per-row edge records
+      std::vector<int> we((size_t)std::max(h.ns, 1) * 8, -1);
+      for (int k = 0; k < h.ns; ++k)
+        for (int q = h.rptr[k], u = 0; q < h.rptr[k + 1]; ++q, ++u) {
+          we[(size_t)k * 8 + u] = h.redge[q].x - h.n0;
+          we[(size_t)k * 8 + 4 + u] = h.redge[q].y;
+        }
+      if ((rc = pupload(P, reinterpret_cast<int**>(&c.wg_edges), we))) return rc;
+    }
     c.porig = std::move(h.porig);
     c.hrecs = std::move(h.recs);
   }
@@ -1567,8 +1615,10 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     const bool mlp_only = P->NT > 2;  // F = 64: only the edge-MLP operands fit in LDS
     if ((rc = relocate(P.get(), P->sched_fwd, mlp_only)) || (rc = relocate(P.get(), P->sched_roll, mlp_only)))
       return rc;
-    for (auto* q : {&P->sched_fwd, &P->sched_roll})
+    for (auto* q : {&P->sched_fwd, &P->sched_roll}) {
+      merge_wg_chains(P.get(), *q);
       for (Launch& L : *q) set_grid_cap(P.get(), L);
+    }
     // every cooperative edge hop's staged region must fit the LDS its kernel was given; a
     // fused (un)pooling launch that does not (e.g. F = 32 with mlp_layers = 4: two edge MLPs
     // + the projection) falls back to the separate pooling / unpooling launches
@@ -2023,13 +2073,6 @@ int msw_plan_get_stats(const msw_plan* P, msw_plan_stats* s) {
   s->graph_captured = P->step_exec != nullptr || P->multi_exec != nullptr || P->fwd_exec != nullptr;
   s->rccl_calls = P->rccl_calls;
   s->rccl_steps = P->rccl_steps;
-  s->dma_edge_hops = 0;
-  for (const Launch& L : P->sched_roll) {
-    const EdgeHopArgs& a = L.eh;
-    if (L.kind == L_EDGE_HOP && a.dma && !a.last && a.fit_blocks > 0 && a.max_blocks > 0 &&
-        (a.ntiles + kWaves - 1) / kWaves > a.fit_blocks)
-      ++s->dma_edge_hops;
-  }
   return MSW_OK;
 }
 

@@ -69,8 +69,7 @@ class MswPlanStats(C.Structure):
                 ("hid_features", C.c_int32), ("padded_features", C.c_int32),
                 ("kernels_per_step", C.c_int32), ("forward_calls", C.c_int64),
                 ("rollout_steps", C.c_int64), ("device_bytes", C.c_int64),
-                ("graph_captured", C.c_int32), ("dma_edge_hops", C.c_int32),
-                ("rccl_calls", C.c_int64), ("rccl_steps", C.c_int64)]
+                ("graph_captured", C.c_int32), ("rccl_calls", C.c_int64), ("rccl_steps", C.c_int64)]
 
 
 class MswExchangeDesc(C.Structure):

@@ -618,15 +618,13 @@ def test_split_edge_mlp_matches_fused(cuda, F, monkeypatch):
     assert per_step_rel(outs["1"][3][:ga.num_nodes], ref) <= REL_TOL
 
 
-@pytest.mark.parametrize("F,P", [(32, None), (64, None), (64, "2")])
-def test_coop_encoder_matches_single_wave(cuda, F, P, monkeypatch):
+@pytest.mark.parametrize("F", [32, 64])
+def test_coop_encoder_matches_single_wave(cuda, F, monkeypatch):
     """k_encode_coop (F / 16 waves per 16-row tile, every MFMA layer's output tiles split over
     them; the F = 64 default while that leaves <= 4 waves per SIMD) == k_encode (MSW_ENC_COOP=0), bit
     for bit: forward (encoders, projection 0, unpool V) and rollout (the previous step's
     decoder in the encoder launch, the final decode-only launch); and vs the oracle."""
     g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=6), seed=7)
-    if P:  # F = 64 on two waves per row tile (MSW_ENC_COOP_P=2) instead of four
-        monkeypatch.setenv("MSW_ENC_COOP_P", P)
     outs = {}
     for sv in ("0", "1"):
         monkeypatch.setenv("MSW_ENC_COOP", sv)
@@ -640,6 +638,37 @@ def test_coop_encoder_matches_single_wave(cuda, F, P, monkeypatch):
     m = build_msgnn(4, F, 4)
     ref = orc.rollout(state_dict_of(m), orc.msgnn_config(num_scales=4, hid_features=F, K=4), g)
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
+
+
+@pytest.mark.parametrize("mesh,K,act", [("tiny", 4, "prelu"), ("small", 4, "prelu"), ("small", 3, "relu"),
+                                         ("zenodo4", 4, "prelu")])
+def test_hop_chain_matches_launch_per_hop(cuda, monkeypatch, mesh, K, act):
+    """One-workgroup hop chains (k_hop_wg: the hops of a layer on a scale of <= 256 rows in ONE
+    launch, rows kept in LDS between hops; MSW_HOP_WG=1 the middle hops, =2 also the last hop and
+    its epilogue) == one launch per hop (MSW_HOP_WG=0), bit for bit: a wet-start rollout and a
+    forward, with the shipped K4_F32 checkpoint (PReLU) and a seeded K = 3 ReLU model; on the
+    tiny / small meshes (chains on 3 / 2 scales) and zenodo4 (its 163-row coarsest scale)."""
+    from mswegnn.engine import EnginePlan
+    T = 6
+    g = wet_state(make_multiscale_mesh(**mesh_config(mesh), T=T), seed=2).to(cuda)
+    m = (build_msgnn(4, 32, 4, state=weights("K4_F32")) if act == "prelu"
+         else build_msgnn(4, 32, K, mlp_activation=act)).to(cuda)
+    outs, launches = [], []
+    for v in ("0", "1", "2"):
+        monkeypatch.setenv("MSW_HOP_WG", v)
+        plan = EnginePlan(m, g, cuda)
+        r = plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone()
+        launches.append(plan.stats()["kernels_per_step"])
+        y = plan.forward(g.x).clone()
+        outs.append((r, y))
+        plan.close()
+    print(mesh, K, act, "launches per step (off / middle / all):", launches)
+    assert launches[2] < launches[0] and launches[1] <= launches[0], launches
+    if K == 4:
+        assert launches[1] < launches[0], launches
+    for r, y in outs[1:]:
+        assert torch.equal(r, outs[0][0]), (r - outs[0][0]).abs().max().item()
+        assert torch.equal(y, outs[0][1]), (y - outs[0][1]).abs().max().item()
 
 
 @pytest.mark.parametrize("knob", ["MSW_XCD_MAX", "MSW_TILE_PACK"])
@@ -770,35 +799,6 @@ def test_grid_stride_edge_hops_match_one_tile_per_wave(cuda, monkeypatch, S, F, 
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("case", ["forced_small", "medium_natural"])
-def test_dma_edge_hops_match_grid_stride(cuda, monkeypatch, case):
-    """The LDS-DMA pipelined grid-stride fused edge MLP + hop (k_edge_hop_dma, MSW_EH_DMA=1:
-    the next tile's U / V / Pe and out rows gathered into the wave's LDS region during the
-    current tile's MLP, waits counted by hand) == the grid-stride k_edge_hop bit for bit over a
-    wet rollout: on the small 4-scale mesh with the grid-stride path forced (MSW_EH_LOOP=1, one
-    or two tiles per wave), and on a 115 k-node 3-scale mesh whose finest scale takes the
-    grid-stride path by size (~11 tiles per wave: the prefetch pipeline runs in steady state)."""
-    from mswegnn.engine import EnginePlan
-    T = 3
-    if case == "forced_small":
-        g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=4).to(cuda)
-        m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
-        monkeypatch.setenv("MSW_EH_LOOP", "1")
-    else:
-        g = wet_state(make_multiscale_mesh(n_coarse=60, num_scales=3, T=T), seed=5, all_wet=True).to(cuda)
-        m = build_msgnn(3, 32, 4).to(cuda)
-    outs, dma = [], []
-    for v in ("0", "1", "2"):  # 2: four waves per workgroup (one per SIMD) instead of eight
-        monkeypatch.setenv("MSW_EH_DMA", v)
-        plan = EnginePlan(m, g, cuda)
-        outs.append(plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone())
-        dma.append(plan.stats()["dma_edge_hops"])
-        plan.close()
-    assert dma[0] == 0 and dma[1] >= 1 and dma[2] == dma[1], dma
-    assert torch.equal(outs[0], outs[1])
-    assert torch.equal(outs[0], outs[2])
-
-
 def _built_variants():
     lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mswe-gnn_amd", "lib")
     names = sorted(f[len("libmswegnn_"):-3] for f in os.listdir(lib) if f.startswith("libmswegnn_") and
@@ -835,20 +835,17 @@ def test_build_variant_matches_default_bitwise(variant):
         assert res[0]["sha256"] == res[1]["sha256"], res
 
 
-@pytest.mark.parametrize("variant", ["mlp_pipe", "coop2_direct", "mlp_stagger"])
+@pytest.mark.parametrize("variant", ["coop2_direct"])
 def test_f64_kernel_variants_match_default(cuda, monkeypatch, variant):
     """F = 64 kernel variants == the default bit for bit over a wet-start rollout (forced on the
-    small mesh): k_edge_mlp_pipe (the split edge MLP with the next chunk's gathers in flight,
-    MSW_MLP_PIPE) against k_edge_mlp, the two-wave cooperative edge hop reading its MLP region
-    from the blob (MSW_COOP2_DIRECT=2) against the LDS-staged one, and k_edge_mlp's start
-    stagger (MSW_MLP_STAGGER=0 against 2)."""
+    small mesh): the two-wave cooperative edge hop reading its MLP region from the blob
+    (MSW_COOP2_DIRECT=2) against the LDS-staged one."""
     from mswegnn.engine import EnginePlan
     T = 6
     g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=4).to(cuda)
     m = build_msgnn(4, 64, 4).to(cuda)
-    base = {"mlp_pipe": {"MSW_SPLIT_EDGE_MLP": "1"}, "coop2_direct": {"MSW_COOP2_F64": "2"},
-            "mlp_stagger": {"MSW_SPLIT_EDGE_MLP": "1"}}[variant]
-    knob = {"mlp_pipe": "MSW_MLP_PIPE", "coop2_direct": "MSW_COOP2_DIRECT", "mlp_stagger": "MSW_MLP_STAGGER"}[variant]
+    base = {"coop2_direct": {"MSW_COOP2_F64": "2"}}[variant]
+    knob = {"coop2_direct": "MSW_COOP2_DIRECT"}[variant]
     for k, v in base.items():
         monkeypatch.setenv(k, v)
     outs = []

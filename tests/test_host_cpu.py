@@ -862,3 +862,15 @@ def test_bench_gpus_flag_launches_ranks_without_a_launcher():
     r = subprocess.run([sys.executable, bench_py, "--gpus", "2"], env=env_n, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 2 and "needs 2 GPUs" in r.stderr and "launching" not in r.stderr, r.stderr[-2000:]
+
+
+def test_cpu_batch_baseline_one_process_per_simulation():
+    """bench.cpu_batch_baseline: the batch's simulations run one per spawned
+    process over the CPU share, started together behind a barrier; the rate counts every
+    simulation's fine nodes x steps over the common wall time."""
+    import bench
+    rec = bench.cpu_batch_baseline("tiny", [0, 1], T=3, share=2, seconds=0.2, t1=0.05, t1_threads=2)
+    assert rec["processes"] == 2 and rec["threads_per_process"] == 1 and rec["cores"] == 2
+    assert rec["value"] > 0 and rec["unit"] == "fine-node-steps/s"
+    host, share = bench.cpu_share()
+    assert host == os.cpu_count() and 1 <= share <= 16

@@ -47,6 +47,20 @@ case $MODE in
     rm -rf $OUT/prof
     step rocprof 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > $OUT/bench_prof.json 2> $OUT/bench_prof.err
     python3 tools/step_breakdown.py $OUT/prof/run_kernel_trace.csv > $OUT/step_breakdown.txt 2>&1 ;;
+  divab)  # the shared-reciprocal division: exactness sweep, bit-identity of the variants, A/B
+    step div_check 120 ./tools/div_check > $OUT/div_check.txt 2>&1
+    step variants 600 $PYT tests/test_gpu_parity.py -m gpu -k "build_variant" > $OUT/variants.txt 2>&1
+    # (the nofastdiv variant predates the hop chains: MSW_HOP_WG=0 on the default library)
+    step ab_hbm1m 900 bash tools/ab.sh "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" -- --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1
+    cp gpurun_out/ab.log $OUT/ab_hbm1m.txt
+    step ab_zenodo4 600 bash tools/ab.sh "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv"
+    cp gpurun_out/ab.log $OUT/ab_zenodo4.txt ;;
+  chain)  # one-workgroup hop chains: bit identity, then the A/B on zenodo4 and the batch of 8
+    step chain_tests 600 $PYT tests/test_gpu_parity.py -m gpu -k "hop_chain or partitioned or group_rollout" > $OUT/chain_tests.txt 2>&1
+    step ab_chain 900 bash tools/ab.sh "MSW_HOP_WG=0" "MSW_HOP_WG=1" "MSW_HOP_WG=2" "MSW_HOP_WG=0" "MSW_HOP_WG=1" "MSW_HOP_WG=2"
+    cp gpurun_out/ab.log $OUT/ab_chain_zenodo4.txt ;;
+  cputhreads)
+    step cpu_threads 600 python tools/cpu_threads.py > $OUT/cpu_threads.json 2> $OUT/cpu_threads.err ;;
   *)
     echo "unknown mode $MODE" >&2; exit 2 ;;
 esac
