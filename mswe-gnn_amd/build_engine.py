@@ -61,10 +61,9 @@ def build(force=False, verbose=True, variant=""):
     # build variants: the -DMSW_TRACE diagnostic library, and the speed A/Bs of the current
     # round (each bit-identical to the default: test_build_variant_matches_default_bitwise)
     extra = {"trace": ["-DMSW_TRACE"],
-             # the VALU diets of rounds 5-6 all off (PReLU as max, FULL edge kernels, shared-reciprocal
-             # division): test_build_variant_matches_default_bitwise[valubase]
-             "valubase": ["-DMSW_PRELU_MAX=0", "-DMSW_EDGE_FULL=0", "-DMSW_FAST_DIV=0"],
-             "nofastdiv": ["-DMSW_FAST_DIV=0"]}.get(variant, [])
+             # the round-5 VALU diets off (PReLU as max, FULL edge kernels):
+             # test_build_variant_matches_default_bitwise[valubase]
+             "valubase": ["-DMSW_PRELU_MAX=0", "-DMSW_EDGE_FULL=0"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     out = lib_path(variant)

@@ -220,17 +220,7 @@ struct HopArgs {
   int nrows;         // destinations of the scale (local rows [0, nrows) = internal n0 + k)
   const int* rptr;   // [nrows + 1] CSR offsets (local destination order)
   const int2* redge; // [E] {internal source row, tile-padded s slot}, reference edge order
-  // one-workgroup hop chain (k_hop_wg, small scales): wg_hops > 0 hops in this launch, from
-  // `in` (the first hop's input) to `out`, with filters wg_filt[] (blob offsets, -1 = none)
-  // copied to LDS at float offset wg_foff (after the staged epilogue region of a LAST chain)
-  int wg_hops, wg_foff;
-  int wg_filt[MSW_MAX_HOPS];
-  const int4* wg_edges;  // per local row: {source local row, tile-padded s slot} x kWgDeg as two
-                         // int4 (sources, slots; -1 = no edge), one load each, no CSR round trip
 };
-constexpr int kWgWaves = 16;   // k_hop_wg: one workgroup, one 16-row tile per wave
-constexpr int kWgRows = 16 * kWgWaves;
-constexpr int kWgDeg = 4;      // in-edges per destination held in registers
 
 // Mean pooling into the coarse rows + projection of the next processor.
 

@@ -71,10 +71,8 @@ struct HostScale {
   std::vector<LaneRec> recs;     // [ntiles][16]
   std::vector<EdgeChunk> chunks; // [nchunks][16]
   std::vector<int> porig;        // tile-padded edge slot -> original edge id, -1 = padding
-  std::vector<int> rptr;         // row layout (large scales, and the small ones of the
-                                 // one-workgroup hop chain): CSR offsets by local destination
+  std::vector<int> rptr;         // row layout (large scales): CSR offsets by local destination
   std::vector<I2> redge;         //   {internal source row, tile-padded s slot} per CSR edge
-  int maxdeg = 0;                // largest in-degree (with the CSR)
 };
 struct HostLevel {               // level l: coarse scale l + 1, fine scale l
   int I = 0;
@@ -168,10 +166,10 @@ inline std::vector<LaneRec> make_recs(const std::vector<int>& rowptr, const std:
 // The whole host graph plan.  align: scale starts are padded to multiples of this many rows
 // (the encoder's workgroup rows: a workgroup never straddles two scales); pack: destinations
 // in tiling.h pack_order (else graph order); row_min_tiles: scales with at least this many
-// edge tiles get the row-layout CSR (0: every scale), and so do scales of at most
-// row_max_rows rows (k_hop_wg).  Returns MSW_OK or an MSW_ERR_* code with `err` set.
+// edge tiles get the row-layout CSR (0: every scale).  Returns MSW_OK or an MSW_ERR_* code
+// with `err` set.
 inline int build_host_graph(const msw_graph_desc* g, int S, int align, bool pack, int row_min_tiles, HostGraph& H,
-                            std::string& err, int row_max_rows = 0) {
+                            std::string& err) {
   auto bad = [&](int code, const std::string& m) {
     err = m;
     return code;
@@ -262,14 +260,13 @@ inline int build_host_graph(const msw_graph_desc* g, int S, int align, bool pack
         c.chunks.push_back(EdgeChunk{c.recs[q].src, c.recs[q / kRowsPerWave * kRowsPerWave + c.recs[q].dl].n, (int)q, 0});
     c.nchunks = (int)((c.chunks.size() + kRowsPerWave - 1) / kRowsPerWave);
     c.chunks.resize((size_t)c.nchunks * kRowsPerWave, EdgeChunk{-1, -1, -1, 0});
-    if (c.ntiles >= row_min_tiles || c.ns <= row_max_rows) {  // row-layout hops: CSR + s slots
+    if (c.ntiles >= row_min_tiles) {  // row-layout middle hops: CSR + s slots
       std::vector<int> slot_of_csr(c.E, -1);
       for (size_t q = 0; q < pcsr.size(); ++q)
         if (pcsr[q] >= 0) slot_of_csr[pcsr[q]] = (int)q;
       c.rptr = rowptr;
       c.redge.resize(std::max(c.E, 1), I2{0, 0});
       for (int i = 0; i < c.E; ++i) c.redge[i] = I2{so[i], slot_of_csr[i]};
-      for (size_t k = 0; k + 1 < rowptr.size(); ++k) c.maxdeg = std::max(c.maxdeg, rowptr[k + 1] - rowptr[k]);
     }
   }
   // intra-scale levels

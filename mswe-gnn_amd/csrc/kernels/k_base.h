@@ -22,34 +22,9 @@ __device__ __forceinline__ float row_sum(float v) {
 }
 
 // s_ij / ||s_ij||, NaN -> 0 (gnn.py:424-426) over one edge row held as NT f32x4 per lane (the
-// 4 lane groups of the row together), IEEE division.  The compiler's f32 division is 11 VALU
-// per element: v_div_scale of both operands, rcp + one Newton step of the reciprocal, the
-// quotient with two residual corrections, v_div_fmas and v_div_fixup, plus 2 for the NaN select.
-// Where v_div_scale leaves both operands unscaled and v_div_fixup returns the quotient -- the
-// norm in [2^-40, 2^40] and every |s| >= 2^-80, so 1/norm, s/norm and s are far from the
-// subnormal range and nothing is 0, inf or NaN -- that sequence reduces to the same
-// instructions on the same operands without them: the reciprocal (rcp + Newton) is shared by
-// the row's elements, 5 VALU per element, no NaN select.  Bit-identical by construction
-// (test_fast_division_matches_ieee_division, tools/div_check.hip); other rows run the full
-// sequence.
-#ifndef MSW_FAST_DIV
-#define MSW_FAST_DIV 1  // 0: the compiler's division on every row (A/B build variant)
-#endif
-__device__ __forceinline__ float div_shared(float n, float d, float r) {
-#pragma clang fp contract(off)
-  float q = n * r;
-  float x = __builtin_fmaf(-d, q, n);
-  q = __builtin_fmaf(x, r, q);
-  x = __builtin_fmaf(-d, q, n);
-  return __builtin_fmaf(x, r, q);
-}
-__device__ __forceinline__ bool div_fast_ok(float d, float amin) {
-  return d >= 0x1p-40f && d <= 0x1p40f && amin >= 0x1p-80f;  // false for NaN
-}
-__device__ __forceinline__ float div_recip(float d) {
-  const float r0 = __builtin_amdgcn_rcpf(d);
-  return __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);
-}
+// 4 lane groups of the row together), IEEE division.  (Round 6 measured a shared-reciprocal form
+// of the compiler's division sequence -- 5 instead of 11 VALU per element, bit-identical -- and
+// it ran slower: profiles/r06/ab_fastdiv.txt.)
 template <int NT>
 __device__ __forceinline__ void normalize_s(f32x4 (&sv)[NT]) {
 #pragma clang fp contract(off)
@@ -57,33 +32,14 @@ __device__ __forceinline__ void normalize_s(f32x4 (&sv)[NT]) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) ss += hsum(sv[t] * sv[t]);
   const float nrm = sqrtf(row_sum(ss));
-  bool fast = false;
-  if constexpr (MSW_FAST_DIV) {
-    float amin = fminf(fminf(fabsf(sv[0].x), fabsf(sv[0].y)), fminf(fabsf(sv[0].z), fabsf(sv[0].w)));
 #pragma unroll
-    for (int t = 1; t < NT; ++t)
-      amin = fminf(amin, fminf(fminf(fabsf(sv[t].x), fabsf(sv[t].y)), fminf(fabsf(sv[t].z), fabsf(sv[t].w))));
-    fast = div_fast_ok(nrm, amin);
-  }
-  if (fast) {
-    const float r = div_recip(nrm);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      sv[t].x = div_shared(sv[t].x, nrm, r);
-      sv[t].y = div_shared(sv[t].y, nrm, r);
-      sv[t].z = div_shared(sv[t].z, nrm, r);
-      sv[t].w = div_shared(sv[t].w, nrm, r);
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      f32x4 q = sv[t] / nrm;
-      q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
-      q.y = (q.y == q.y) ? q.y : 0.f;
-      q.z = (q.z == q.z) ? q.z : 0.f;
-      q.w = (q.w == q.w) ? q.w : 0.f;
-      sv[t] = q;
-    }
+  for (int t = 0; t < NT; ++t) {
+    f32x4 q = sv[t] / nrm;
+    q.x = (q.x == q.x) ? q.x : 0.f;  // masked_fill_(isnan, 0)
+    q.y = (q.y == q.y) ? q.y : 0.f;
+    q.z = (q.z == q.z) ? q.z : 0.f;
+    q.w = (q.w == q.w) ? q.w : 0.f;
+    sv[t] = q;
   }
 }
 

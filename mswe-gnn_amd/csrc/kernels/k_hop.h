@@ -220,149 +220,6 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------- one-workgroup hop chain
-// Consecutive hops of one layer on a scale small enough for ONE workgroup (zenodo4's coarsest
-// scale: 163 rows, 11 row tiles): the layer's rows stay in LDS between hops (ping-pong), so
-// hop k + 1 follows hop k after a workgroup barrier instead of a kernel boundary (a dependent
-// launch costs ~4.5 us on this chip; a whole row-layout hop of 16 rows per wave from LDS well
-// under 1 us).  Row layout as k_hop_rows (a wave owns 16 consecutive destinations, each lane
-// row pulls its in-edges from the scale's CSR); every in-edge's source row index and s row are
-// loaded ONCE into registers and serve every hop (in-degree <= kWgDeg); the hops' filters are
-// copied into LDS at the start.  LAST: the chain ends with the layer's last hop and its
-// epilogue (node_epilogue on the 16-row tiles, as k_epi), else with a middle hop whose rows go
-// to `out`.  Arithmetic: k_hop_rows' (= k_hop's) operation for operation -- bit-identical.
-// LDS: [epilogue region (LAST)] [wg_hops filters] [state 0] [state 1], rows padded to F + 4.
-// Waves: 16 (one row tile each) for a chain of middle hops; 8 (two row tiles each, 256 VGPRs)
-// when it ends with the epilogue, whose MFMA chains do not fit 128 VGPRs beside the tiles' s rows.
-template <bool LAST> constexpr int wg_waves() { return LAST ? kWgWaves / 2 : kWgWaves; }
-template <int NT, int ACT, bool LAST>
-__global__ __launch_bounds__(64 * wg_waves<LAST>()) void k_hop_wg(HopArgs a) {
-#pragma clang fp contract(off)
-  constexpr int F = 16 * NT, FS = F + 4, FW = NT * NT * 256;
-  constexpr int WV = wg_waves<LAST>(), TPW = kWgWaves / WV;  // row tiles per wave
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15, w = wave_id();
-  Common c = a.c;
-  MSW_MARK(c, 0);
-  float* Wf = smem + a.wg_foff;
-  float* S0 = Wf + a.wg_hops * FW;
-  float* S1 = S0 + kWgRows * FS;
-  if constexpr (LAST && kStaged<NT>) stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
-  // every global load of the prologue is issued before the first LDS store: the layer's rows
-  // (RPT float4 per thread), the hops' filters (FPT), the tiles' edge records, then their s rows
-  constexpr int RPT = kWgRows * (F / 4) / (64 * WV), FPT = (MSW_MAX_HOPS * FW / 4 + 64 * WV - 1) / (64 * WV);
-  f32x4 rv[RPT], fv[FPT];
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) {
-    const int i = threadIdx.x + r * 64 * WV;
-    rv[r] = i < a.nrows * (F / 4) ? ld4(a.in + (size_t)(a.n0 + i / (F / 4)) * F + 4 * (i % (F / 4))) : zero4();
-  }
-#pragma unroll
-  for (int r = 0; r < FPT; ++r) {
-    const int i = threadIdx.x + r * 64 * WV, h = i / (FW / 4);
-    const int fa = h < a.wg_hops && a.wg_filt[h] >= 0 ? a.wg_filt[h] : 0;
-    fv[r] = h < a.wg_hops ? ld4(a.c.W + fa + 4 * (i % (FW / 4))) : zero4();
-  }
-  // this wave's row tiles w, w + WV, ... (nrows <= kWgRows): their in-edges into registers
-  int kc[TPW], deg[TPW], dmax[TPW], src[TPW][kWgDeg];
-  bool valid[TPW];
-  f32x4 sv[TPW][kWgDeg][NT];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int k = 16 * (w + i * WV) + j;
-    valid[i] = k < a.nrows;
-    kc[i] = valid[i] ? k : 0;
-    const int4 es = a.wg_edges[2 * kc[i]], ep = a.wg_edges[2 * kc[i] + 1];  // in-edges in CSR order
-    const int sr[4] = {es.x, es.y, es.z, es.w}, sl[4] = {ep.x, ep.y, ep.z, ep.w};
-    deg[i] = valid[i] ? (sr[0] >= 0) + (sr[1] >= 0) + (sr[2] >= 0) + (sr[3] >= 0) : 0;
-    int dm = deg[i];  // wave-uniform trip count
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) dm = max(dm, __shfl_xor(dm, o));
-    dmax[i] = dm;
-#pragma unroll
-    for (int u = 0; u < kWgDeg; ++u) {  // absent edges read the row's own entries (never used)
-      const bool on = u < deg[i];
-      src[i][u] = on ? sr[u] : kc[i];
-      load_row<NT>(sv[i][u], a.s + (size_t)(on ? sl[u] : 0) * F, g);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) {  // the layer's rows -> state 0
-    const int i = threadIdx.x + r * 64 * WV;
-    if (i < a.nrows * (F / 4)) st4(S0 + (i / (F / 4)) * FS + 4 * (i % (F / 4)), rv[r]);
-  }
-#pragma unroll
-  for (int r = 0; r < FPT; ++r) {  // filters (packed A operands) -> LDS
-    const int i = threadIdx.x + r * 64 * WV;
-    if (i / (FW / 4) < a.wg_hops) st4(Wf + 4 * i, fv[r]);
-  }
-  __syncthreads();  // rows, filters and the staged epilogue operands have landed
-  if constexpr (LAST && kStaged<NT>) c.W = smem;
-  MSW_MARK(c, 1);
-  for (int h = 0; h < a.wg_hops; ++h) {
-    const float* in = (h & 1) ? S1 : S0;
-    float* nx = (h & 1) ? S0 : S1;
-    const bool end = h + 1 == a.wg_hops;
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      if (16 * (w + i * WV) >= a.nrows) continue;  // wave-uniform
-      // the epilogue's row inputs: issued at the start of the chain's last hop, live only there
-      [[maybe_unused]] EpiPre<NT> pre;
-      if constexpr (LAST)
-        if (end) epi_prefetch<NT>(pre, a.epi, a.c, a.xs, (size_t)(a.n0 + kc[i]), g);
-      f32x4 od[NT];
-      load_row<NT>(od, in + kc[i] * FS, g);
-      float rd = 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) rd += hsum(od[t]);
-      const bool zd = row_sum(rd) != 0.f;
-      f32x4 agg[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) agg[t] = zero4();
-#pragma unroll
-      for (int u = 0; u < kWgDeg; ++u) {
-        if (u >= dmax[i]) break;
-        f32x4 os[NT];
-        load_row<NT>(os, in + src[i][u] * FS, g);
-        float rs = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) rs += hsum(os[t]);
-        const bool act = (row_sum(rs) != 0.f) || zd;  // gnn.py:408-411
-        const bool hs = u < deg[i];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          f32x4 gv;
-          if (a.grad) {
-            gv = od[t] - os[t];
-            if (a.upwind) {
-              gv.x = gv.x < 0.f ? 0.f : gv.x; gv.y = gv.y < 0.f ? 0.f : gv.y;
-              gv.z = gv.z < 0.f ? 0.f : gv.z; gv.w = gv.w < 0.f ? 0.f : gv.w;
-            }
-          } else {
-            gv = os[t];
-          }
-          const f32x4 m = act ? gv * sv[i][u][t] : zero4();
-          const f32x4 sum = agg[t] + m;
-          agg[t] = hs ? sum : agg[t];
-        }
-      }
-      f32x4 res[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) res[t] = od[t];
-      apply_filter<NT>(res, agg, a.wg_filt[h] >= 0 ? h * FW : -1, Wf, lane);
-      if (!end) {
-        if (valid[i]) store_row<NT>(nx + kc[i] * FS, res, NT, g);
-      } else if constexpr (LAST) {
-        node_epilogue<NT, ACT>(res, a.epi, c, pre, a.out, a.n0 + kc[i], valid[i], lane, g);
-      } else {
-        if (valid[i]) store_row<NT>(a.out + (size_t)(a.n0 + kc[i]) * F, res, NT, g);
-      }
-    }
-    if (!end) __syncthreads();
-  }
-  MSW_MARK(c, 9);
-}
-
 // ---------------------------------------------------------------------------- feature-split middle hop
 // A middle hop (no epilogue) with each edge tile's features split over two waves: rank r
 // gathers, messages and sums features [F r / 2, F (r + 1) / 2) only (half the loads per wave,

@@ -37,13 +37,6 @@ hipError_t prepare_kernels() {
     hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, mx(f.second));
     if (e != hipSuccess) return e;
   }
-  if constexpr (kStaged<NT>) {  // one-workgroup hop chains: all of their LDS is dynamic
-    for (const void* f : {(const void*)k_hop_wg<NT, 1, false>, (const void*)k_hop_wg<NT, 1, true>,
-                          (const void*)k_hop_wg<NT, -1, true>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      if (e != hipSuccess) return e;
-    }
-  }
   for (const void* f : {(const void*)k_edge_mlp<NT, 1>, (const void*)k_edge_mlp<NT, -1>}) {  // no slab
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
@@ -205,19 +198,6 @@ hipError_t launch_hop_kernel(const HopArgs& a, bool loop, dim3 grid, dim3 block,
 template <int NT>
 hipError_t launch_hop(const HopArgs& a, hipStream_t st) {
   if (a.ntiles <= 0) return hipSuccess;
-  if (a.wg_hops > 0) {  // one-workgroup hop chain (plan.hip merge_wg_chains: F <= 32 only)
-    if constexpr (kStaged<NT>) {
-      const size_t sh = ((size_t)a.wg_foff + (size_t)a.wg_hops * NT * NT * 256 + 2 * (size_t)kWgRows * (16 * NT + 4)) *
-                        sizeof(float);
-      if (sh > 160 * 1024 || a.nrows > kWgRows) return hipErrorInvalidValue;
-      const void* f = !a.last ? (const void*)k_hop_wg<NT, 1, false>
-                    : a.c.prelu ? (const void*)k_hop_wg<NT, 1, true> : (const void*)k_hop_wg<NT, -1, true>;
-      HopArgs b = a;
-      void* args[] = {&b};
-      return hipLaunchKernel(f, dim3(1), dim3(64 * (a.last ? wg_waves<true>() : wg_waves<false>())), args, sh, st);
-    }
-    return hipErrorInvalidValue;
-  }
   if (a.coop > 1 && a.last) {  // waves per tile = NT (2 for F = 32, 4 for F = 64)
     const void* f = hop_coop_kernel<NT>(a.c.prelu);
     if (!f) return hipErrorInvalidValue;

@@ -152,11 +152,8 @@ struct ScaleCSR {
   int ntiles = 0;
   EdgeChunk* chunks = nullptr;  // [nchunks][16] dense edge chunks (k_edge_mlp)
   int nchunks = 0;
-  int* rptr = nullptr;          // row-layout middle hops (k_hop_rows, large scales) and the
-  int2* redge = nullptr;        // one-workgroup chains (k_hop_wg, small scales): CSR by
-                                // destination, {source row, s slot} per edge
-  int maxdeg = 0;               // largest in-degree (with the CSR)
-  int4* wg_edges = nullptr;     // k_hop_wg: [ns][2] int4 {sources}, {s slots} (small scales)
+  int* rptr = nullptr;          // row-layout middle hops (k_hop_rows, large scales): CSR by
+  int2* redge = nullptr;        // destination, {source row, s slot} per edge
 
   std::vector<int> porig;       // tile-padded edge slot -> original edge id, -1 = padding
   std::vector<LaneRec> hrecs;   // host copy of recs (fused pooling slots, PoolSlot)
@@ -282,8 +279,6 @@ struct Knobs {
   int coop2_f64 = 1;        // MSW_COOP2_F64       F = 64 two-wave edge hops: 0 off, 2 also for four
   int enc_coop = -1;        // MSW_ENC_COOP        cooperative encoder: -1 size rule, 0 / 1 force
   int eh_loop = 0;          // MSW_EH_LOOP         grid-stride fused edge hops at any size
-  int hop_wg = 0;           // MSW_HOP_WG          one-workgroup hop chains on small scales (k_hop_wg):
-                            //                     0 off, 1 the middle hops, 2 + the last hop
   int hop_split = -1;       // MSW_HOP_SPLIT       feature-split middle hops: -1 = F = 64 rule
   int pool_wide = 1;        // MSW_POOL_WIDE       2F / 16 waves per pooling tile
   int tile_pack = 1;        // MSW_TILE_PACK       degree-aware destination order
@@ -298,7 +293,7 @@ inline Knobs knobs_from_env() {
       {"MSW_SPLIT_EDGE_MLP", &k.split_edge_mlp}, {"MSW_POOL_FUSE", &k.pool_fuse},
       {"MSW_UNPOOL_FUSE", &k.unpool_fuse}, {"MSW_DEFER_DECODE", &k.defer_decode}, {"MSW_HOP_ROWS", &k.hop_rows},
       {"MSW_COOP2_DIRECT", &k.coop2_direct}, {"MSW_COOP2_F64", &k.coop2_f64}, {"MSW_ENC_COOP", &k.enc_coop},
-      {"MSW_EH_LOOP", &k.eh_loop}, {"MSW_HOP_WG", &k.hop_wg},
+      {"MSW_EH_LOOP", &k.eh_loop},
       {"MSW_HOP_SPLIT", &k.hop_split}, {"MSW_POOL_WIDE", &k.pool_wide}, {"MSW_TILE_PACK", &k.tile_pack},
       {"MSW_XCD_MAX", &k.xcd_max}, {"MSW_COOP_WAVES", &k.coop_waves},
       {"MSW_EPI_SPLIT_TILES", &k.epi_split_tiles}, {"MSW_TRACE_ENCODE", &k.trace_encode}};
@@ -1002,58 +997,6 @@ int relocate(msw_plan* P, std::vector<Launch>& q, bool mlp_only = false) {
   return MSW_OK;
 }
 
-// One-workgroup hop chains (k_hop_wg): on a scale of at most kWgRows rows whose in-degree is at
-// most kWgDeg (F <= 32, not on parts), consecutive hop launches of one layer become ONE launch
-// -- MSW_HOP_WG=1: the middle hops, =2 (default): the middle hops and the last hop with its
-// epilogue -- when the chain's LDS (epilogue region, filters, two row buffers) fits.  Runs
-// after relocate (the epilogue region's size) and before set_grid_cap.  Bit-identical to one
-// launch per hop (test_hop_chain_matches_launch_per_hop).
-size_t wg_lds_floats(const HopArgs& h, int NT) {
-  return (size_t)h.wg_foff + (size_t)h.wg_hops * NT * NT * 256 + 2 * (size_t)kWgRows * (16 * NT + 4);
-}
-void merge_wg_chains(msw_plan* P, std::vector<Launch>& q) {
-  if (P->kn.hop_wg <= 0 || P->part_rank >= 0 || P->NT > 2) return;
-  std::vector<Launch> out;
-  for (size_t i = 0; i < q.size();) {
-    const Launch& L0 = q[i];
-    const bool ok0 = L0.kind == L_HOP && !L0.hop.wg_hops && L0.scale >= 0 && L0.scale < P->S;
-    const ScaleCSR* g = ok0 ? &P->sc[L0.scale] : nullptr;
-    if (!ok0 || !g->wg_edges || g->ns > kWgRows || g->maxdeg > kWgDeg || g->ns <= 0) {
-      out.push_back(q[i++]);
-      continue;
-    }
-    // the run: hop launches of this scale, each reading what the previous one wrote
-    size_t j = i + 1;
-    while (j < q.size() && q[j].kind == L_HOP && q[j].scale == L0.scale && q[j].hop.in == q[j - 1].hop.out &&
-           !q[j - 1].hop.last)
-      ++j;
-    size_t end = j;  // [i, end): hops; drop the last hop unless mode 2
-    if (P->kn.hop_wg < 2 && q[end - 1].hop.last) --end;
-    const int n = (int)(end - i);
-    if (n < 2) {
-      for (size_t k = i; k < j; ++k) out.push_back(q[k]);
-      i = j;
-      continue;
-    }
-    Launch M = q[end - 1];  // the chain's last hop: its output, epilogue and staged region
-    HopArgs& h = M.hop;
-    h.in = q[i].hop.in;
-    h.wg_hops = n;
-    h.wg_foff = h.last ? (h.reg.len + kChunk - 1) / kChunk * kChunk : 0;
-    for (int k = 0; k < n; ++k) h.wg_filt[k] = q[i + k].hop.filt_a;
-    h.nrows = g->ns; h.rptr = g->rptr; h.redge = g->redge; h.wg_edges = g->wg_edges;
-    if (wg_lds_floats(h, P->NT) * sizeof(float) > 160 * 1024) {
-      for (size_t k = i; k < j; ++k) out.push_back(q[k]);
-      i = j;
-      continue;
-    }
-    out.push_back(M);
-    for (size_t k = end; k < j; ++k) out.push_back(q[k]);
-    i = j;
-  }
-  q.swap(out);
-}
-
 // Grid cap of a grid-stride launch: the workgroups the chip holds at once, so that each
 // stages its weight region once (large meshes) and none waits for a second wave of blocks.
 int resident_of(int NT, int kind, int prelu, int last, size_t bytes, int loop) {
@@ -1144,12 +1087,6 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       break;
     }
     case L_HOP:
-      if (L.hop.wg_hops > 0) {  // one-workgroup chain (merge_wg_chains): one block, no variants
-        L.hop.max_blocks = L.hop.fit_blocks = 0;
-        L.hop.coop = L.hop.split = L.hop.rows = 0;
-        L.common().xcd_max = 0;
-        break;
-      }
       caps(P, L.hop, 2, L.hop.c.prelu, L.hop.last, L.hop.reg.len);
       // one tile per wave below kHopLoopTiles: the grid-stride variant measured 1.1-1.6 % slower on the batch of 8 and
       // dk15, equal on the 1M-node mesh whose finest hop alone it runs 3 % faster
@@ -1340,7 +1277,7 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   HostGraph H;
   std::string err;
   int rc = build_host_graph(g, P->S, kRowsPerBlock, P->kn.tile_pack != 0,
-                            row_hops_forced(P) ? 0 : kRowHopMinTiles, H, err, P->kn.hop_wg > 0 ? kWgRows : 0);
+                            row_hops_forced(P) ? 0 : kRowHopMinTiles, H, err);
   if (rc) return fail(rc, err);
   P->N = H.N;
   P->E = H.E;
@@ -1352,19 +1289,10 @@ int build_graph_plan(msw_plan* P, const msw_graph_desc* g) {
   for (int s = 0; s < S; ++s) {
     HostScale& h = H.sc[s];
     ScaleCSR& c = P->sc[s];
-    c.n0 = h.n0; c.ns = h.ns; c.E = h.E; c.ntiles = h.ntiles; c.nchunks = h.nchunks; c.maxdeg = h.maxdeg;
+    c.n0 = h.n0; c.ns = h.ns; c.E = h.E; c.ntiles = h.ntiles; c.nchunks = h.nchunks;
     if ((rc = pupload(P, &c.recs, h.recs))) return rc;
     if (c.nchunks > 0 && (rc = pupload(P, &c.chunks, h.chunks))) return rc;
     if (!h.rptr.empty() && ((rc = pupload(P, &c.rptr, h.rptr)) || (rc = pupload(P, &c.redge, h.redge)))) return rc;
-    if (!h.rptr.empty() && h.ns <= kWgRows && h.maxdeg <= kWgDeg) {  // k_hop_wg's per-row edge records
-      std::vector<int> we((size_t)std::max(h.ns, 1) * 8, -1);
-      for (int k = 0; k < h.ns; ++k)
-        for (int q = h.rptr[k], u = 0; q < h.rptr[k + 1]; ++q, ++u) {
-          we[(size_t)k * 8 + u] = h.redge[q].x - h.n0;
-          we[(size_t)k * 8 + 4 + u] = h.redge[q].y;
-        }
-      if ((rc = pupload(P, reinterpret_cast<int**>(&c.wg_edges), we))) return rc;
-    }
     c.porig = std::move(h.porig);
     c.hrecs = std::move(h.recs);
   }
@@ -1615,10 +1543,8 @@ int plan_create_impl(const msw_graph_desc* g, const msw_model_desc* m, int devic
     const bool mlp_only = P->NT > 2;  // F = 64: only the edge-MLP operands fit in LDS
     if ((rc = relocate(P.get(), P->sched_fwd, mlp_only)) || (rc = relocate(P.get(), P->sched_roll, mlp_only)))
       return rc;
-    for (auto* q : {&P->sched_fwd, &P->sched_roll}) {
-      merge_wg_chains(P.get(), *q);
+    for (auto* q : {&P->sched_fwd, &P->sched_roll})
       for (Launch& L : *q) set_grid_cap(P.get(), L);
-    }
     // every cooperative edge hop's staged region must fit the LDS its kernel was given; a
     // fused (un)pooling launch that does not (e.g. F = 32 with mlp_layers = 4: two edge MLPs
     // + the projection) falls back to the separate pooling / unpooling launches

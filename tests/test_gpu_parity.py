@@ -640,37 +640,6 @@ def test_coop_encoder_matches_single_wave(cuda, F, monkeypatch):
     assert per_step_rel(outs["1"][1], ref) <= REL_TOL
 
 
-@pytest.mark.parametrize("mesh,K,act", [("tiny", 4, "prelu"), ("small", 4, "prelu"), ("small", 3, "relu"),
-                                         ("zenodo4", 4, "prelu")])
-def test_hop_chain_matches_launch_per_hop(cuda, monkeypatch, mesh, K, act):
-    """One-workgroup hop chains (k_hop_wg: the hops of a layer on a scale of <= 256 rows in ONE
-    launch, rows kept in LDS between hops; MSW_HOP_WG=1 the middle hops, =2 also the last hop and
-    its epilogue) == one launch per hop (MSW_HOP_WG=0), bit for bit: a wet-start rollout and a
-    forward, with the shipped K4_F32 checkpoint (PReLU) and a seeded K = 3 ReLU model; on the
-    tiny / small meshes (chains on 3 / 2 scales) and zenodo4 (its 163-row coarsest scale)."""
-    from mswegnn.engine import EnginePlan
-    T = 6
-    g = wet_state(make_multiscale_mesh(**mesh_config(mesh), T=T), seed=2).to(cuda)
-    m = (build_msgnn(4, 32, 4, state=weights("K4_F32")) if act == "prelu"
-         else build_msgnn(4, 32, K, mlp_activation=act)).to(cuda)
-    outs, launches = [], []
-    for v in ("0", "1", "2"):
-        monkeypatch.setenv("MSW_HOP_WG", v)
-        plan = EnginePlan(m, g, cuda)
-        r = plan.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone()
-        launches.append(plan.stats()["kernels_per_step"])
-        y = plan.forward(g.x).clone()
-        outs.append((r, y))
-        plan.close()
-    print(mesh, K, act, "launches per step (off / middle / all):", launches)
-    assert launches[2] < launches[0] and launches[1] <= launches[0], launches
-    if K == 4:
-        assert launches[1] < launches[0], launches
-    for r, y in outs[1:]:
-        assert torch.equal(r, outs[0][0]), (r - outs[0][0]).abs().max().item()
-        assert torch.equal(y, outs[0][1]), (y - outs[0][1]).abs().max().item()
-
-
 @pytest.mark.parametrize("knob", ["MSW_XCD_MAX", "MSW_TILE_PACK"])
 def test_launch_layout_knobs_are_bit_identical(cuda, knob, monkeypatch):
     """XCD packing of small grids (MSW_XCD_MAX=0: all eight XCDs) and the degree-aware

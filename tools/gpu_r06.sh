@@ -50,15 +50,48 @@ case $MODE in
   divab)  # the shared-reciprocal division: exactness sweep, bit-identity of the variants, A/B
     step div_check 120 ./tools/div_check > $OUT/div_check.txt 2>&1
     step variants 600 $PYT tests/test_gpu_parity.py -m gpu -k "build_variant" > $OUT/variants.txt 2>&1
-    # (the nofastdiv variant predates the hop chains: MSW_HOP_WG=0 on the default library)
-    step ab_hbm1m 900 bash tools/ab.sh "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" -- --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1
+    step ab_hbm1m 900 bash tools/ab.sh "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv" -- --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1
     cp gpurun_out/ab.log $OUT/ab_hbm1m.txt
-    step ab_zenodo4 600 bash tools/ab.sh "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv" "MSW_HOP_WG=0" "MSW_LIB_VARIANT=nofastdiv"
+    step ab_zenodo4 600 bash tools/ab.sh "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv"
     cp gpurun_out/ab.log $OUT/ab_zenodo4.txt ;;
-  chain)  # one-workgroup hop chains: bit identity, then the A/B on zenodo4 and the batch of 8
-    step chain_tests 600 $PYT tests/test_gpu_parity.py -m gpu -k "hop_chain or partitioned or group_rollout" > $OUT/chain_tests.txt 2>&1
-    step ab_chain 900 bash tools/ab.sh "MSW_HOP_WG=0" "MSW_HOP_WG=1" "MSW_HOP_WG=2" "MSW_HOP_WG=0" "MSW_HOP_WG=1" "MSW_HOP_WG=2"
-    cp gpurun_out/ab.log $OUT/ab_chain_zenodo4.txt ;;
+  sq)  # SQ counters of config 5's fused edge MLP + hop, per launch (tools/pmc_generic.py --split-duration)
+    KRE='k_edge_hop'
+    C1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
+    C2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
+    C3="SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VALU_TRANS_F32 SQ_VALU_MFMA_COEXEC_CYCLES"
+    i=0
+    for C in "$C1" "$C2" "$C3"; do
+      i=$((i+1)); rm -rf $OUT/sq$i
+      step sq$i 240 rocprofv3 --pmc $C --kernel-include-regex "$KRE" -d $PWD/$OUT/sq$i -o run --output-format csv -- python3 tools/pmc_step.py hbm1m 2 > $OUT/sq$i.log 2>&1
+    done
+    python3 tools/pmc_generic.py --split-duration $OUT/sq1 $OUT/sq2 $OUT/sq3 > $OUT/sq_hbm1m.txt 2>&1 ;;
+  final-a)  # closing session, part a: the -m gpu suite and smoke(), the rocprofv3 kernel trace of
+            # bench.py (-> roofline timing summary + step breakdown), the two PMC passes (-> HBM
+            # traffic summary), copied into profiles/ so that the bench line after them reads
+            # summaries measured on the library it loads
+    step tests 1000 $PYT tests -m gpu > $OUT/gpu_tests.txt 2>&1
+    step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+    rm -rf $OUT/prof $OUT/pmc_fetch $OUT/pmc_write
+    step rocprof 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+    python3 tools/roofline_check.py $OUT/prof/run_kernel_trace.csv --json $OUT/roofline_rocprof.json > $OUT/roofline_check.txt 2>&1
+    python3 tools/step_breakdown.py $OUT/prof/run_kernel_trace.csv > $OUT/step_breakdown.txt 2>&1
+    KRE='k_hop|k_edge_hop|k_pool|k_encode'
+    step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_fetch.log 2>&1
+    step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $OUT/pmc_write.log 2>&1
+    python3 tools/pmc_summary.py $OUT/pmc_summary.json $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_summary.log 2>&1
+    cp $OUT/roofline_rocprof.json profiles/roofline_rocprof.json && cp $OUT/pmc_summary.json profiles/pmc_summary.json
+    step bench 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err ;;
+  final-b)  # part b: the other workloads' lines, F = 64 trace, the CPU thread sweep, the N > 1 rehearsal
+    rm -rf $OUT/prof_f64
+    step rocprof_f64 300 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_f64 -o run --output-format csv -- python3 bench.py --workload zenodo4_f64 --no-cpu-baseline --no-roofline-large --steps 5 --warmup 1 > $OUT/bench_f64_prof.json 2> $OUT/bench_f64_prof.err
+    python3 tools/step_breakdown.py $OUT/prof_f64/run_kernel_trace.csv > $OUT/step_breakdown_f64.txt 2>&1
+    step bench_f64 300 python bench.py --workload zenodo4_f64 --no-roofline-large > $OUT/bench_f64.json 2> $OUT/bench_f64.err
+    step bench_hbm1m 400 python bench.py --workload hbm1m --no-cpu-baseline --steps 3 --warmup 1 > $OUT/bench_hbm1m.json 2> $OUT/bench_hbm1m.err
+    step refloop 300 python bench.py --caller reference-loop --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_refloop.json 2> $OUT/bench_refloop.err
+    step config3 400 python bench.py --workload config3 --global-batch 8 --no-roofline-large --steps 5 --warmup 2 > $OUT/bench_config3.json 2> $OUT/bench_config3.err
+    step dk15 300 python bench.py --workload dk15 --T 200 --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_dk15.json 2> $OUT/bench_dk15.err
+    step cpu_threads 400 python tools/cpu_threads.py > $OUT/cpu_threads.json 2> $OUT/cpu_threads.err
+    step rehearsal 420 env MSW_DIST_BACKEND=gloo python bench.py --gpus 2 --extras-budget 180 > $OUT/rehearsal_2rank_gloo.json 2> $OUT/rehearsal_2rank_gloo.err ;;
   cputhreads)
     step cpu_threads 600 python tools/cpu_threads.py > $OUT/cpu_threads.json 2> $OUT/cpu_threads.err ;;
   *)
