@@ -10,10 +10,7 @@
 namespace msw {
 
 constexpr int kMaxLayers = 4;
-#ifndef MSW_WAVES
-#define MSW_WAVES 4
-#endif
-constexpr int kWaves = MSW_WAVES;  // waves per block (tiles per workgroup)
+constexpr int kWaves = 4;  // waves per block (tiles per workgroup)
 constexpr int kRowsPerBlock = kRowsPerWave * kWaves;
 constexpr int kXcds = 8, kCusPerXcd = 32;  // MI355X: 8 XCDs x 32 CUs (workgroup i -> XCD i % 8)
 

@@ -50,14 +50,11 @@ __device__ __forceinline__ void enc_coop_mlp(const f32x4 (&in)[IN0], f32x4 (&out
 // during layer 0's MFMA chain and exchange, deeper layers load theirs at the layer.  PF: every
 // layer's rank slice has TS = T / P output tiles (all F = 64 and F = 32 encoder MLPs at P =
 // NT); otherwise it is enc_coop_mlp.  Same arithmetic.
-#ifndef MSW_ENC_PF
-#define MSW_ENC_PF 1
-#endif
 template <int IN0, int T, int TL, int ACT, int P, int XW>
 struct CoopMlp {
   static constexpr int TS = T / P;
   static constexpr bool XL = TL % P == 0;  // the last layer split over the ranks, else on every rank
-  static constexpr bool PF = MSW_ENC_PF && (XL ? TL / P : TL) == TS;
+  static constexpr bool PF = (XL ? TL / P : TL) == TS;
   LayerOps<IN0, TS> first;
   __device__ __forceinline__ void load(const MlpDev& m, const float* __restrict__ W, int r, int lane, int g) {
     if constexpr (PF) ops_load<IN0, TS>(first, m.l[0], W, (m.n == 1 && !XL) ? 0 : r * TS, lane, g);
@@ -105,7 +102,7 @@ struct CoopMlp {
   }
 };
 // projections' operands: this many k-tiles in flight (0: proj)
-constexpr int kEncProjAhead = MSW_ENC_PF ? 4 : 0;
+constexpr int kEncProjAhead = 4;
 // Workgroup: WV waves = WV / P row tiles (F = 32: eight waves, the four row tiles of k_encode's
 // workgroup, so the weight region is staged as often as there; F = 64 reads the blob).
 template <int NT> constexpr int enc_coop_waves() { return NT == 2 ? 8 : kWaves; }

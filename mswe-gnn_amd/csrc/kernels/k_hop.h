@@ -142,14 +142,12 @@ __global__ __launch_bounds__((64 * hop_waves<NT, LOOP>())) void k_hop(HopArgs a)
 // The arithmetic is k_hop's operation for operation -- the activity predicate's sums, the
 // message, agg = ((0 + m_0) + m_1) + ... in edge order, the filter -- so it is bit-identical.
 constexpr int kRowHopWaves = 8;
-#ifndef MSW_ROW_DC
-#define MSW_ROW_DC 3  // edges in flight per lane (F <= 32): 113 VGPRs, 4 waves per SIMD
-#endif
+constexpr int kRowDc = 3;  // edges in flight per lane (F <= 32): 113 VGPRs, 4 waves per SIMD
 template <int NT>
 __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
 #pragma clang fp contract(off)
   constexpr int F = 16 * NT;
-  constexpr int DC = NT >= 4 ? 2 : MSW_ROW_DC;
+  constexpr int DC = NT >= 4 ? 2 : kRowDc;
   [[maybe_unused]] const int lane = threadIdx.x & 63;
   const int w = wave_id();
   const int stride = gridDim.x * kRowHopWaves;

@@ -33,25 +33,18 @@ constexpr int kBlock = 64 * kWaves;
 template <int NT, bool LOOP>
 constexpr int waves_of() { return LOOP && NT <= 2 ? 8 : kWaves; }
 // the grid-stride middle / last hop (k_hop, large meshes): its own workgroup size
-#ifndef MSW_HOP_WAVES
-#define MSW_HOP_WAVES 8
-#endif
 template <int NT, bool LOOP>
-constexpr int hop_waves() { return LOOP && NT <= 2 ? MSW_HOP_WAVES : kWaves; }
+constexpr int hop_waves() { return LOOP && NT <= 2 ? 8 : kWaves; }
 // the fused edge MLP + hop keeps one tile per wave in flight in its grid-stride loop: a
 // software-pipelined loop (tile i+1's gathers and tile i+2's record during tile i's MLP) fits
 // two waves per SIMD (212 VGPRs, no spills) and measured 5 % slower on the 1M-node mesh than
 // four waves per SIMD without it (673 vs 639 us, profiles/r04/ab_eh_pipe_hbm1m.txt; removed)
-#ifndef MSW_EDGE_WAVES
-#define MSW_EDGE_WAVES 12   // grid-stride, with epilogue (LST = 1): 3 waves per SIMD
-#endif
-#ifndef MSW_EDGE_WAVES0
-#define MSW_EDGE_WAVES0 16  // grid-stride, no epilogue (LST = 0): 4 waves per SIMD
-#endif
+constexpr int kEdgeWaves = 12;   // grid-stride, with epilogue (LST = 1): 3 waves per SIMD
+constexpr int kEdgeWaves0 = 16;  // grid-stride, no epilogue (LST = 0): 4 waves per SIMD
 // Workgroup of the grid-stride edge MLP + hop: as many waves as the register budget allows
 // per SIMD, times 4 -- one workgroup per CU, so one staged weight copy serves all of them.
 template <int NT, bool LOOP, int LST = 1>
-constexpr int edge_waves() { return LOOP && NT <= 2 ? (LST ? MSW_EDGE_WAVES : MSW_EDGE_WAVES0) : kWaves; }
+constexpr int edge_waves() { return LOOP && NT <= 2 ? (LST ? kEdgeWaves : kEdgeWaves0) : kWaves; }
 template <int NT, bool LOOP, int LST>
 constexpr int edge_eu() { return LOOP && NT <= 2 ? edge_waves<NT, LOOP, LST>() / 4 : 1; }
 
