@@ -125,7 +125,7 @@ def cpu_share():
 def _cpu_sim_worker(job):
     """One simulation of a workload through the oracle on the host (a spawned process of
     cpu_batch_baseline): built, then every worker starts its timed rollout together."""
-    name, seed, T, Tc, threads, barrier = job
+    name, seed, T, Tc, threads, seconds, barrier = job
     torch.set_num_threads(threads)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import msgnn_torch as orc  # test/baseline infrastructure only
@@ -134,15 +134,18 @@ def _cpu_sim_worker(job):
     cfg = orc.msgnn_config(num_scales=w["S"], hid_features=w["F"], K=w["K"])
     barrier.wait(timeout=300)
     c0 = time.time()
-    orc.rollout(P, cfg, g, Tc)
-    return desc["fine_nodes"], Tc, c0, time.time()
+    steps = 0
+    while steps == 0 or time.time() - c0 < seconds:  # whole Tc-step rollouts for ~`seconds`
+        orc.rollout(P, cfg, g, Tc)
+        steps += Tc
+    return desc["fine_nodes"], steps, c0, time.time()
 
 
 def cpu_batch_baseline(name, ids, T, share, seconds, t1, t1_threads):
     """The CPU analogue of the reference's batched evaluation: the simulations `ids` one per
     process, all at once, over the `share` host threads (threads split evenly), each a
-    Tc-step rollout sized to ~`seconds` from the single-simulation step time t1 (measured on
-    t1_threads).  -> {value, unit, processes, threads_per_process, sample}."""
+    Tc-step rollout sized from the single-simulation step time t1 (measured on t1_threads),
+    repeated for ~`seconds`.  -> {value, unit, processes, threads_per_process, sample}."""
     import multiprocessing as mp
     ids = list(ids)[:share]
     procs = len(ids)
@@ -152,13 +155,14 @@ def cpu_batch_baseline(name, ids, T, share, seconds, t1, t1_threads):
     with ctx.Manager() as man:
         bar = man.Barrier(procs)
         with ctx.Pool(procs) as pool:
-            res = pool.map(_cpu_sim_worker, [(name, i, T, Tc, tpp, bar) for i in ids], chunksize=1)
+            res = pool.map(_cpu_sim_worker, [(name, i, T, Tc, tpp, seconds, bar) for i in ids], chunksize=1)
     wall = max(r[3] for r in res) - min(r[2] for r in res)
     work = sum(r[0] * r[1] for r in res)
     return {"value": work / wall, "unit": "fine-node-steps/s", "processes": procs, "threads_per_process": tpp,
             "cores": procs * tpp, "kind": "port",
-            "sample": f"{procs} simulations of the workload (ids {ids[0]}..{ids[-1]}), one {Tc}-step rollout each "
-                      f"in its own process, started together; wall {wall:.1f} s"}
+            "sample": f"{procs} simulations of the workload (ids {ids[0]}..{ids[-1]}), {Tc}-step rollouts repeated "
+                      f"for ~{seconds:.0f} s in one process each, started together; "
+                      f"{sum(r[1] for r in res)} simulation-steps in all, wall {wall:.1f} s"}
 
 
 def make_gatherer(dist, world, n0, T, device):

@@ -1,6 +1,6 @@
 """Thread sweep of the CPU baseline (bench.py cpu_baseline): the oracle's rollout of one
-zenodo4 simulation (the reference's algorithm, same ATen CPU ops) at 1 / 8 / 16 / 32 / 64 /
-all host threads, fine-node-steps/s each.  Why bench.py caps the baseline at 16 threads: the
+zenodo4 simulation (the reference's algorithm, same ATen CPU ops) at 1 / 8 / 16 / 32 / 64
+host threads (and all of them on hosts of at most 64 cores), fine-node-steps/s each.  Why bench.py caps the baseline at 16 threads: the
 GPU box gives one GPU a 16-thread CPU share, and the rate does not grow past it.
 
     python tools/cpu_threads.py [--steps 3] > profiles/r06/cpu_threads.json
@@ -34,7 +34,11 @@ def main():
     except AttributeError:
         aff = None
     rows = []
-    for n in sorted({1, 8, 16, 32, 64, host} & set(range(1, host + 1))):
+    # the host's full core count only where it is small: on the GPU box the process has a 16-CPU
+    # share of a 256-core machine, and 256 threads there took > 3 minutes for one step (the
+    # round-6 run was killed there; 64 threads already run 5x slower than 16)
+    counts = {1, 8, 16, 32, 64} | ({host} if host <= 64 else set())
+    for n in sorted(c for c in counts if c <= host):
         torch.set_num_threads(n)
         orc.rollout(P, cfg, g, 1)  # warm
         t0 = time.perf_counter()

@@ -92,6 +92,10 @@ case $MODE in
     step dk15 300 python bench.py --workload dk15 --T 200 --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_dk15.json 2> $OUT/bench_dk15.err
     step cpu_threads 400 python tools/cpu_threads.py > $OUT/cpu_threads.json 2> $OUT/cpu_threads.err
     step rehearsal 420 env MSW_DIST_BACKEND=gloo python bench.py --gpus 2 --extras-budget 180 > $OUT/rehearsal_2rank_gloo.json 2> $OUT/rehearsal_2rank_gloo.err ;;
+  final-c)  # part c: the config-3 line (CPU batch leg), the CPU thread sweep, the N > 1 rehearsal
+    step config3 400 python bench.py --workload config3 --global-batch 8 --no-roofline-large --steps 5 --warmup 2 > $OUT/bench_config3.json 2> $OUT/bench_config3.err
+    step cpu_threads 300 python -u tools/cpu_threads.py > $OUT/cpu_threads.json 2> $OUT/cpu_threads.err
+    step rehearsal 420 env MSW_DIST_BACKEND=gloo python bench.py --gpus 2 --extras-budget 180 > $OUT/rehearsal_2rank_gloo.json 2> $OUT/rehearsal_2rank_gloo.err ;;
   cputhreads)
     step cpu_threads 600 python tools/cpu_threads.py > $OUT/cpu_threads.json 2> $OUT/cpu_threads.err ;;
   *)
