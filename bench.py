@@ -110,9 +110,9 @@ def build_workload(name, seed, T):
 
 
 CPU_SHARE_NOTE = ("threads = the CPU share of one GPU on the GPU box, 16 (gpurun sets OMP_NUM_THREADS=16; "
-                  "os.cpu_count() there reports the whole machine, host_cores); more threads on the "
-                  "oracle's ATen CPU ops do not help: profiles/r06/cpu_threads.json (1 / 8 / 16 / 32 / 64 / "
-                  "all threads on one simulation)")
+                  "os.cpu_count() there reports the whole machine, host_cores); more threads run slower: "
+                  "one zenodo4 simulation at 1 / 8 / 16 / 32 / 64 threads 0.065 / 0.113 / 0.131 / 0.062 / "
+                  "0.028 M fine-node-steps/s (profiles/r06/cpu_threads.json)")
 
 
 def cpu_share():
