@@ -912,7 +912,10 @@ def main():
                 if B > 1:
                     # the reference evaluates batches of simulations (test_model.py:37): on the host
                     # that is one simulation per process over the CPU share
-                    cpu["batch"] = cpu_batch_baseline(args.workload, ids, T, share, args.cpu_seconds, t1, threads)
+                    try:
+                        cpu["batch"] = cpu_batch_baseline(args.workload, ids, T, share, args.cpu_seconds, t1, threads)
+                    except Exception as e:  # noqa: BLE001
+                        cpu["batch"] = {"error": repr(e)}
                 r0 = r_gpu[:g_cpu.num_nodes, :, :Tc]  # simulation 0 = the batch's first graph
                 d = (r0 - r_cpu).abs()
                 parity["vs_cpu_reference"] = {
