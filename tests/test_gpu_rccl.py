@@ -182,3 +182,19 @@ def test_nccl_world1_process_group(cuda):
     assert rec["gather_equal"] and rec["gather_second_equal"]
     assert rec["distributed_rollout_equal"] and rec["gather_owned_equal"]
     assert rec["comm_set"]
+
+
+def test_rccl_partition_checker_runs_at_world1(cuda):
+    """tools/rccl_partition_check.py -- the single-mesh decomposition checker bench.py runs at
+    N > 1 (eager RCCL exchanges, then captured) -- end to end on the one GPU at W = 1: spawned
+    rank, nccl group, DistributedRollout, gather_owned, the captured pass; both records
+    bit-identical to the undivided rollout."""
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_partition_check.py"), "1",
+                        "--mesh", "small", "--steps", "2", "--T", "8", "--wait", "200"],
+                       env=dict(os.environ, NCCL_SOCKET_IFNAME=os.environ.get("NCCL_SOCKET_IFNAME", "lo")),
+                       capture_output=True, text=True, timeout=260)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    print(rec)
+    assert rec["bit_identical"] and rec["world"] == 1
+    assert rec["captured"]["bit_identical_to_eager"] and rec["captured"]["graph_captured"] == 1, rec["captured"]
