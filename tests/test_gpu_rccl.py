@@ -26,14 +26,20 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, build_msgnn, golden, per_step_rel, weights, REL_TOL
-from mswegnn.mesh import make_multiscale_mesh, mesh_config, wet_state
+from conftest import ROOT, build_gnn, build_msgnn, golden, per_step_rel, weights, REL_TOL
+from mswegnn.mesh import make_multiscale_mesh, make_single_scale_mesh, mesh_config, wet_state
 
 pytestmark = pytest.mark.gpu
 
 
-def _model(cuda):
-    m = build_msgnn(4, 32, 4, state=weights("K4_F32")).to(cuda)
+def _model(cuda, kind="msgnn32"):
+    if kind == "msgnn32":
+        m = build_msgnn(4, 32, 4, state=weights("K4_F32"))
+    elif kind == "msgnn64":
+        m = build_msgnn(4, 64, 4)
+    else:
+        m = build_gnn(state=weights("gnn_F32_seed42"))
+    m = m.to(cuda)
     m.engine = "hip"
     return m
 
@@ -42,7 +48,8 @@ def _self_plan(g, stride, shift):
     """exchange_plan-style {scale: {0: (recv, send)}}: on every scale the rows k*stride (+1 per
     scale, so that scale 0 includes a BC-free interior row) received from rank 0 itself, send
     row i = recv row (i + shift) mod n."""
-    npt = g.node_ptr.cpu().numpy().astype(np.int64)
+    from mswegnn.partition import _scales
+    npt, _ = _scales(g)
     plan = {}
     for s in range(len(npt) - 1):
         rows = np.arange(int(npt[s]) + s % stride, int(npt[s + 1]), stride, dtype=np.int64)
@@ -123,13 +130,18 @@ def test_rccl_one_rank_identity_exchange_matches_plain_plan(cuda):
     pl.close()
 
 
-def test_rccl_self_exchange_moves_rows_like_loopback(cuda):
+@pytest.mark.parametrize("kind", ["msgnn32", "msgnn64", "gnn"])
+def test_rccl_self_exchange_moves_rows_like_loopback(cuda, kind):
     """Shifted self entries (receive row k <- send row k+1): the rollout is no longer the plain
     one, and the RCCL transport (eager and captured) gives the in-process transport's result
-    bit for bit -- the bytes really went through ncclSend / ncclRecv and landed in the right rows."""
+    bit for bit -- the bytes really went through ncclSend / ncclRecv and landed in the right rows
+    (4-scale MSGNN at F = 32 / 64: U rows of 2F floats and out rows of F; the 1-scale GNN)."""
     T = 20
-    g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=3).to(cuda)
-    m = _model(cuda)
+    if kind == "gnn":
+        g = wet_state(make_single_scale_mesh(n_coarse=3, refinements=3, T=T), seed=2).to(cuda)
+    else:
+        g = wet_state(make_multiscale_mesh(**mesh_config("small"), T=T), seed=3).to(cuda)
+    m = _model(cuda, kind)
     whole = m.rollout(g, T).clone()
     xp = _self_plan(g, stride=5, shift=1)
     loop_pl = _part_plan(m, g, cuda, xp)
