@@ -44,23 +44,6 @@ __device__ __forceinline__ void normalize_s(f32x4 (&sv)[NT]) {
 }
 
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
-// Grid-stride loops of several waves per SIMD (wave w runs on SIMD w % 4): a distinct static
-// issue priority per co-resident wave (w / 4) so that the waves of a SIMD drift out of lockstep
-// instead of reaching their gathers, MFMA chains and VALU blocks together (MI355X_MICROARCH
-// "two waves per SIMD", item 4).  Scheduling only: results are unchanged.
-#ifndef MSW_SETPRIO
-#define MSW_SETPRIO 0  // 1: per-wave static priority in the grid-stride loops (A/B build variant)
-#endif
-__device__ __forceinline__ void loop_priority() {
-  if constexpr (MSW_SETPRIO) {
-    switch (wave_id() >> 2) {
-      case 0: break;
-      case 1: __builtin_amdgcn_s_setprio(1); break;
-      case 2: __builtin_amdgcn_s_setprio(2); break;
-      default: __builtin_amdgcn_s_setprio(3); break;
-    }
-  }
-}
 // XCD packing (Common::xcd = k > 0, small one-round grids): the launch has 8x the workgroups
 // it needs and only those the dispatcher places on XCDs 0 .. k-1 (workgroup i -> XCD i % 8)
 // work.  The XCDs start a launch's workgroups up to ~1.3 us apart, most of a small hop's

@@ -332,7 +332,6 @@ void k_edge_hop(EdgeHopArgs a) {
     else
       body(std::false_type{});
   } else {
-    loop_priority();
     const float* Wm = c.W;
     if constexpr (kStaged<NT>) {
       stage_glds<WV>(smem, a.c.W, a.reg, 0, a.reg.len);
@@ -494,7 +493,6 @@ void k_edge_mlp(EdgeHopArgs a) {
   // one's VALU work never overlaps the other's MFMA chain
   if (w >= 4)
     for (int k = 0; k < a.stagger; ++k) __builtin_amdgcn_s_sleep(32);
-  loop_priority();
   if (a.reg.len > 0) {
     if (full)
       run(smem, std::true_type{});

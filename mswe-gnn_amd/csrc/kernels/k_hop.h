@@ -154,7 +154,6 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
   const int ntile = (a.nrows + kRowsPerWave - 1) / kRowsPerWave;
   f32x4 wf[NT][NT];  // the filter in registers (in LDS: equal, profiles/r03/ab_rows_variants.jsonl)
   load_filter<NT>(wf, a.c.W, a.filt_a, lane);
-  loop_priority();
   for (int tile = blockIdx.x * kRowHopWaves + w; tile < ntile; tile += stride) {
     const int ln = opaque_lane(), g = ln >> 4, j = ln & 15;
     const int k = tile * kRowsPerWave + j;

@@ -54,14 +54,6 @@ case $MODE in
     cp gpurun_out/ab.log $OUT/ab_hbm1m.txt
     step ab_zenodo4 600 bash tools/ab.sh "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv"
     cp gpurun_out/ab.log $OUT/ab_zenodo4.txt ;;
-  prio)  # per-wave static priority in the grid-stride loops (build variant prio): identity, A/B
-    step variants 600 $PYT tests/test_gpu_parity.py -m gpu -k "build_variant" > $OUT/variants.txt 2>&1
-    step ab_hbm1m 900 bash tools/ab.sh "" "MSW_LIB_VARIANT=prio" "" "MSW_LIB_VARIANT=prio" -- --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1
-    cp gpurun_out/ab.log $OUT/ab_hbm1m.txt
-    step ab_f64 600 bash tools/ab.sh "" "MSW_LIB_VARIANT=prio" "" "MSW_LIB_VARIANT=prio" -- --workload zenodo4_f64 --no-cpu-baseline --no-roofline-large --steps 10 --warmup 3
-    cp gpurun_out/ab.log $OUT/ab_f64.txt
-    step ab_config3 600 bash tools/ab.sh "" "MSW_LIB_VARIANT=prio" "" "MSW_LIB_VARIANT=prio" -- --workload config3 --global-batch 8 --no-cpu-baseline --no-roofline-large --steps 5 --warmup 2
-    cp gpurun_out/ab.log $OUT/ab_config3.txt ;;
   sq)  # SQ counters of config 5's fused edge MLP + hop, per launch (tools/pmc_generic.py --split-duration)
     KRE='k_edge_hop'
     C1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
