@@ -127,7 +127,50 @@ def test_rccl_one_rank_identity_exchange_matches_plain_plan(cuda):
     st3 = pl.stats()
     assert st3["rccl_calls"] == st2["rccl_calls"] and st3["rccl_steps"] == 3 * T
     assert torch.equal(cap, whole) and torch.equal(again, whole)
+    # forward mode (the reference's per-step loop, msw_forward): the exchange points of the
+    # forward schedule through RCCL, captured into the forward graph, == the plain forward
+    from mswegnn.engine import plan_for
+    y_plain = plan_for(m, g).forward(g.x).clone()
+    calls = pl.stats()["rccl_calls"]
+    y = pl.forward(g.x).clone()
+    torch.cuda.synchronize()
+    assert pl.stats()["rccl_calls"] > calls  # the forward graph's capture issued them
+    assert torch.equal(y, y_plain), (y - y_plain).abs().max().item()
     pl.close()
+
+
+def test_rccl_self_exchange_on_a_batch(cuda):
+    """A batch of two meshes (the reference's disjoint-union layout, graph-major rows inside a
+    scale): shifted self entries whose rows span both graphs move rows exactly as the in-process
+    transport does, eager and captured."""
+    from mswegnn.batch import collate
+    from mswegnn.rollout import adapt_batch_training
+    T = 8
+    ga = wet_state(make_multiscale_mesh(**mesh_config("tiny"), seed=1, T=T), seed=1)
+    gb = wet_state(make_multiscale_mesh(**mesh_config("tiny"), seed=2, T=T), seed=2)
+    g = adapt_batch_training(collate([ga, gb])).to(cuda)
+    m = _model(cuda)
+    npt = g.node_ptr.cpu().numpy()  # [graphs][scales + 1]
+    xp = {}
+    for s in range(npt.shape[1] - 1):  # on every scale: rows of graph 0 and graph 1 together
+        rows = np.concatenate([np.arange(npt[0, s], npt[0, s + 1], 4), np.arange(npt[1, s] + 1, npt[1, s + 1], 4)])
+        xp[s] = {0: (rows.tolist(), np.roll(rows, -3).tolist())}
+    from mswegnn.engine import EnginePlan
+    from mswegnn.partition import exchange_desc
+    d, keep = exchange_desc(xp)
+    loop_pl = EnginePlan(m, g, cuda, exchange=d, rank=0)
+    rccl_pl = EnginePlan(m, g, cuda, exchange=d, rank=0)
+    del keep
+    loop = _group_rollout(loop_pl, g, T).clone()
+    _set_comm(rccl_pl)
+    eager = rccl_pl.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone()
+    rccl_pl.set_graph_capture(1)
+    cap = rccl_pl.rollout(g.x, g.BC, g.node_BC, g.type_BC, T).clone()
+    torch.cuda.synchronize()
+    assert rccl_pl.stats()["rccl_steps"] == 2 * T
+    assert torch.equal(eager, loop) and torch.equal(cap, loop)
+    loop_pl.close()
+    rccl_pl.close()
 
 
 @pytest.mark.parametrize("kind", ["msgnn32", "msgnn64", "gnn"])
