@@ -253,3 +253,17 @@ def test_rccl_partition_checker_runs_at_world1(cuda):
     print(rec)
     assert rec["bit_identical"] and rec["world"] == 1
     assert rec["captured"]["bit_identical_to_eager"] and rec["captured"]["graph_captured"] == 1, rec["captured"]
+
+
+def test_ddp_training_step_nccl_world1(cuda):
+    """tools/ddp_train_check.py over nccl at W = 1 (the DDP training check bench.py runs at
+    N > 1): DistributedDataParallel's gradient all-reduce through RCCL around the HIP training
+    kernels, gradients against one process's own step."""
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "ddp_train_check.py"), "1",
+                        "--backend", "nccl", "--wait", "200"],
+                       env=dict(os.environ, NCCL_SOCKET_IFNAME=os.environ.get("NCCL_SOCKET_IFNAME", "lo")),
+                       capture_output=True, text=True, timeout=260)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    print(rec)
+    assert rec["backend"] == "nccl" and rec["world"] == 1
