@@ -7,7 +7,10 @@ of random sizes, dry or wet, and compares a 3-step rollout (rollout_test semanti
 the oracle at the fp32 bar (per step 1e-4 relative; a mask-threshold flip of the fp32
 reference itself is judged against fp64, conftest.assert_rollout_parity).  The shipped
 configurations are covered elsewhere; this looks for combinations no fixed test names.
+FUZZ_SEEDS="a:b" widens the seed range (default 0:16) for a longer sweep on the GPU box.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -68,7 +71,12 @@ def build(c):
     return m, cfg, gs, T
 
 
-@pytest.mark.parametrize("seed", range(16))
+def _seeds():
+    a, b = (int(v) for v in os.environ.get("FUZZ_SEEDS", "0:16").split(":"))
+    return range(a, b)
+
+
+@pytest.mark.parametrize("seed", _seeds())
 def test_random_configuration_vs_oracle(cuda, seed):
     c = draw(seed)
     m, cfg, gs, T = build(c)

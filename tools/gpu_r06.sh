@@ -5,7 +5,9 @@
 #   rccl        the one-rank RCCL tests (tests/test_gpu_rccl.py) + the partitioned-rollout tests
 #   train       the HIP training-gradient tests (tests/test_gpu_train.py)
 #   tests       the whole -m gpu suite and smoke()
+#   schedfuzz   tests/test_gpu_schedule_fuzz.py over a seed range (SCHED_FUZZ_SEEDS, default 0:200)
 #   pytest      pytest -m gpu on the test ids given as args
+#   fuzz        tests/test_gpu_fuzz.py over a wider seed range (FUZZ_SEEDS, default 16:400)
 #   ab          tools/ab.sh with the args (A/B of MSW_* settings on bench.py)
 #   bench       bench.py with the args
 #   prof        rocprofv3 kernel trace of bench.py with the args (+ step breakdown)
@@ -36,6 +38,10 @@ case $MODE in
   tests)
     step tests 1000 $PYT tests -m gpu > $OUT/gpu_tests.txt 2>&1
     step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
+  fuzz)  # a wider seed range of tests/test_gpu_fuzz.py (args: the range, default 16:400)
+    export FUZZ_SEEDS=${1:-16:400}; step fuzz 1000 $PYT -m gpu tests/test_gpu_fuzz.py > $OUT/fuzz.txt 2>&1 ;;
+  schedfuzz)  # tests/test_gpu_schedule_fuzz.py over a seed range (args: the range, default 0:200)
+    export SCHED_FUZZ_SEEDS=${1:-0:200}; step schedfuzz 1000 $PYT -m gpu tests/test_gpu_schedule_fuzz.py > $OUT/schedfuzz.txt 2>&1 ;;
   pytest)
     step pytest 900 $PYT -m gpu "$@" > $OUT/pytest.txt 2>&1 ;;
   ab)
