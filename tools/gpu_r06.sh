@@ -6,6 +6,7 @@
 #   train       the HIP training-gradient tests (tests/test_gpu_train.py)
 #   tests       the whole -m gpu suite and smoke()
 #   schedfuzz   tests/test_gpu_schedule_fuzz.py over a seed range (SCHED_FUZZ_SEEDS, default 0:200)
+#   partfuzz    tests/test_gpu_partition_fuzz.py over a seed range (PART_FUZZ_SEEDS, default 0:200)
 #   pytest      pytest -m gpu on the test ids given as args
 #   fuzz        tests/test_gpu_fuzz.py over a wider seed range (FUZZ_SEEDS, default 16:400)
 #   ab          tools/ab.sh with the args (A/B of MSW_* settings on bench.py)
@@ -42,6 +43,8 @@ case $MODE in
     export FUZZ_SEEDS=${1:-16:400}; step fuzz 1000 $PYT -m gpu tests/test_gpu_fuzz.py > $OUT/fuzz.txt 2>&1 ;;
   schedfuzz)  # tests/test_gpu_schedule_fuzz.py over a seed range (args: the range, default 0:200)
     export SCHED_FUZZ_SEEDS=${1:-0:200}; step schedfuzz 1000 $PYT -m gpu tests/test_gpu_schedule_fuzz.py > $OUT/schedfuzz.txt 2>&1 ;;
+  partfuzz)  # tests/test_gpu_partition_fuzz.py over a seed range (args: the range, default 0:200)
+    export PART_FUZZ_SEEDS=${1:-0:200}; step partfuzz 1000 $PYT -m gpu tests/test_gpu_partition_fuzz.py > $OUT/partfuzz.txt 2>&1 ;;
   pytest)
     step pytest 900 $PYT -m gpu "$@" > $OUT/pytest.txt 2>&1 ;;
   ab)
