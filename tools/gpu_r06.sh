@@ -8,6 +8,7 @@
 #   schedfuzz   tests/test_gpu_schedule_fuzz.py over a seed range (SCHED_FUZZ_SEEDS, default 0:200)
 #   partfuzz    tests/test_gpu_partition_fuzz.py over a seed range (PART_FUZZ_SEEDS, default 0:200)
 #   encloop     the tile-strided encoder (k_encode_loop): parity tests, config-5 A/B and trace
+#   trainfuzz   tests/test_gpu_train_fuzz.py over a seed range (TRAIN_FUZZ_SEEDS, default 0:300)
 #   pytest      pytest -m gpu on the test ids given as args
 #   fuzz        tests/test_gpu_fuzz.py over a wider seed range (FUZZ_SEEDS, default 16:400)
 #   ab          tools/ab.sh with the args (A/B of MSW_* settings on bench.py)
@@ -53,6 +54,8 @@ case $MODE in
     rm -rf $OUT/prof
     step rocprof 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --workload hbm1m --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
     python3 tools/step_breakdown.py $OUT/prof/run_kernel_trace.csv > $OUT/step_breakdown_hbm1m.txt 2>&1 ;;
+  trainfuzz)  # tests/test_gpu_train_fuzz.py over a seed range (args: the range, default 0:300)
+    export TRAIN_FUZZ_SEEDS=${1:-0:300}; step trainfuzz 1000 $PYT -m gpu tests/test_gpu_train_fuzz.py > $OUT/trainfuzz.txt 2>&1 ;;
   pytest)
     step pytest 900 $PYT -m gpu "$@" > $OUT/pytest.txt 2>&1 ;;
   ab)
