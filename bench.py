@@ -667,7 +667,10 @@ def main():
 
     from mswegnn.engine import plan_for
     from mswegnn import _lib
+    t_plan = time.perf_counter()
     plan = plan_for(model, g)
+    torch.cuda.synchronize()
+    t_plan = time.perf_counter() - t_plan
     out = torch.empty(g.num_nodes, 2, T, device=dev)
     # the all-gather runs on the GPU over RCCL; gloo (rehearsal) gathers host copies
     gather = make_gatherer(dist, world, fine_rank, T, dev if backend == "nccl" else torch.device("cpu"))
@@ -697,8 +700,13 @@ def main():
         if world > 1:
             gather(r[:n0] if fine_rows is None else r.index_select(0, fine_rows))
 
-    for _ in range(args.warmup):
+    t_first = None
+    for i in range(args.warmup):
+        t0 = time.perf_counter()
         one_step()
+        if i == 0:
+            torch.cuda.synchronize()
+            t_first = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -949,7 +957,12 @@ def main():
                        "device_bytes": st["device_bytes"],
                        "device_bytes_note": "plan-owned: graph tables, weights, per-node buffers and the "
                                             "edge-encoder inputs / outputs kept for the per-rollout "
-                                            "recompute of the edge terms"},
+                                            "recompute of the edge terms",
+                       "plan_build_s": t_plan, "first_rollout_s": t_first,
+                       "setup_note": "once per mesh, outside the timed region: plan_build_s = host graph "
+                                     "tables (CSR, tiles, exchange lists) + uploads + first-use kernel "
+                                     "setup; first_rollout_s = the first warmup rollout incl. its "
+                                     "hipGraph capture"},
         }
         if caller_overhead is not None:
             result["caller_overhead"] = caller_overhead
