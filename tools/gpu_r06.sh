@@ -7,7 +7,6 @@
 #   tests       the whole -m gpu suite and smoke()
 #   schedfuzz   tests/test_gpu_schedule_fuzz.py over a seed range (SCHED_FUZZ_SEEDS, default 0:200)
 #   partfuzz    tests/test_gpu_partition_fuzz.py over a seed range (PART_FUZZ_SEEDS, default 0:200)
-#   encloop     the tile-strided encoder (k_encode_loop): parity tests, config-5 A/B and trace
 #   trainfuzz   tests/test_gpu_train_fuzz.py over a seed range (TRAIN_FUZZ_SEEDS, default 0:300)
 #   pytest      pytest -m gpu on the test ids given as args
 #   fuzz        tests/test_gpu_fuzz.py over a wider seed range (FUZZ_SEEDS, default 16:400)
@@ -47,13 +46,6 @@ case $MODE in
     export SCHED_FUZZ_SEEDS=${1:-0:200}; step schedfuzz 1000 $PYT -m gpu tests/test_gpu_schedule_fuzz.py > $OUT/schedfuzz.txt 2>&1 ;;
   partfuzz)  # tests/test_gpu_partition_fuzz.py over a seed range (args: the range, default 0:200)
     export PART_FUZZ_SEEDS=${1:-0:200}; step partfuzz 1000 $PYT -m gpu tests/test_gpu_partition_fuzz.py > $OUT/partfuzz.txt 2>&1 ;;
-  encloop)  # the tile-strided encoder (measured -1 %, then removed with its test and switch): parity, A/B, trace
-    step tests 600 $PYT -m gpu tests/test_gpu_parity.py -k "tile_strided_encoder or coop_encoder or launch_layout" tests/test_gpu_fullsize.py::test_config5_million_node_rollout100_teacher_forced > $OUT/encloop_tests.txt 2>&1
-    step ab_hbm1m 900 bash tools/ab.sh "" "MSW_ENC_LOOP=0" "" "MSW_ENC_LOOP=0" -- --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1
-    cp gpurun_out/ab.log $OUT/ab_hbm1m.txt
-    rm -rf $OUT/prof
-    step rocprof 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --workload hbm1m --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
-    python3 tools/step_breakdown.py $OUT/prof/run_kernel_trace.csv > $OUT/step_breakdown_hbm1m.txt 2>&1 ;;
   trainfuzz)  # tests/test_gpu_train_fuzz.py over a seed range (args: the range, default 0:300)
     export TRAIN_FUZZ_SEEDS=${1:-0:300}; step trainfuzz 1000 $PYT -m gpu tests/test_gpu_train_fuzz.py > $OUT/trainfuzz.txt 2>&1 ;;
   pytest)
