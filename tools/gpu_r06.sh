@@ -8,6 +8,7 @@
 #   schedfuzz   tests/test_gpu_schedule_fuzz.py over a seed range (SCHED_FUZZ_SEEDS, default 0:200)
 #   partfuzz    tests/test_gpu_partition_fuzz.py over a seed range (PART_FUZZ_SEEDS, default 0:200)
 #   trainfuzz   tests/test_gpu_train_fuzz.py over a seed range (TRAIN_FUZZ_SEEDS, default 0:300)
+#   pmc5        HBM bytes per launch of config 5's kernels (FETCH_SIZE / WRITE_SIZE passes)
 #   pytest      pytest -m gpu on the test ids given as args
 #   fuzz        tests/test_gpu_fuzz.py over a wider seed range (FUZZ_SEEDS, default 16:400)
 #   ab          tools/ab.sh with the args (A/B of MSW_* settings on bench.py)
@@ -48,6 +49,11 @@ case $MODE in
     export PART_FUZZ_SEEDS=${1:-0:200}; step partfuzz 1000 $PYT -m gpu tests/test_gpu_partition_fuzz.py > $OUT/partfuzz.txt 2>&1 ;;
   trainfuzz)  # tests/test_gpu_train_fuzz.py over a seed range (args: the range, default 0:300)
     export TRAIN_FUZZ_SEEDS=${1:-0:300}; step trainfuzz 1000 $PYT -m gpu tests/test_gpu_train_fuzz.py > $OUT/trainfuzz.txt 2>&1 ;;
+  pmc5)  # HBM bytes per launch of config 5's kernels (FETCH_SIZE / WRITE_SIZE, separate passes)
+    KRE='k_encode|k_edge_hop|k_hop|k_pool|k_epi'
+    step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1
+    step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_write -o run --output-format csv -- python3 bench.py --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 1 --warmup 1 > $OUT/pmc_write.log 2>&1
+    python3 tools/pmc_summary.py $OUT/pmc_summary_hbm1m.json $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_summary.log 2>&1 ;;
   pytest)
     step pytest 900 $PYT -m gpu "$@" > $OUT/pytest.txt 2>&1 ;;
   ab)
