@@ -63,7 +63,9 @@ def build(force=False, verbose=True, variant=""):
     extra = {"trace": ["-DMSW_TRACE"],
              # the round-5 VALU diets off (PReLU as max, FULL edge kernels):
              # test_build_variant_matches_default_bitwise[valubase]
-             "valubase": ["-DMSW_PRELU_MAX=0", "-DMSW_EDGE_FULL=0"]}.get(variant, [])
+             "valubase": ["-DMSW_PRELU_MAX=0", "-DMSW_EDGE_FULL=0"],
+             # plain stores in place of the large-mesh launches' streaming stores
+             "nostream": ["-DMSW_STREAM_ST=0"]}.get(variant, [])
     os.makedirs(odir, exist_ok=True)
     os.makedirs(os.path.join(HERE, "lib"), exist_ok=True)
     out = lib_path(variant)

@@ -121,6 +121,7 @@ struct EncodeArgs {
   const float* dec_in;     // [Npad][F] decoder input rows (x_up / the GNN's last layer output)
   int decode_only;
   int coop;                // = NT: k_encode_coop (NT waves per 16-row tile), else k_encode
+  int stream;              // 1: streaming stores (grid-stride launch without the decoder)
 };
 
 struct Epilogue {

@@ -6,6 +6,19 @@
 // ---------------------------------------------------------------------------- helpers
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+// Streaming (non-temporal) store for rows a large-mesh launch writes and nothing re-reads
+// while they could still sit in L2 / the MALL (config 5's encoder: 1.26 GB per launch, 426 ->
+// 367 us; on Zenodo-size meshes the next launch re-reads from cache and the hint loses, so
+// only the grid-stride variants use it).  MSW_STREAM_ST=0: plain stores (A/B build variant).
+#ifndef MSW_STREAM_ST
+#define MSW_STREAM_ST 1
+#endif
+__device__ __forceinline__ void st4_stream(float* p, f32x4 v) {
+  if constexpr (MSW_STREAM_ST)
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  else
+    st4(p, v);
+}
 __device__ __forceinline__ float hsum(f32x4 v) { return (v.x + v.y) + (v.z + v.w); }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
@@ -177,17 +190,22 @@ __device__ __forceinline__ void load_row(f32x4 (&v)[N], const float* row, int g)
 #pragma unroll
   for (int t = 0; t < N; ++t) v[t] = ld4(row + 16 * t + 4 * g);
 }
-template <int N>
+template <int N, bool STREAM = false>
 __device__ __forceinline__ void store_row(float* row, const f32x4 (&v)[N], int ntiles, int g) {
 #pragma unroll
   for (int t = 0; t < N; ++t)
-    if (t < ntiles) st4(row + 16 * t + 4 * g, v[t]);
+    if (t < ntiles) {
+      if constexpr (STREAM)
+        st4_stream(row + 16 * t + 4 * g, v[t]);
+      else
+        st4(row + 16 * t + 4 * g, v[t]);
+    }
 }
 
 // ---------------------------------------------------------------------------- epilogues
 // Projection of a SWEGNN layer (U, V, O) from [x_s ; x_in] of a node tile; H1T = tiles of
 // the first edge-MLP layer (2F, or F for one-layer MLPs).
-template <int NT, int H1T>
+template <int NT, int H1T, bool STREAM = false>
 __device__ __forceinline__ void np_project_t(const f32x4 (&xs)[NT], const f32x4 (&xin)[NT],
                                              const NpDesc& d, const float* W, size_t n, bool valid,
                                              int lane, int g) {
@@ -201,44 +219,44 @@ __device__ __forceinline__ void np_project_t(const f32x4 (&xs)[NT], const f32x4 
   if (d.a_u >= 0) {
     f32x4 acc[H1T];
     proj<T2, H1T>(in, acc, W + d.a_u, lane);
-    if (valid) store_row<H1T>(d.U + n * (16 * H1T), acc, H1T, g);
+    if (valid) store_row<H1T, STREAM>(d.U + n * (16 * H1T), acc, H1T, g);
   }
   if (d.a_v >= 0) {
     f32x4 acc[H1T];
     proj<T2, H1T>(in, acc, W + d.a_v, lane);
-    if (valid) store_row<H1T>(d.V + n * (16 * H1T), acc, H1T, g);
+    if (valid) store_row<H1T, STREAM>(d.V + n * (16 * H1T), acc, H1T, g);
   }
   if (d.a_o >= 0) {
     f32x4 acc[NT];
     proj<NT, NT>(xin, acc, W + d.a_o, lane);
-    if (valid) store_row<NT>(d.O + n * F, acc, NT, g);
+    if (valid) store_row<NT, STREAM>(d.O + n * F, acc, NT, g);
   }
 }
-template <int NT>
+template <int NT, bool STREAM = false>
 __device__ __forceinline__ void np_project(const f32x4 (&xs)[NT], const f32x4 (&xin)[NT],
                                            const NpDesc& d, const float* W, size_t n, bool valid,
                                            int lane, int g) {
   if (d.h1t == 2 * NT)
-    np_project_t<NT, 2 * NT>(xs, xin, d, W, n, valid, lane, g);
+    np_project_t<NT, 2 * NT, STREAM>(xs, xin, d, W, n, valid, lane, g);
   else
-    np_project_t<NT, NT>(xs, xin, d, W, n, valid, lane, g);
+    np_project_t<NT, NT, STREAM>(xs, xin, d, W, n, valid, lane, g);
 }
 
 // U (or V) = W[:, blocks] [x_s ; x] with H1T output tiles, TIN input tiles.
-template <int TIN, int H1T, int NT>
+template <int TIN, int H1T, int NT, bool STREAM = false>
 __device__ __forceinline__ void side_proj_t(const f32x4 (&in)[TIN], const float* A, float* dst, size_t n,
                                             bool valid, int lane, int g) {
   f32x4 acc[H1T];
   proj<TIN, H1T>(in, acc, A, lane);
-  if (valid) store_row<H1T>(dst + n * (16 * H1T), acc, H1T, g);
+  if (valid) store_row<H1T, STREAM>(dst + n * (16 * H1T), acc, H1T, g);
 }
-template <int TIN, int NT>
+template <int TIN, int NT, bool STREAM = false>
 __device__ __forceinline__ void side_proj(const f32x4 (&in)[TIN], int h1t, const float* A, float* dst,
                                           size_t n, bool valid, int lane, int g) {
   if (h1t == 2 * NT)
-    side_proj_t<TIN, 2 * NT, NT>(in, A, dst, n, valid, lane, g);
+    side_proj_t<TIN, 2 * NT, NT, STREAM>(in, A, dst, n, valid, lane, g);
   else
-    side_proj_t<TIN, NT, NT>(in, A, dst, n, valid, lane, g);
+    side_proj_t<TIN, NT, NT, STREAM>(in, A, dst, n, valid, lane, g);
 }
 
 // Everything an epilogue reads from HBM that does not depend on the tile's result, loaded

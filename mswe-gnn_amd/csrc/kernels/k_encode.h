@@ -10,8 +10,11 @@
 // DEC: the rollout variant that decodes the previous step first (EncodeArgs::dec.on); the
 // other variant keeps the encoders' register budget (four waves per SIMD) for forward mode
 // and the large meshes whose last hops decode.
-template <int NT, int ACT, bool DEC>
+// STREAM (grid-stride launches without DEC, EncodeArgs::stream): the rows go out with
+// streaming stores (k_base.h st4_stream).
+template <int NT, int ACT, bool DEC, bool STREAM = false>
 __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
+  constexpr bool ST = STREAM && !DEC;
   constexpr int F = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
@@ -98,19 +101,19 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncodeArgs a) {
       for (int r = 0; r < 4; ++r) v[r] = (c.with_wl && 4 * g + r == nstat) ? wlv : raw[r];
       const f32x4 in[1] = {v};
       run_mlp<1, NT, NT, ACT>(in, xs, a.stat, Wl, lane, g);
-      if (valid) store_row<NT>(a.xs + (size_t)n * F, xs, NT, g);
+      if (valid) store_row<NT, ST>(a.xs + (size_t)n * F, xs, NT, g);
     }
     MSW_MARK(c, 5);
     if (s == 0) {
       f32x4 xd[NT];
       const f32x4 in[1] = {f32x4{dyn[0], dyn[1], dyn[2], dyn[3]}};
       run_mlp<1, NT, NT, ACT>(in, xd, a.dynm, Wl, lane, g);
-      if (valid && a.xd) store_row<NT>(a.xd + (size_t)n * F, xd, NT, g);
+      if (valid && a.xd) store_row<NT, ST>(a.xd + (size_t)n * F, xd, NT, g);
       MSW_MARK(c, 6);
-      np_project<NT>(xs, xd, a.np0, Wl, n, valid, lane, g);
+      np_project<NT, ST>(xs, xd, a.np0, Wl, n, valid, lane, g);
     }
     MSW_MARK(c, 8);
-    if (a.vu_a[s] >= 0) side_proj<NT, NT>(xs, a.vu_h1t, Wl + a.vu_a[s], a.Vu, n, valid, lane, g);
+    if (a.vu_a[s] >= 0) side_proj<NT, NT, ST>(xs, a.vu_h1t, Wl + a.vu_a[s], a.Vu, n, valid, lane, g);
   }
   MSW_MARK(c, 9);
 }

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(64 * kRowHopWaves) void k_hop_rows(HopArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) res[t] = od[t];
     apply_filter_regs<NT>(res, agg, a.filt_a, wf);
-    if (valid) store_row<NT>(a.out + n * F, res, NT, g);
+    if (valid) store_row<NT, true>(a.out + n * F, res, NT, g);  // streaming (large meshes only)
   }
 }
 

@@ -20,6 +20,7 @@ hipError_t prepare_kernels() {
   const std::pair<const void*, int> fns[] = {
       {(const void*)k_encode<NT, 1, false>, kWaves}, {(const void*)k_encode<NT, -1, false>, kWaves},
       {(const void*)k_encode<NT, 1, true>, kWaves}, {(const void*)k_encode<NT, -1, true>, kWaves},
+      {(const void*)k_encode<NT, 1, false, true>, kWaves}, {(const void*)k_encode<NT, -1, false, true>, kWaves},
       {(const void*)k_edge_hop<NT, 1, false, 0>, kWaves}, {(const void*)k_edge_hop<NT, -1, false, 0>, kWaves},
       {(const void*)k_edge_hop<NT, 1, false, 1>, kWaves}, {(const void*)k_edge_hop<NT, -1, false, 1>, kWaves},
       {(const void*)k_edge_hop<NT, 1, true, 0>, edge_waves<NT, true, 0>()},
@@ -115,6 +116,13 @@ hipError_t launch_encode(const EncodeArgs& a, hipStream_t st) {
   const int n = a.Npad / kRowsPerBlock;
   const dim3 grid(a.max_blocks > 0 && n > a.max_blocks ? a.max_blocks : n), block(kBlock);
   const size_t sh = lds_bytes<NT>(a.lds_floats);
+  if (a.stream && !a.dec.on) {
+    if (a.c.prelu)
+      hipLaunchKernelGGL((k_encode<NT, 1, false, true>), grid, block, sh, st, a);
+    else
+      hipLaunchKernelGGL((k_encode<NT, -1, false, true>), grid, block, sh, st, a);
+    return hipGetLastError();
+  }
   if (a.dec.on) {
     if (a.c.prelu)
       hipLaunchKernelGGL((k_encode<NT, 1, true>), grid, block, sh, st, a);

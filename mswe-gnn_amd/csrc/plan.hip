@@ -1031,6 +1031,10 @@ void set_grid_cap(msw_plan* P, Launch& L) {
       bool coop = P->NT == 4 && (long)(L.enc.Npad / kRowsPerWave) * P->NT <= kEncCoopWaves;
       if (P->kn.enc_coop >= 0) coop = P->NT >= 2 && P->kn.enc_coop != 0;
       L.enc.coop = coop ? P->NT : 0;
+      // grid-stride (more 64-row chunks than resident workgroups) without the decoder: the
+      // encoder's rows (config 5: 1.26 GB per launch) go out as streaming stores
+      L.enc.stream = !L.enc.coop && !L.enc.dec.on && L.enc.max_blocks > 0 &&
+                     L.enc.Npad / kRowsPerBlock > L.enc.max_blocks;
       break;
     }
     case L_EDGE_MLP: {

@@ -780,8 +780,9 @@ def test_build_variant_matches_default_bitwise(variant):
     """A library build variant (build_engine.py --variant=<name>, loaded with MSW_LIB_VARIANT:
     workgroup sizes, wave counts, how the MLP operands are addressed -- speed knobs) == the
     default library bit for bit: a 3-step rollout of the dk15-size mesh with the grid-stride
-    edge hops forced (MSW_EH_LOOP=1, ~4.3 k finest tiles) and one of zenodo4 at F = 64, one
-    child process per library (a process loads one).  Round 4 ran it on the
+    edge hops forced (MSW_EH_LOOP=1, ~4.3 k finest tiles), one of zenodo4 at F = 64 and a
+    2-step rollout of config 5's 1.3 M-node mesh (the grid-stride encoder without the deferred
+    decoder, the row-layout hops), one child process per library (a process loads one).  Round 4 ran it on the
     software-pipelined edge hop (ehpipe8, profiles/r04/ab_eh_pipe_hbm1m.txt, rejected).
     Skipped when no variant is built."""
     import json
@@ -790,7 +791,8 @@ def test_build_variant_matches_default_bitwise(variant):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if not os.path.exists(os.path.join(root, "mswe-gnn_amd", "lib", f"libmswegnn_{variant}.so")):
         pytest.skip(f"build variant {variant} not built")
-    for args in (["--mesh", "dk15", "--T", "3", "--eh-loop"], ["--mesh", "zenodo4", "--T", "3", "--hid", "64"]):
+    for args in (["--mesh", "dk15", "--T", "3", "--eh-loop"], ["--mesh", "zenodo4", "--T", "3", "--hid", "64"],
+                 ["--mesh", "hbm1m", "--T", "2"]):
         res = []
         for v in ("", variant):
             env = {k: x for k, x in os.environ.items() if not k.startswith("MSW_")}

@@ -9,6 +9,7 @@
 #   partfuzz    tests/test_gpu_partition_fuzz.py over a seed range (PART_FUZZ_SEEDS, default 0:200)
 #   trainfuzz   tests/test_gpu_train_fuzz.py over a seed range (TRAIN_FUZZ_SEEDS, default 0:300)
 #   pmc5        HBM bytes per launch of config 5's kernels (FETCH_SIZE / WRITE_SIZE passes)
+#   stream      streaming stores of the large-mesh encoder / row hop: bit-identity, parity, A/B, trace
 #   pytest      pytest -m gpu on the test ids given as args
 #   fuzz        tests/test_gpu_fuzz.py over a wider seed range (FUZZ_SEEDS, default 16:400)
 #   ab          tools/ab.sh with the args (A/B of MSW_* settings on bench.py)
@@ -54,6 +55,17 @@ case $MODE in
     step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1
     step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -d $PWD/$OUT/pmc_write -o run --output-format csv -- python3 bench.py --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 1 --warmup 1 > $OUT/pmc_write.log 2>&1
     python3 tools/pmc_summary.py $OUT/pmc_summary_hbm1m.json $OUT/pmc_fetch $OUT/pmc_write > $OUT/pmc_summary.log 2>&1 ;;
+  stream)  # streaming stores of the large-mesh encoder / row hop + the encoder's input prefetch:
+           # variant bit-identity (nostream = the closing-session kernels), parity, A/B, trace
+    step variants 600 $PYT tests/test_gpu_parity.py -m gpu -k "build_variant or row_layout or coop_encoder" > $OUT/variants.txt 2>&1
+    step fullsize 600 $PYT -m gpu tests/test_gpu_fullsize.py -k config5 > $OUT/fullsize.txt 2>&1
+    step ab_hbm1m 900 bash tools/ab.sh "" "MSW_LIB_VARIANT=nostream" "" "MSW_LIB_VARIANT=nostream" -- --workload hbm1m --no-cpu-baseline --no-roofline-large --steps 3 --warmup 1
+    cp gpurun_out/ab.log $OUT/ab_hbm1m.txt
+    step ab_zenodo4 600 bash tools/ab.sh "" "MSW_LIB_VARIANT=nostream" "" "MSW_LIB_VARIANT=nostream"
+    cp gpurun_out/ab.log $OUT/ab_zenodo4.txt
+    rm -rf $OUT/prof
+    step rocprof 500 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --workload hbm1m --no-roofline-large --steps 3 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+    python3 tools/step_breakdown.py $OUT/prof/run_kernel_trace.csv > $OUT/step_breakdown_hbm1m.txt 2>&1 ;;
   pytest)
     step pytest 900 $PYT -m gpu "$@" > $OUT/pytest.txt 2>&1 ;;
   ab)
@@ -73,7 +85,7 @@ case $MODE in
     step ab_zenodo4 600 bash tools/ab.sh "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv" "" "MSW_LIB_VARIANT=nofastdiv"
     cp gpurun_out/ab.log $OUT/ab_zenodo4.txt ;;
   sq)  # SQ counters of config 5's fused edge MLP + hop, per launch (tools/pmc_generic.py --split-duration)
-    KRE='k_edge_hop'
+    KRE=${SQ_KRE:-k_edge_hop}
     C1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
     C2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
     C3="SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VALU_TRANS_F32 SQ_VALU_MFMA_COEXEC_CYCLES"
